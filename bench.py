@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark of the IPLS gradient-partition aggregation hot path on MI355X.
+
+Metric (BASELINE.json): "aggregated-gradient GB/s (device-resident), 32
+peers x 4M doubles/partition".  Workload = config C of SURVEY.md §8(d): per
+GPU, 16 partitions x 4,194,304-double buckets (count slot included) x 32 peers,
+synthetic splitmix64 counter data generated on the device before timing.
+
+One step = ONE launch of the batched fixed-order reduce over all of the GPU's
+partitions through the C-ABI (ipls_agg_reduce_batch, ZERO start = fresh
+Aggregated_Gradients, Updater.java:115-117 semantics), with every bucket
+already resident in HBM.  Algorithmic bytes per step = P * (K+1) * L * 8
+(read K buckets, write 1 sum).  Multi-GPU: one process per GPU, partitions
+sharded 16 per GPU (`-pa` segments mapped to devices), no data-path
+collective -> weak scaling; value = all ranks' bytes / max-over-ranks time.
+
+Extra JSON objects: `roofline` (dominant kernel, HIP-event time on the
+handle's stream vs 8 TB/s HBM peak; traffic from the committed rocprofv3 PMC
+pass when one matches this workload) and `cpu_baseline` (the reference's
+single-thread Updater decode+fold loop restated in C, oracle/, timed on this
+host on a bounded sample; rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "ipls-java-api_amd"))
+sys.path.insert(0, str(ROOT))
+
+METRIC = "aggregated-gradient GB/s (device-resident), 32 peers×4M doubles/partition"
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (partitions per GPU, bucket length incl. count slot, peers)
+    "B": (16, 1048576, 8),
+    "C": (16, 4194304, 32),
+    "D": (64, 4194304, 32),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
+    ap.add_argument("--be", action="store_true", help="buckets are big-endian IPFS bytes (fused unpack)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-passes", type=int, default=16,
+                    help="CPU baseline sample: passes over one partition's K buckets")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(L: int, K: int, passes: int) -> dict:
+    """Reference Updater loop (Updater.java:162-187 + 115-117, MyIPFSClass.java:
+    444-455) restated in C, ONE thread as the reference's single Updater thread:
+    per bucket a BE getDouble decode into a reused buffer, then the fold."""
+    from oracle import oracle as O
+    be = []
+    for k in range(K):
+        b = O.c_synth_bucket(L, 0, k)
+        be.append(np.frombuffer(b.astype(">f8").tobytes(), dtype=np.uint8).copy())
+    O.c_updater_loop(be, L)                      # warm pages
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        O.c_updater_loop(be, L)
+    dt = time.perf_counter() - t0
+    nbytes = passes * (K + 1) * L * 8
+    return {"value": round(nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} passes x 1 partition x {K} peers x {L} doubles "
+                      f"({nbytes / 1e9:.1f} GB algorithmic, {dt:.1f} s), BE decode + fold, "
+                      f"oracle/ipls_oracle.c ipls_oracle_updater_loop (JDK absent: C restatement)",
+            "host_cpus": os.cpu_count()}
+
+
+def pmc_traffic(workload_key: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass for this
+    workload (profiles/pmc_traffic.json), or None."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        e = d.get(workload_key)
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if not torch.cuda.is_available():
+        sys.exit("bench.py needs an MI355X (no HIP device visible)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+
+    import ipls
+    P, L, K = CONFIGS[args.config]
+    p0 = rank * P                                  # this GPU's -pa segment
+    elem = L + 32                                  # 256-B pad between buckets
+    arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
+    base = (int(arena.data_ptr()) + 255) // 256 * 256
+    rows = []
+    for q in range(P):
+        row = []
+        for k in range(K):
+            b = ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L, big_endian=args.be)
+            ipls.synth_fill(b, p0 + q, k, ipls.SEED)
+            row.append(b)
+        rows.append(row)
+    torch.cuda.synchronize()
+
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=local)
+    stream = torch.cuda.ExternalStream(agg.stream, device=torch.device("cuda", local))
+
+    def step():
+        agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO, big_endian=args.be)
+
+    for _ in range(args.warmup):
+        step()
+    agg.sync()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    agg.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+
+    bytes_step = P * (K + 1) * L * 8
+    total_bytes = bytes_step * args.steps * world
+    value = total_bytes / dt_max / 1e9
+
+    verified = None
+    if not args.no_verify and rank == 0:
+        from oracle import oracle as O   # checker only: the oracle's checksum of the fixed-order sum
+        verified = agg.checksum(0) == O.c_synth_sum_checksum(L, p0, K)
+
+    out = None
+    if rank == 0:
+        achieved = bytes_step / (kern_ms / 1e3) / 1e9
+        wkey = f"{args.config}{'-be' if args.be else ''}"
+        traffic = pmc_traffic(wkey)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 counter buckets generated on device, SURVEY.md 8(d))",
+            "config": {
+                "workload": f"{args.config}: {P} partitions x {L} doubles x {K} peers per GPU"
+                            + (" (big-endian IPFS bytes in, fused bswap)" if args.be else ""),
+                "partitions": P * world, "bucket_len": L, "peers": K,
+                "parallelism": f"partition-sharded x{world} (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "ipls::k_reduce",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_step,
+                "kernel_ms": round(kern_ms, 4),
+            },
+            "verified_checksum_p0": verified,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(L, K, args.cpu_passes)
+        print(json.dumps(out), flush=True)
+    agg.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+/*
+ * ipls_agg.h -- C-ABI of the MI355X-native IPLS gradient-partition aggregator.
+ *
+ * Drop-in boundary for the reference's aggregation path.
+ * The reference has no FFI: its reduce loops are inlined into static-state
+ * Java methods.  Each entry point below replaces the body of one of those
+ * loops; the Java callers keep their signatures and call through the JNI
+ * shim shown in INTEGRATION.md (1:1 mapping, no torch / HIP types here).
+ *
+ * Reference citations are relative to /root/reference/src/main/java/.
+ *
+ * Conventions
+ *  - Every function returns IPLS_OK (0) or a negative IPLS_E_* code and never
+ *    aborts; ipls_agg_last_error() gives the message (Java code catches and
+ *    prints exceptions at the same places, e.g. Updater.java:213-215).
+ *  - The caller owns host buffers for the duration of the call only: a call
+ *    that reads or writes host memory has finished with it when it returns.
+ *  - Calls with only device-resident operands are stream-ordered on the
+ *    handle's HIP stream and may return before the GPU finishes; use
+ *    ipls_agg_sync() before reading device results from another stream.
+ *  - A handle is internally serialised (one mutex): it may be called from
+ *    the Updater thread and the daemon thread concurrently, as the Java code
+ *    does under PeerData.mtx (PeerData.java:27).  Calls on one partition
+ *    take effect in call order -- the reference's arrival order.
+ *  - Arithmetic is IEEE binary64 with no contraction and no reassociation:
+ *    each element is folded over the peers in the order given, starting from
+ *    +0.0 (or from the first bucket), so results are bit-identical to the
+ *    Java loops on the same inputs.
+ */
+#ifndef IPLS_AGG_H
+#define IPLS_AGG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPLS_AGG_ABI_VERSION 1
+
+/* ---- error codes (Java exception the reference would raise) ---- */
+#define IPLS_OK           0
+#define IPLS_E_INVAL     -1  /* bad argument / null handle                         */
+#define IPLS_E_RANGE     -2  /* partition index or length out of range
+                                (ArrayIndexOutOfBoundsException, Updater.java:115) */
+#define IPLS_E_NEGSIZE   -3  /* chunk rule gives a partition of length < 1
+                                (NegativeArraySizeException, IPLS.java:1024,1863)  */
+#define IPLS_E_NOMEM     -4  /* device or pinned-host allocation failed             */
+#define IPLS_E_DEVICE    -5  /* HIP runtime / kernel launch error                   */
+#define IPLS_E_FORMAT    -6  /* malformed frame or byte length
+                                (BufferUnderflowException, MyIPFSClass.java:1444)  */
+#define IPLS_E_NODEV     -7  /* no usable GPU                                       */
+
+/* ---- accumulator targets (PeerData.java:137,144,149,189) ---- */
+#define IPLS_TGT_AGG      0  /* PeerData.Aggregated_Gradients[p]  */
+#define IPLS_TGT_REP      1  /* PeerData.Replicas_Gradients[p]    */
+#define IPLS_TGT_WEIGHTS  2  /* PeerData.Weights[p]               */
+#define IPLS_TGT_WADDR    3  /* PeerData.Weight_Address[p]        */
+
+/* ---- operand kinds ---- */
+#define IPLS_HOST_F64     0  /* host double[] (native byte order)                          */
+#define IPLS_HOST_BE      1  /* host byte[] of big-endian doubles: update_file / GetParameters
+                                format (MyIPFSClass.java:105-116, 444-455); n = #doubles     */
+#define IPLS_HOST_FRAME   2  /* host byte[] pubsub frame after base64 (Marshall_Packet,
+                                MyIPFSClass.java:990-1017); n = frame byte length           */
+#define IPLS_DEV_F64      3  /* device double*                                               */
+#define IPLS_DEV_BE       4  /* device bytes, big-endian doubles, 8-byte aligned             */
+#define IPLS_HOST_BE_CANON 5 /* output only: BE with NaN canonicalised, DataOutputStream
+                                .writeDouble (Middleware.java:164-170)                      */
+
+/* ---- fold start modes ---- */
+#define IPLS_START_ACCUM  0  /* fold into the target's current value (Updater arrival fold)     */
+#define IPLS_START_ZERO   1  /* target = +0.0 first (fresh accumulator, IPLS.java:1888,1268)    */
+#define IPLS_START_FIRST  2  /* target = bucket 0, then fold the rest
+                                (Decentralized_Storage_Receiver.java:240-246)                   */
+
+#define IPLS_ALL_PARTITIONS (-1)
+
+typedef struct ipls_agg ipls_agg;
+
+typedef struct ipls_agg_cfg {
+    int64_t model_size;          /* PeerData._MODEL_SIZE; > 0 selects the reference chunk rule   */
+    int32_t n_partitions;        /* -pa  (Middleware.java:35, PeerData._PARTITIONS)              */
+    int32_t max_peers;           /* -n   (Middleware.java:44); sizes host staging, may be 0       */
+    int32_t partial_aggregation; /* -aggr (Middleware.java:57); informational                     */
+    int32_t secure;              /* PeerData.secure_ipls (PeerData.java:62): /1e12 in the divide  */
+    int32_t device;              /* HIP device ordinal                                           */
+    int32_t flags;               /* reserved, must be 0                                          */
+    int64_t bucket_len;          /* model_size == 0: every partition has this length incl. the
+                                    count slot (synthetic configs, SURVEY.md §8 notation)        */
+} ipls_agg_cfg;
+
+/* ABI version of the loaded library (IPLS_AGG_ABI_VERSION). */
+int ipls_agg_abi_version(void);
+
+/* Allocate the per-partition accumulators on the device, all zero.
+ * Replaces IPLS.init's InitializeWeights() (IPLS.java:1860-1878). */
+int ipls_agg_open(const ipls_agg_cfg *cfg, ipls_agg **out);
+
+/* Free everything.  NULL is accepted. */
+int ipls_agg_close(ipls_agg *h);
+
+/* Message of the last failure on h (h == NULL: last failure of this thread). */
+const char *ipls_agg_last_error(const ipls_agg *h);
+
+/* Partition length incl. the count slot: IPLS.java:1019-1028. */
+int ipls_agg_partition_len(const ipls_agg *h, int p, int64_t *len);
+
+/* Offset of partition p's first value in the flat model (p * chunk). */
+int ipls_agg_partition_offset(const ipls_agg *h, int p, int64_t *off);
+
+/* InitializeWeights(List<Double> Model), IPLS.java:1880-1901: Weights and
+ * Weight_Address get the model values with count slot 0.0; AGG, REP = 0.
+ * src: HOST_F64 / HOST_BE (read_file format, IPLS.java:2000-2008) / DEV_*. */
+int ipls_agg_load_model(ipls_agg *h, const void *src, int64_t n, int src_kind);
+
+/* OrganizeGradients (IPLS.java:1018-1040) for partition p: dst gets
+ * double[L_p] with the count slot 1.0.  dst_kind: HOST_F64, HOST_BE, DEV_F64,
+ * DEV_BE.  n is the length of the flat gradient vector. */
+int ipls_agg_split(ipls_agg *h, const void *flat, int64_t n, int src_kind,
+                   int p, void *dst, int dst_kind);
+
+/* UpdateGradient's own-partition accumulate (IPLS.java:1737-1743):
+ * for every p in owned[0..n_owned): AGG[p] = AGG[p] + OrganizeGradients(flat)[p].
+ * flat == NULL is the "did not train in time" case (Gradients == null): no-op. */
+int ipls_agg_update_gradient(ipls_agg *h, const void *flat, int64_t n, int src_kind,
+                             const int32_t *owned, int n_owned);
+
+/* Updater._Update for one arriving bucket (Updater.java:36-48 REP branch,
+ * 74-137 AGG branches): target[p][i] = target[p][i] + g[i], i < L_p.
+ * n = #doubles (F64/BE kinds) or frame byte length (FRAME kind; the frame's
+ * n field must be >= L_p).  Returns IPLS_E_RANGE when the bucket is shorter
+ * than L_p.  Also Collect_Replicas (IPLS.java:1217-1241) with target REP. */
+int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t n,
+                        int src_kind);
+
+/* Batched fixed-order fold, ONE kernel launch for n_parts partitions:
+ *   for q in [0,n_parts): target[p_first+q] = fold(start_mode; bufs[q*k + 0..k-1])
+ * bufs are device pointers (DEV_F64 or DEV_BE), each at least L_p long.
+ * This is the benchmarked kernel. */
+int ipls_agg_reduce_batch(ipls_agg *h, int p_first, int n_parts,
+                          const void *const *bufs, int k, int src_kind,
+                          int start_mode, int target);
+
+/* AggregatePartition (IPLS.java:1248-1274): W = AGG + REP, Weight_Address = W,
+ * AGG = REP = 0.  p may be IPLS_ALL_PARTITIONS.  Optional host outputs for one
+ * partition: sum_out (the commit_update file bytes, IPLS_Comm.java:27-37 ->
+ * update_file, when sum_kind == HOST_BE; or doubles, HOST_F64) and avg_out
+ * (L_p - 1 averaged values, the GetPartitions divide).  Either may be NULL. */
+int ipls_agg_finalize(ipls_agg *h, int p, void *sum_out, int sum_kind, double *avg_out);
+
+/* Download_Scheduler.cache_partition (Download_Scheduler.java:752-792):
+ * Weight_Address[p] = GetParameters(hash) -- the downloaded updated partition. */
+int ipls_agg_set_weights(ipls_agg *h, int p, const void *src, int64_t n, int src_kind);
+
+/* GetPartitions (IPLS.java:1140-1174): Weights = Weight_Address, then the
+ * flat model with every partition divided by its count slot (count 0.0 ->
+ * values unchanged; secure -> / (1e12 * count)).  out holds model_size
+ * doubles; out_kind HOST_F64, HOST_BE_CANON (Middleware task-3 stream), DEV_F64. */
+int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
+
+/* Copy an accumulator out (tests, replica publish IPLS.java:1423-1431).
+ * dst_kind HOST_F64, HOST_BE, DEV_F64, DEV_BE; n >= L_p. */
+int ipls_agg_read(ipls_agg *h, int p, int target, void *dst, int64_t n, int dst_kind);
+
+/* Zero AGG[p] and REP[p] (IPLS.java:1268-1269); p may be IPLS_ALL_PARTITIONS. */
+int ipls_agg_reset(ipls_agg *h, int p);
+
+/* Device address of an accumulator (for RCCL send/recv of replica partials). */
+int ipls_agg_device_ptr(ipls_agg *h, int p, int target, void **ptr);
+
+/* The handle's HIP stream (hipStream_t as void*) and a host wait on it. */
+void *ipls_agg_stream(ipls_agg *h);
+int ipls_agg_sync(ipls_agg *h);
+
+/* Order-independent checksum of partition p of a target:
+ *   sum_i splitmix64(bits(x_i) + i*0x9E3779B97F4A7C15) mod 2^64
+ * computed on the device (wave DPP + LDS reduction, exact integer sum). */
+int ipls_agg_checksum(ipls_agg *h, int p, int target, uint64_t *out);
+
+/* ---- device utilities (no handle) -- stream may be NULL (default stream) ---- */
+
+/* Fill a device bucket with the synthetic workload of SURVEY.md §8(d):
+ * x_i = (2u-1)*1e-2, u = (splitmix64(seed ^ p<<40 ^ k<<32 ^ i) >> 11) * 2^-53,
+ * x_{L-1} = 1.0 (count slot).  dst_kind DEV_F64 or DEV_BE. */
+int ipls_synth_fill(void *dst, int64_t len, uint64_t seed, int p, int k, int dst_kind,
+                    void *stream);
+
+/* Checksum (as above) of n device doubles (DEV_F64) or BE doubles (DEV_BE). */
+int ipls_checksum_dev(const void *src, int64_t n, int src_kind, uint64_t *out, void *stream);
+
+/* Pubsub frame header parse (MyIPFSClass.java:1437-1446 / 1462-1469).
+ * Returns the number of doubles n, or IPLS_E_FORMAT. */
+int64_t ipls_frame_parse(const uint8_t *frame, int64_t len, int16_t *pid, int32_t *a,
+                         int32_t *b, int64_t *payload_off, int64_t *origin_off);
+
+/* Frame encode (MyIPFSClass.java:990-1017) of n device or host doubles into a
+ * host byte buffer of 14 + 8n + origin_len bytes.  Returns bytes written. */
+int64_t ipls_frame_encode(const double *g, int64_t n, int g_kind, int32_t a, int32_t b,
+                          int16_t pid, const uint8_t *origin, int32_t origin_len,
+                          uint8_t *out, int64_t out_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPLS_AGG_H */

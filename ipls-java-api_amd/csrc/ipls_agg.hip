@@ -1,0 +1,1023 @@
+// ipls_agg.hip -- C-ABI implementation (include/ipls_agg.h) of the MI355X
+// IPLS aggregator.  One handle = one aggregator's PeerData accumulator state
+// on one GPU, one HIP stream, one mutex.
+//
+// Device layout: one arena of doubles per handle holding, for
+// every partition p, three arrays of L_p doubles -- AGG (Aggregated_Gradients,
+// PeerData.java:144), REP (Replicas_Gradients, :137) and W (Weights, :149,
+// which IPLS.java:1141 aliases with Weight_Address, :189) -- each starting on
+// a 256-byte boundary.  Device-side tables (partition descriptors + bucket
+// pointers) are uploaded through a small pinned ring and cached, so a
+// repeated reduce over resident buckets is one kernel launch and nothing else.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/ipls_agg.h"
+#include "ipls_kernels.hpp"
+
+using namespace ipls;
+
+namespace {
+
+thread_local std::string g_tls_err;
+
+constexpr int64_t kAlignElems = 32;  // 256 B
+constexpr int kRingSlots = 4;
+constexpr size_t kStageChunk = 8u << 20;  // host->device staging chunk (bytes)
+
+int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+struct PinnedSlot {
+  void* host = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+
+}  // namespace
+
+struct ipls_agg {
+  std::mutex mu;
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+
+  // geometry
+  int64_t model_size = 0;  // 0 => synthetic geometry
+  int P = 0;
+  int64_t chunk = 0;  // flat stride between partitions
+  int secure = 0;
+  std::vector<int64_t> len, flat_off;
+  int64_t max_len = 0, flat_total = 0;
+
+  // arena
+  double* arena = nullptr;
+  int64_t arena_elems = 0;
+  std::vector<int64_t> agg_off, rep_off, w_off;
+  std::vector<uint8_t> agg_zero, rep_zero;  // "logically +0.0" flags
+
+  // table upload ring (pinned host slots -> device slots)
+  PinnedSlot ring[kRingSlots];
+  void* d_table[kRingSlots] = {};
+  size_t d_table_cap[kRingSlots] = {};
+  int ring_next = 0;
+  std::vector<unsigned char> last_table;  // cache of the last uploaded table
+  int last_slot = -1;
+
+  // staging
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  PinnedSlot stage[2];
+  int stage_next = 0;
+
+  // checksum result
+  unsigned long long* d_sum = nullptr;
+};
+
+namespace {
+
+int fail(ipls_agg* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  g_tls_err = buf;
+  return code;
+}
+
+#define HIP_TRY(h, expr)                                                                \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail((h), e_ == hipErrorOutOfMemory ? IPLS_E_NOMEM : IPLS_E_DEVICE,        \
+                  "%s failed: %s", #expr, hipGetErrorString(e_));                       \
+  } while (0)
+
+int64_t ref_chunk(int64_t m, int p) { return (int64_t)(int32_t)(m / p) + 1; }  // IPLS.java:1019
+
+
+int check_part(ipls_agg* h, int p) {
+  if (p < 0 || p >= h->P) return fail(h, IPLS_E_RANGE, "partition %d out of range [0,%d)", p, h->P);
+  return IPLS_OK;
+}
+
+int64_t target_off(ipls_agg* h, int p, int target) {
+  switch (target) {
+    case IPLS_TGT_AGG: return h->agg_off[p];
+    case IPLS_TGT_REP: return h->rep_off[p];
+    case IPLS_TGT_WEIGHTS:
+    case IPLS_TGT_WADDR: return h->w_off[p];
+    default: return -1;
+  }
+}
+
+uint8_t* zero_flag(ipls_agg* h, int p, int target) {
+  if (target == IPLS_TGT_AGG) return &h->agg_zero[p];
+  if (target == IPLS_TGT_REP) return &h->rep_zero[p];
+  return nullptr;
+}
+
+// Make a logically-zero accumulator physically zero (before anything reads it
+// with ACCUM semantics or hands its address out).
+int materialize(ipls_agg* h, int p, int target) {
+  uint8_t* f = zero_flag(h, p, target);
+  if (f && *f) {
+    HIP_TRY(h, hipMemsetAsync(h->arena + target_off(h, p, target), 0, (size_t)h->len[p] * 8, h->stream));
+    *f = 0;
+  }
+  return IPLS_OK;
+}
+
+int ensure_pinned(ipls_agg* h, PinnedSlot& s, size_t bytes) {
+  if (s.pending) {
+    HIP_TRY(h, hipEventSynchronize(s.ev));
+    s.pending = false;
+  }
+  if (s.cap < bytes) {
+    if (s.host) HIP_TRY(h, hipHostFree(s.host));
+    s.host = nullptr;
+    s.cap = 0;
+    size_t cap = std::max<size_t>(bytes, 64 << 10);
+    HIP_TRY(h, hipHostMalloc(&s.host, cap, hipHostMallocDefault));
+    s.cap = cap;
+  }
+  if (!s.ev) HIP_TRY(h, hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+  return IPLS_OK;
+}
+
+int ensure_scratch(ipls_agg* h, size_t bytes) {
+  if (h->scratch_bytes >= bytes) return IPLS_OK;
+  if (h->d_scratch) {
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    HIP_TRY(h, hipFree(h->d_scratch));
+    h->d_scratch = nullptr;
+    h->scratch_bytes = 0;
+  }
+  size_t cap = (size_t)align_up((int64_t)bytes, 1 << 20);
+  HIP_TRY(h, hipMalloc(&h->d_scratch, cap));
+  h->scratch_bytes = cap;
+  return IPLS_OK;
+}
+
+// Upload a table through the pinned ring; returns its device address.  An
+// identical table to the previous upload is not re-sent.
+int upload_table(ipls_agg* h, const void* data, size_t bytes, void** dev) {
+  if (h->last_slot >= 0 && h->last_table.size() == bytes &&
+      std::memcmp(h->last_table.data(), data, bytes) == 0) {
+    *dev = h->d_table[h->last_slot];
+    return IPLS_OK;
+  }
+  const int s = h->ring_next;
+  h->ring_next = (s + 1) % kRingSlots;
+  int rc = ensure_pinned(h, h->ring[s], bytes);
+  if (rc) return rc;
+  if (h->d_table_cap[s] < bytes) {
+    if (h->d_table[s]) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      HIP_TRY(h, hipFree(h->d_table[s]));
+    }
+    h->d_table[s] = nullptr;
+    h->d_table_cap[s] = 0;
+    size_t cap = std::max<size_t>(bytes, 64 << 10);
+    HIP_TRY(h, hipMalloc(&h->d_table[s], cap));
+    h->d_table_cap[s] = cap;
+  }
+  std::memcpy(h->ring[s].host, data, bytes);
+  HIP_TRY(h, hipMemcpyAsync(h->d_table[s], h->ring[s].host, bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(h, hipEventRecord(h->ring[s].ev, h->stream));
+  h->ring[s].pending = true;
+  h->last_table.assign((const unsigned char*)data, (const unsigned char*)data + bytes);
+  h->last_slot = s;
+  *dev = h->d_table[s];
+  return IPLS_OK;
+}
+
+// Copy `bytes` of host memory to device `dst` through the pinned double buffer.
+// The caller's buffer is no longer referenced when this returns.
+int stage_h2d(ipls_agg* h, void* dst, const void* src, size_t bytes) {
+  const char* s = (const char*)src;
+  char* d = (char*)dst;
+  for (size_t off = 0; off < bytes; off += kStageChunk) {
+    const size_t n = std::min(kStageChunk, bytes - off);
+    PinnedSlot& slot = h->stage[h->stage_next];
+    h->stage_next ^= 1;
+    int rc = ensure_pinned(h, slot, kStageChunk);
+    if (rc) return rc;
+    std::memcpy(slot.host, s + off, n);
+    HIP_TRY(h, hipMemcpyAsync(d + off, slot.host, n, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(slot.ev, h->stream));
+    slot.pending = true;
+  }
+  return IPLS_OK;
+}
+
+int d2h(ipls_agg* h, void* dst, const void* src, size_t bytes) {
+  HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
+}
+
+unsigned blocks_for(int64_t n, int64_t per_block) { return (unsigned)((n + per_block - 1) / per_block); }
+
+// ---- kernel dispatch: k_reduce ----
+constexpr int kG = 8;  // peers in flight per lane
+constexpr int kR = 1;  // 16-byte vectors per lane per tile
+
+template <bool BE_IN, bool BE_OUT, int START>
+void launch_reduce_t(dim3 grid, hipStream_t st, const unsigned long long* const* bufs,
+                     const PartDesc* parts, unsigned long long* dst, int k, int tpp) {
+  hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kG, kR, true>), grid, dim3(kBlock), 0, st,
+                     bufs, parts, dst, k, tpp);
+}
+
+void launch_reduce(bool be_in, int start, dim3 grid, hipStream_t st,
+                   const unsigned long long* const* bufs, const PartDesc* parts,
+                   unsigned long long* dst, int k, int tpp) {
+  if (be_in) {
+    if (start == kZero) launch_reduce_t<true, false, kZero>(grid, st, bufs, parts, dst, k, tpp);
+    else if (start == kFirst) launch_reduce_t<true, false, kFirst>(grid, st, bufs, parts, dst, k, tpp);
+    else launch_reduce_t<true, false, kAccum>(grid, st, bufs, parts, dst, k, tpp);
+  } else {
+    if (start == kZero) launch_reduce_t<false, false, kZero>(grid, st, bufs, parts, dst, k, tpp);
+    else if (start == kFirst) launch_reduce_t<false, false, kFirst>(grid, st, bufs, parts, dst, k, tpp);
+    else launch_reduce_t<false, false, kAccum>(grid, st, bufs, parts, dst, k, tpp);
+  }
+}
+
+void launch_reduce_scalar(bool be_in, int start, dim3 grid, hipStream_t st,
+                          const unsigned long long* const* bufs, const PartDesc* parts,
+                          unsigned long long* dst, int k, int tpp, int64_t tile) {
+#define RS(BE, ST) hipLaunchKernelGGL((k_reduce_scalar<BE, ST>), grid, dim3(kBlock), 0, st, bufs, parts, dst, k, tpp, tile)
+  if (be_in) {
+    if (start == kZero) RS(true, kZero); else if (start == kFirst) RS(true, kFirst); else RS(true, kAccum);
+  } else {
+    if (start == kZero) RS(false, kZero); else if (start == kFirst) RS(false, kFirst); else RS(false, kAccum);
+  }
+#undef RS
+}
+
+// Core of accumulate / reduce_batch: all pointers device-resident.
+int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k,
+               bool be_in, int start_mode, int target) {
+  if (k <= 0) {
+    if (start_mode == IPLS_START_ZERO) {
+      for (int q = 0; q < n_parts; ++q) {
+        uint8_t* f = zero_flag(h, p_first + q, target);
+        if (f) *f = 1;
+        else HIP_TRY(h, hipMemsetAsync(h->arena + target_off(h, p_first + q, target), 0,
+                                       (size_t)h->len[p_first + q] * 8, h->stream));
+      }
+    }
+    return IPLS_OK;  // ACCUM / FIRST with no bucket: nothing to fold
+  }
+  // Resolve start mode per the logically-zero flags: an ACCUM into a +0.0
+  // accumulator is exactly a ZERO-start fold.
+  int start = start_mode;
+  if (start_mode == IPLS_START_ACCUM) {
+    int nz = 0;
+    for (int q = 0; q < n_parts; ++q) {
+      uint8_t* f = zero_flag(h, p_first + q, target);
+      nz += (f && *f) ? 1 : 0;
+    }
+    if (nz == n_parts) start = IPLS_START_ZERO;
+    else if (nz) {
+      for (int q = 0; q < n_parts; ++q) {
+        int rc = materialize(h, p_first + q, target);
+        if (rc) return rc;
+      }
+    }
+  }
+  bool aligned16 = true;
+  int64_t maxL = 0;
+  for (int q = 0; q < n_parts; ++q) maxL = std::max(maxL, h->len[p_first + q]);
+  for (int64_t i = 0; i < (int64_t)n_parts * k; ++i) {
+    if (!bufs[i]) return fail(h, IPLS_E_INVAL, "bucket pointer %lld is NULL", (long long)i);
+    uintptr_t a = (uintptr_t)bufs[i];
+    if (a & 7) return fail(h, IPLS_E_INVAL, "bucket %lld not 8-byte aligned", (long long)i);
+    if (a & 15) aligned16 = false;
+  }
+  // table = [PartDesc x n_parts][ptr x n_parts*k]
+  const size_t desc_bytes = sizeof(PartDesc) * n_parts;
+  const size_t bytes = desc_bytes + sizeof(void*) * (size_t)n_parts * k;
+  std::vector<unsigned char> tbl(bytes);
+  PartDesc* pd = (PartDesc*)tbl.data();
+  for (int q = 0; q < n_parts; ++q) {
+    pd[q].len = h->len[p_first + q];
+    pd[q].dst_off = target_off(h, p_first + q, target);
+  }
+  std::memcpy(tbl.data() + desc_bytes, bufs, sizeof(void*) * (size_t)n_parts * k);
+  void* dtab = nullptr;
+  int rc = upload_table(h, tbl.data(), bytes, &dtab);
+  if (rc) return rc;
+  const PartDesc* dparts = (const PartDesc*)dtab;
+  auto dbufs = (const unsigned long long* const*)((char*)dtab + desc_bytes);
+  auto dst = (unsigned long long*)h->arena;
+  if (aligned16) {
+    const int64_t tile = (int64_t)kBlock * 2 * kR;
+    const int tpp = (int)((maxL + tile - 1) / tile);
+    launch_reduce(be_in, start, dim3((unsigned)tpp * n_parts), h->stream, dbufs, dparts, dst, k, tpp);
+  } else {
+    const int64_t tile = (int64_t)kBlock * 8;
+    const int tpp = (int)((maxL + tile - 1) / tile);
+    launch_reduce_scalar(be_in, start, dim3((unsigned)tpp * n_parts), h->stream, dbufs, dparts, dst, k,
+                         tpp, tile);
+  }
+  HIP_TRY(h, hipGetLastError());
+  for (int q = 0; q < n_parts; ++q) {
+    uint8_t* f = zero_flag(h, p_first + q, target);
+    if (f) *f = 0;
+  }
+  return IPLS_OK;
+}
+
+int partition_geometry(const ipls_agg_cfg* c, std::vector<int64_t>& len, std::vector<int64_t>& off,
+                       int64_t& chunk, std::string& why) {
+  const int P = c->n_partitions;
+  len.resize(P);
+  off.resize(P);
+  if (c->model_size > 0) {
+    chunk = ref_chunk(c->model_size, P);
+    for (int i = 0; i < P; ++i) {
+      // IPLS.java:1023-1028 / 1862-1872
+      int64_t L = ((int64_t)(i + 1) * chunk > c->model_size) ? c->model_size - (int64_t)i * chunk + 1
+                                                             : chunk + 1;
+      if (L < 1) {
+        // L < 0: new double[L] throws NegativeArraySizeException (IPLS.java:1863);
+        // L == 0: the count-slot store overruns the array (IPLS.java:1894, 1033).
+        char b[160];
+        snprintf(b, sizeof b, "partition %d length %lld < 1 (%s)", i, (long long)L,
+                 L < 0 ? "NegativeArraySizeException, IPLS.java:1863"
+                       : "ArrayIndexOutOfBoundsException, IPLS.java:1894");
+        why = b;
+        return L < 0 ? IPLS_E_NEGSIZE : IPLS_E_RANGE;
+      }
+      len[i] = L;
+      off[i] = (int64_t)i * chunk;
+    }
+  } else {
+    if (c->bucket_len < 1) {
+      why = "bucket_len must be >= 1 when model_size == 0";
+      return IPLS_E_INVAL;
+    }
+    chunk = c->bucket_len - 1;
+    for (int i = 0; i < P; ++i) {
+      len[i] = c->bucket_len;
+      off[i] = (int64_t)i * chunk;
+    }
+  }
+  return IPLS_OK;
+}
+
+int host_decode_count(int kind, int64_t n, int64_t L, ipls_agg* h) {
+  if (n < L) return fail(h, IPLS_E_RANGE, "bucket of %lld doubles shorter than partition length %lld", (long long)n, (long long)L);
+  (void)kind;
+  return IPLS_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int ipls_agg_abi_version(void) { return IPLS_AGG_ABI_VERSION; }
+
+const char* ipls_agg_last_error(const ipls_agg* h) {
+  if (h) return h->err.c_str();
+  return g_tls_err.c_str();
+}
+
+int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
+  if (!cfg || !out) return fail(nullptr, IPLS_E_INVAL, "null cfg/out");
+  *out = nullptr;
+  if (cfg->n_partitions <= 0) return fail(nullptr, IPLS_E_INVAL, "n_partitions must be > 0 (-pa)");
+  if (cfg->model_size < 0) return fail(nullptr, IPLS_E_INVAL, "model_size < 0");
+  if (cfg->flags != 0) return fail(nullptr, IPLS_E_INVAL, "cfg.flags must be 0");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(nullptr, IPLS_E_NODEV, "no HIP device available");
+  if (cfg->device < 0 || cfg->device >= ndev)
+    return fail(nullptr, IPLS_E_NODEV, "device %d not in [0,%d)", cfg->device, ndev);
+
+  ipls_agg* h = new (std::nothrow) ipls_agg();
+  if (!h) return fail(nullptr, IPLS_E_NOMEM, "host allocation failed");
+  std::string why;
+  int rc = partition_geometry(cfg, h->len, h->flat_off, h->chunk, why);
+  if (rc) {
+    delete h;
+    return fail(nullptr, rc, "%s", why.c_str());
+  }
+  h->device = cfg->device;
+  h->model_size = cfg->model_size;
+  h->P = cfg->n_partitions;
+  h->secure = cfg->secure;
+  h->agg_off.resize(h->P);
+  h->rep_off.resize(h->P);
+  h->w_off.resize(h->P);
+  h->agg_zero.assign(h->P, 1);
+  h->rep_zero.assign(h->P, 1);
+  int64_t cur = 0;
+  for (int p = 0; p < h->P; ++p) {
+    h->max_len = std::max(h->max_len, h->len[p]);
+    h->flat_total = std::max(h->flat_total, h->flat_off[p] + h->len[p] - 1);
+    h->agg_off[p] = cur; cur = align_up(cur + h->len[p], kAlignElems);
+    h->rep_off[p] = cur; cur = align_up(cur + h->len[p], kAlignElems);
+    h->w_off[p] = cur;   cur = align_up(cur + h->len[p], kAlignElems);
+  }
+  h->arena_elems = cur;
+  auto cleanup = [&](int code) {
+    ipls_agg_close(h);
+    return code;
+  };
+  if (hipSetDevice(h->device) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipSetDevice(%d) failed", h->device));
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipStreamCreate failed"));
+  if (hipMalloc(&h->arena, (size_t)h->arena_elems * 8) != hipSuccess) {
+    h->arena = nullptr;
+    return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc of %lld-byte arena failed", (long long)h->arena_elems * 8));
+  }
+  if (hipMalloc(&h->d_sum, 64) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc failed"));
+  // InitializeWeights(): new double[] -> all zero (IPLS.java:1860-1878).
+  if (hipMemsetAsync(h->arena, 0, (size_t)h->arena_elems * 8, h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess)
+    return cleanup(fail(nullptr, IPLS_E_DEVICE, "arena clear failed"));
+  *out = h;
+  return IPLS_OK;
+}
+
+int ipls_agg_close(ipls_agg* h) {
+  if (!h) return IPLS_OK;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (auto& s : h->ring) {
+    if (s.host) hipHostFree(s.host);
+    if (s.ev) hipEventDestroy(s.ev);
+  }
+  for (auto& s : h->stage) {
+    if (s.host) hipHostFree(s.host);
+    if (s.ev) hipEventDestroy(s.ev);
+  }
+  for (void* d : h->d_table)
+    if (d) hipFree(d);
+  if (h->d_scratch) hipFree(h->d_scratch);
+  if (h->d_sum) hipFree(h->d_sum);
+  if (h->arena) hipFree(h->arena);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return IPLS_OK;
+}
+
+int ipls_agg_partition_len(const ipls_agg* hc, int p, int64_t* L) {
+  ipls_agg* h = const_cast<ipls_agg*>(hc);
+  if (!h || !L) return fail(h, IPLS_E_INVAL, "null argument");
+  if (int rc = check_part(h, p)) return rc;
+  *L = h->len[p];
+  return IPLS_OK;
+}
+
+int ipls_agg_partition_offset(const ipls_agg* hc, int p, int64_t* off) {
+  ipls_agg* h = const_cast<ipls_agg*>(hc);
+  if (!h || !off) return fail(h, IPLS_E_INVAL, "null argument");
+  if (int rc = check_part(h, p)) return rc;
+  *off = h->flat_off[p];
+  return IPLS_OK;
+}
+
+void* ipls_agg_stream(ipls_agg* h) { return h ? (void*)h->stream : nullptr; }
+
+int ipls_agg_sync(ipls_agg* h) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
+}
+
+int ipls_agg_reduce_batch(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k,
+                          int src_kind, int start_mode, int target) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_parts <= 0 || p_first < 0 || p_first + n_parts > h->P)
+    return fail(h, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, h->P);
+  if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE)
+    return fail(h, IPLS_E_INVAL, "reduce_batch takes device buckets (DEV_F64/DEV_BE)");
+  if (start_mode < IPLS_START_ACCUM || start_mode > IPLS_START_FIRST) return fail(h, IPLS_E_INVAL, "bad start mode");
+  if (target_off(h, 0, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (k < 0 || (k > 0 && !bufs)) return fail(h, IPLS_E_INVAL, "bad bucket list");
+  HIP_TRY(h, hipSetDevice(h->device));
+  return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, target);
+}
+
+int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (!src) return IPLS_OK;  // Gradient == null: the Updater loops do nothing (Updater.java:115)
+  HIP_TRY(h, hipSetDevice(h->device));
+  const int64_t L = h->len[p];
+  const void* dptr = nullptr;
+  bool be = false;
+  switch (src_kind) {
+    case IPLS_DEV_F64:
+    case IPLS_DEV_BE:
+      if (int rc = host_decode_count(src_kind, n, L, h)) return rc;
+      dptr = src;
+      be = src_kind == IPLS_DEV_BE;
+      break;
+    case IPLS_HOST_F64:
+    case IPLS_HOST_BE: {
+      if (int rc = host_decode_count(src_kind, n, L, h)) return rc;
+      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+      if (int rc = stage_h2d(h, h->d_scratch, src, (size_t)L * 8)) return rc;
+      dptr = h->d_scratch;
+      be = src_kind == IPLS_HOST_BE;
+      break;
+    }
+    case IPLS_HOST_FRAME: {
+      int16_t pid;
+      int32_t a, b;
+      int64_t poff, ooff;
+      int64_t nd = ipls_frame_parse((const uint8_t*)src, n, &pid, &a, &b, &poff, &ooff);
+      if (nd < 0) return fail(h, IPLS_E_FORMAT, "malformed frame (BufferUnderflowException)");
+      if (nd == 0) return IPLS_OK;  // arr_len == 0 -> Gradients = null (MyIPFSClass.java:1449-1451)
+      if (int rc = host_decode_count(src_kind, nd, L, h)) return rc;
+      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+      // The payload starts at byte 14 (unaligned); staging realigns it.
+      if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
+      dptr = h->d_scratch;
+      be = true;
+      break;
+    }
+    default:
+      return fail(h, IPLS_E_INVAL, "bad src_kind %d", src_kind);
+  }
+  const void* bl[1] = {dptr};
+  return reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target);
+}
+
+int ipls_agg_reset(ipls_agg* h, int p) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (p == IPLS_ALL_PARTITIONS) {
+    for (int q = 0; q < h->P; ++q) h->agg_zero[q] = h->rep_zero[q] = 1;
+    return IPLS_OK;
+  }
+  if (int rc = check_part(h, p)) return rc;
+  h->agg_zero[p] = h->rep_zero[p] = 1;
+  return IPLS_OK;
+}
+
+int ipls_agg_device_ptr(ipls_agg* h, int p, int target, void** ptr) {
+  if (!h || !ptr) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (int rc = materialize(h, p, target)) return rc;
+  *ptr = h->arena + target_off(h, p, target);
+  return IPLS_OK;
+}
+
+int ipls_agg_read(ipls_agg* h, int p, int target, void* dst, int64_t n, int dst_kind) {
+  if (!h || !dst) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  const int64_t L = h->len[p];
+  if (n < L) return fail(h, IPLS_E_RANGE, "output of %lld < partition length %lld", (long long)n, (long long)L);
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (int rc = materialize(h, p, target)) return rc;
+  const double* srcd = h->arena + target_off(h, p, target);
+  switch (dst_kind) {
+    case IPLS_HOST_F64:
+      return d2h(h, dst, srcd, (size_t)L * 8);
+    case IPLS_DEV_F64:
+      HIP_TRY(h, hipMemcpyAsync(dst, srcd, (size_t)L * 8, hipMemcpyDeviceToDevice, h->stream));
+      return IPLS_OK;
+    case IPLS_DEV_BE:
+      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
+                         h->stream, (const unsigned long long*)srcd, (unsigned long long*)dst, L);
+      HIP_TRY(h, hipGetLastError());
+      return IPLS_OK;
+    case IPLS_HOST_BE: {
+      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
+                         h->stream, (const unsigned long long*)srcd, (unsigned long long*)h->d_scratch, L);
+      HIP_TRY(h, hipGetLastError());
+      return d2h(h, dst, h->d_scratch, (size_t)L * 8);
+    }
+    default:
+      return fail(h, IPLS_E_INVAL, "bad dst_kind %d", dst_kind);
+  }
+}
+
+int ipls_agg_checksum(ipls_agg* h, int p, int target, uint64_t* out) {
+  if (!h || !out) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (int rc = materialize(h, p, target)) return rc;
+  HIP_TRY(h, hipMemsetAsync(h->d_sum, 0, 8, h->stream));
+  const int64_t L = h->len[p];
+  hipLaunchKernelGGL(k_checksum<false>, dim3(std::max(1u, std::min<unsigned>(blocks_for(L, kBlock * 8), 2048))),
+                     dim3(kBlock), 0, h->stream,
+                     (const unsigned long long*)(h->arena + target_off(h, p, target)), L, h->d_sum);
+  HIP_TRY(h, hipGetLastError());
+  unsigned long long v = 0;
+  if (int rc = d2h(h, &v, h->d_sum, 8)) return rc;
+  *out = v;
+  return IPLS_OK;
+}
+
+int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* avg_out) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  int p0 = p, np = 1;
+  if (p == IPLS_ALL_PARTITIONS) {
+    p0 = 0;
+    np = h->P;
+    if (sum_out || avg_out) return fail(h, IPLS_E_INVAL, "host outputs need a single partition");
+  } else if (int rc = check_part(h, p)) {
+    return rc;
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  // AGG logically zero but present as an operand -> make it physical.
+  bool rep_zero_all = true;
+  for (int q = p0; q < p0 + np; ++q) {
+    if (int rc = materialize(h, q, IPLS_TGT_AGG)) return rc;
+    rep_zero_all = rep_zero_all && h->rep_zero[q];
+  }
+  if (!rep_zero_all)
+    for (int q = p0; q < p0 + np; ++q)
+      if (int rc = materialize(h, q, IPLS_TGT_REP)) return rc;
+  std::vector<FinDesc> fd(np);
+  int64_t maxL = 0;
+  for (int q = 0; q < np; ++q) {
+    fd[q] = FinDesc{h->len[p0 + q], h->agg_off[p0 + q], h->rep_off[p0 + q], h->w_off[p0 + q]};
+    maxL = std::max(maxL, fd[q].len);
+  }
+  void* dtab = nullptr;
+  if (int rc = upload_table(h, fd.data(), fd.size() * sizeof(FinDesc), &dtab)) return rc;
+  const int64_t tile = (int64_t)kBlock * 8;
+  const int tpp = (int)((maxL + tile - 1) / tile);
+  // AGG/REP are left in place and flagged logically zero (IPLS.java:1268-1269
+  // zeroes them; the next fold starts from +0.0 without reading them).
+  if (rep_zero_all)
+    hipLaunchKernelGGL((k_finalize<true, false>), dim3((unsigned)tpp * np), dim3(kBlock), 0, h->stream,
+                       (const FinDesc*)dtab, h->arena, tpp);
+  else
+    hipLaunchKernelGGL((k_finalize<false, false>), dim3((unsigned)tpp * np), dim3(kBlock), 0, h->stream,
+                       (const FinDesc*)dtab, h->arena, tpp);
+  HIP_TRY(h, hipGetLastError());
+  for (int q = p0; q < p0 + np; ++q) h->agg_zero[q] = h->rep_zero[q] = 1;
+
+  if (np == 1 && (sum_out || avg_out)) {
+    const int64_t L = h->len[p0];
+    const double* w = h->arena + h->w_off[p0];
+    if (sum_out) {
+      if (sum_kind == IPLS_HOST_F64) {
+        if (int rc = d2h(h, sum_out, w, (size_t)L * 8)) return rc;
+      } else if (sum_kind == IPLS_HOST_BE) {
+        if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+        hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
+                           h->stream, (const unsigned long long*)w, (unsigned long long*)h->d_scratch, L);
+        HIP_TRY(h, hipGetLastError());
+        if (int rc = d2h(h, sum_out, h->d_scratch, (size_t)L * 8)) return rc;
+      } else {
+        return fail(h, IPLS_E_INVAL, "sum_kind must be HOST_F64 or HOST_BE");
+      }
+    }
+    if (avg_out && L > 1) {
+      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+      DivDesc dd{L, h->w_off[p0], 0};
+      void* dt2 = nullptr;
+      if (int rc = upload_table(h, &dd, sizeof dd, &dt2)) return rc;
+      const int tp = (int)((L - 1 + tile - 1) / tile);
+      if (h->secure)
+        hipLaunchKernelGGL((k_divide<false, true>), dim3((unsigned)tp), dim3(kBlock), 0, h->stream,
+                           (const DivDesc*)dt2, (const double*)h->arena, (unsigned long long*)h->d_scratch, tp);
+      else
+        hipLaunchKernelGGL((k_divide<false, false>), dim3((unsigned)tp), dim3(kBlock), 0, h->stream,
+                           (const DivDesc*)dt2, (const double*)h->arena, (unsigned long long*)h->d_scratch, tp);
+      HIP_TRY(h, hipGetLastError());
+      if (int rc = d2h(h, avg_out, h->d_scratch, (size_t)(L - 1) * 8)) return rc;
+    }
+  }
+  return IPLS_OK;
+}
+
+int ipls_agg_set_weights(ipls_agg* h, int p, const void* src, int64_t n, int src_kind) {
+  if (!h || !src) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  const int64_t L = h->len[p];
+  // GetParameters(hash, arr) writes data.length/8 values (MyIPFSClass.java:449-452);
+  // more than arr.length -> ArrayIndexOutOfBoundsException.
+  if (n > L) return fail(h, IPLS_E_RANGE, "downloaded partition of %lld doubles > length %lld", (long long)n, (long long)L);
+  if (n <= 0) return IPLS_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  double* w = h->arena + h->w_off[p];
+  switch (src_kind) {
+    case IPLS_HOST_F64:
+      return stage_h2d(h, w, src, (size_t)n * 8);
+    case IPLS_HOST_BE: {
+      if (int rc = ensure_scratch(h, (size_t)n * 8)) return rc;
+      if (int rc = stage_h2d(h, h->d_scratch, src, (size_t)n * 8)) return rc;
+      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)), dim3(kBlock), 0,
+                         h->stream, (const unsigned long long*)h->d_scratch, (unsigned long long*)w, n);
+      HIP_TRY(h, hipGetLastError());
+      return IPLS_OK;
+    }
+    case IPLS_DEV_F64:
+      HIP_TRY(h, hipMemcpyAsync(w, src, (size_t)n * 8, hipMemcpyDeviceToDevice, h->stream));
+      return IPLS_OK;
+    case IPLS_DEV_BE:
+      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)), dim3(kBlock), 0,
+                         h->stream, (const unsigned long long*)src, (unsigned long long*)w, n);
+      HIP_TRY(h, hipGetLastError());
+      return IPLS_OK;
+    default:
+      return fail(h, IPLS_E_INVAL, "bad src_kind %d", src_kind);
+  }
+}
+
+// Bring a flat vector of n doubles (host or device, native or BE) onto the
+// device; returns a device pointer and whether it is big-endian.
+static int flat_to_device(ipls_agg* h, const void* flat, int64_t n, int kind, const unsigned long long** d,
+                          bool* be) {
+  switch (kind) {
+    case IPLS_DEV_F64:
+    case IPLS_DEV_BE:
+      *d = (const unsigned long long*)flat;
+      *be = kind == IPLS_DEV_BE;
+      return IPLS_OK;
+    case IPLS_HOST_F64:
+    case IPLS_HOST_BE:
+      if (int rc = ensure_scratch(h, (size_t)std::max<int64_t>(n, 1) * 8)) return rc;
+      if (n > 0)
+        if (int rc = stage_h2d(h, h->d_scratch, flat, (size_t)n * 8)) return rc;
+      *d = (const unsigned long long*)h->d_scratch;
+      *be = kind == IPLS_HOST_BE;
+      return IPLS_OK;
+    default:
+      return fail(h, IPLS_E_INVAL, "bad flat kind %d", kind);
+  }
+}
+
+int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {
+  if (!h || !src) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n < h->flat_total)
+    return fail(h, IPLS_E_RANGE, "model of %lld values < model size %lld", (long long)n, (long long)h->flat_total);
+  HIP_TRY(h, hipSetDevice(h->device));
+  const unsigned long long* d;
+  bool be;
+  if (int rc = flat_to_device(h, src, h->flat_total, src_kind, &d, &be)) return rc;
+  for (int p = 0; p < h->P; ++p) {
+    const int64_t L = h->len[p];
+    // IPLS.java:1883-1895: values for j < min((i+1)c, M), count slot 0.0
+    if (be)
+      hipLaunchKernelGGL(k_load_model<true>, dim3(blocks_for(L, kBlock)), dim3(kBlock), 0, h->stream, d,
+                         h->flat_off[p], L - 1, L, h->arena + h->w_off[p]);
+    else
+      hipLaunchKernelGGL(k_load_model<false>, dim3(blocks_for(L, kBlock)), dim3(kBlock), 0, h->stream, d,
+                         h->flat_off[p], L - 1, L, h->arena + h->w_off[p]);
+    HIP_TRY(h, hipGetLastError());
+    h->agg_zero[p] = h->rep_zero[p] = 1;
+  }
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
+}
+
+// OrganizeGradients bounds for partition p of a flat vector of n values.
+static int split_bounds(ipls_agg* h, int p, int64_t n, int64_t* ncopy) {
+  const int64_t lo = h->flat_off[p];
+  const int64_t hi = std::min(lo + h->chunk, n);
+  const int64_t nc = std::max<int64_t>(0, hi - lo);
+  if (nc > h->len[p] - 1)
+    return fail(h, IPLS_E_RANGE, "gradient vector of %lld values overruns partition %d (ArrayIndexOutOfBounds, IPLS.java:1030)",
+                (long long)n, p);
+  *ncopy = nc;
+  return IPLS_OK;
+}
+
+int ipls_agg_split(ipls_agg* h, const void* flat, int64_t n, int src_kind, int p, void* dst, int dst_kind) {
+  if (!h || !flat || !dst) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  int64_t ncopy;
+  if (int rc = split_bounds(h, p, n, &ncopy)) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  const int64_t L = h->len[p];
+  const unsigned long long* d;
+  bool be_in;
+  // only the partition's own slice is needed on the device
+  const int64_t lo = h->flat_off[p];
+  if (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE) {
+    if (int rc = ensure_scratch(h, (size_t)(2 * L + 2) * 8)) return rc;
+    if (ncopy > 0)
+      if (int rc = stage_h2d(h, h->d_scratch, (const char*)flat + lo * 8, (size_t)ncopy * 8)) return rc;
+    d = (const unsigned long long*)h->d_scratch;
+    be_in = src_kind == IPLS_HOST_BE;
+  } else if (src_kind == IPLS_DEV_F64 || src_kind == IPLS_DEV_BE) {
+    d = (const unsigned long long*)flat + lo;
+    be_in = src_kind == IPLS_DEV_BE;
+    if (int rc = ensure_scratch(h, (size_t)(L + 1) * 8)) return rc;
+  } else {
+    return fail(h, IPLS_E_INVAL, "bad src_kind %d", src_kind);
+  }
+  const bool host_out = dst_kind == IPLS_HOST_F64 || dst_kind == IPLS_HOST_BE;
+  const bool be_out = dst_kind == IPLS_HOST_BE || dst_kind == IPLS_DEV_BE;
+  if (!host_out && dst_kind != IPLS_DEV_F64 && dst_kind != IPLS_DEV_BE)
+    return fail(h, IPLS_E_INVAL, "bad dst_kind %d", dst_kind);
+  unsigned long long* out = host_out ? (unsigned long long*)((char*)h->d_scratch + (size_t)(L + 1) * 8)
+                                     : (unsigned long long*)dst;
+  if (host_out && src_kind != IPLS_HOST_F64 && src_kind != IPLS_HOST_BE)
+    out = (unsigned long long*)h->d_scratch;
+  const dim3 g(blocks_for(L, kBlock));
+#define SPL(BI, BO) hipLaunchKernelGGL((k_split<BI, BO, 0>), g, dim3(kBlock), 0, h->stream, d, (int64_t)0, ncopy, L, out)
+  if (be_in) { if (be_out) SPL(true, true); else SPL(true, false); }
+  else { if (be_out) SPL(false, true); else SPL(false, false); }
+#undef SPL
+  HIP_TRY(h, hipGetLastError());
+  if (host_out) return d2h(h, dst, out, (size_t)L * 8);
+  return IPLS_OK;
+}
+
+int ipls_agg_update_gradient(ipls_agg* h, const void* flat, int64_t n, int src_kind, const int32_t* owned,
+                             int n_owned) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  if (!flat) return IPLS_OK;  // Gradients == null (IPLS.java:1708-1713, 1738 `&& Gradients != null`)
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_owned < 0 || (n_owned > 0 && !owned)) return fail(h, IPLS_E_INVAL, "bad owned list");
+  // OrganizeGradients splits every partition before anything is accumulated
+  // (IPLS.java:1709), so a length error leaves the accumulators untouched.
+  std::vector<int64_t> nc(h->P);
+  for (int p = 0; p < h->P; ++p)
+    if (int rc = split_bounds(h, p, n, &nc[p])) return rc;
+  for (int i = 0; i < n_owned; ++i)
+    if (int rc = check_part(h, owned[i])) return rc;
+  if (n_owned == 0) return IPLS_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  const unsigned long long* d;
+  bool be;
+  if (int rc = flat_to_device(h, flat, std::min(n, h->flat_total), src_kind, &d, &be)) return rc;
+  for (int i = 0; i < n_owned; ++i) {
+    const int p = owned[i];
+    const int64_t L = h->len[p];
+    unsigned long long* acc = (unsigned long long*)(h->arena + h->agg_off[p]);
+    const bool zero = h->agg_zero[p];
+    const dim3 g(blocks_for(L, kBlock));
+    // Logically-zero accumulator: write +0.0 + v (== fold into zeros).
+    if (zero) HIP_TRY(h, hipMemsetAsync(acc, 0, (size_t)L * 8, h->stream));
+    if (be)
+      hipLaunchKernelGGL((k_split<true, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p], nc[p], L, acc);
+    else
+      hipLaunchKernelGGL((k_split<false, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p], nc[p], L, acc);
+    HIP_TRY(h, hipGetLastError());
+    h->agg_zero[p] = 0;
+  }
+  return IPLS_OK;
+}
+
+int ipls_agg_get_partitions(ipls_agg* h, void* out, int64_t n, int out_kind) {
+  if (!h || !out) return fail(h, IPLS_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lk(h->mu);
+  const int64_t M = h->flat_total;
+  if (n < M) return fail(h, IPLS_E_RANGE, "output of %lld < model size %lld", (long long)n, (long long)M);
+  if (out_kind != IPLS_HOST_F64 && out_kind != IPLS_HOST_BE_CANON && out_kind != IPLS_DEV_F64)
+    return fail(h, IPLS_E_INVAL, "bad out_kind %d", out_kind);
+  HIP_TRY(h, hipSetDevice(h->device));
+  unsigned long long* d_out;
+  if (out_kind == IPLS_DEV_F64) {
+    d_out = (unsigned long long*)out;
+  } else {
+    if (int rc = ensure_scratch(h, (size_t)std::max<int64_t>(M, 1) * 8)) return rc;
+    d_out = (unsigned long long*)h->d_scratch;
+  }
+  std::vector<DivDesc> dd(h->P);
+  int64_t maxn = 0;
+  for (int p = 0; p < h->P; ++p) {
+    dd[p] = DivDesc{h->len[p], h->w_off[p], h->flat_off[p]};
+    maxn = std::max(maxn, h->len[p] - 1);
+  }
+  if (maxn > 0) {
+    void* dtab = nullptr;
+    if (int rc = upload_table(h, dd.data(), dd.size() * sizeof(DivDesc), &dtab)) return rc;
+    const int64_t tile = (int64_t)kBlock * 8;
+    const int tpp = (int)((maxn + tile - 1) / tile);
+    const dim3 g((unsigned)tpp * h->P);
+    const bool be = out_kind == IPLS_HOST_BE_CANON;
+#define DIV(B, S) hipLaunchKernelGGL((k_divide<B, S>), g, dim3(kBlock), 0, h->stream, (const DivDesc*)dtab, (const double*)h->arena, d_out, tpp)
+    if (be) { if (h->secure) DIV(true, true); else DIV(true, false); }
+    else { if (h->secure) DIV(false, true); else DIV(false, false); }
+#undef DIV
+    HIP_TRY(h, hipGetLastError());
+  }
+  if (out_kind == IPLS_DEV_F64) return IPLS_OK;
+  return d2h(h, out, d_out, (size_t)M * 8);
+}
+
+// ---- device utilities ----
+int ipls_synth_fill(void* dst, int64_t len, uint64_t seed, int p, int k, int dst_kind, void* stream) {
+  if (!dst || len < 0) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  if (len == 0) return IPLS_OK;
+  const unsigned long long key = seed ^ ((unsigned long long)(uint32_t)p << 40) ^ ((unsigned long long)(uint32_t)k << 32);
+  const dim3 g(std::min<unsigned>(blocks_for(len, kBlock * 4), 8192));
+  if (dst_kind == IPLS_DEV_BE)
+    hipLaunchKernelGGL(k_synth<true>, g, dim3(kBlock), 0, (hipStream_t)stream, (unsigned long long*)dst, len, key);
+  else if (dst_kind == IPLS_DEV_F64)
+    hipLaunchKernelGGL(k_synth<false>, g, dim3(kBlock), 0, (hipStream_t)stream, (unsigned long long*)dst, len, key);
+  else
+    return fail(nullptr, IPLS_E_INVAL, "dst_kind must be DEV_F64 or DEV_BE");
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(nullptr, IPLS_E_DEVICE, "k_synth launch: %s", hipGetErrorString(e));
+  return IPLS_OK;
+}
+
+int ipls_checksum_dev(const void* src, int64_t n, int src_kind, uint64_t* out, void* stream) {
+  if (!src || !out || n < 0) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  unsigned long long* d = nullptr;
+  if (hipMallocAsync((void**)&d, 8, st) != hipSuccess) return fail(nullptr, IPLS_E_NOMEM, "hipMallocAsync failed");
+  hipMemsetAsync(d, 0, 8, st);
+  const dim3 g(std::max(1u, std::min<unsigned>(blocks_for(n, kBlock * 8), 2048)));
+  if (src_kind == IPLS_DEV_BE)
+    hipLaunchKernelGGL(k_checksum<true>, g, dim3(kBlock), 0, st, (const unsigned long long*)src, n, d);
+  else
+    hipLaunchKernelGGL(k_checksum<false>, g, dim3(kBlock), 0, st, (const unsigned long long*)src, n, d);
+  unsigned long long v = 0;
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFreeAsync(d, st);
+  if (e != hipSuccess) return fail(nullptr, IPLS_E_DEVICE, "checksum: %s", hipGetErrorString(e));
+  *out = v;
+  return IPLS_OK;
+}
+
+static uint32_t rd_be32(const uint8_t* b) {
+  return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+}
+
+int64_t ipls_frame_parse(const uint8_t* frame, int64_t len, int16_t* pid, int32_t* a, int32_t* b,
+                         int64_t* payload_off, int64_t* origin_off) {
+  if (!frame || len < 14) return fail(nullptr, IPLS_E_FORMAT, "frame shorter than its 14-byte header");
+  const int16_t pd = (int16_t)(((uint16_t)frame[0] << 8) | frame[1]);
+  const int32_t n = (int32_t)rd_be32(frame + 2);
+  if (n < 0 || 14 + 8 * (int64_t)n > len)
+    return fail(nullptr, IPLS_E_FORMAT, "frame declares %d doubles but holds %lld bytes", n, (long long)len);
+  if (pid) *pid = pd;
+  if (a) *a = (int32_t)rd_be32(frame + 6);
+  if (b) *b = (int32_t)rd_be32(frame + 10);
+  if (payload_off) *payload_off = 14;
+  if (origin_off) *origin_off = 14 + 8 * (int64_t)n;
+  return n;
+}
+
+int64_t ipls_frame_encode(const double* g, int64_t n, int g_kind, int32_t a, int32_t b, int16_t pid,
+                          const uint8_t* origin, int32_t origin_len, uint8_t* out, int64_t out_cap) {
+  if (n < 0 || n > INT32_MAX || origin_len < 0 || !out || (n > 0 && !g) || (origin_len > 0 && !origin))
+    return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  const int64_t total = 14 + 8 * n + origin_len;
+  if (out_cap < total) return fail(nullptr, IPLS_E_RANGE, "frame needs %lld bytes", (long long)total);
+  out[0] = (uint8_t)((uint16_t)pid >> 8);
+  out[1] = (uint8_t)pid;
+  const uint32_t hv[3] = {(uint32_t)n, (uint32_t)a, (uint32_t)b};
+  for (int f = 0; f < 3; ++f)
+    for (int i = 0; i < 4; ++i) out[2 + 4 * f + i] = (uint8_t)(hv[f] >> (24 - 8 * i));
+  if (n > 0) {
+    std::vector<double> tmp;
+    const double* src = g;
+    if (g_kind == IPLS_DEV_F64) {
+      tmp.resize(n);
+      if (hipMemcpy(tmp.data(), g, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(nullptr, IPLS_E_DEVICE, "frame encode D2H failed");
+      src = tmp.data();
+    } else if (g_kind != IPLS_HOST_F64) {
+      return fail(nullptr, IPLS_E_INVAL, "g_kind must be HOST_F64 or DEV_F64");
+    }
+    for (int64_t i = 0; i < n; ++i) {  // putDouble(14 + 8i, g[i]) -- raw bits, BE
+      uint64_t v;
+      std::memcpy(&v, &src[i], 8);
+      v = __builtin_bswap64(v);
+      std::memcpy(out + 14 + 8 * i, &v, 8);
+    }
+  }
+  if (origin_len) std::memcpy(out + 14 + 8 * n, origin, (size_t)origin_len);
+  return total;
+}
+
+}  // extern "C"

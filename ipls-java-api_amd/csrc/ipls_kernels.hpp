@@ -1,0 +1,409 @@
+// ipls_kernels.hpp -- gfx950 (CDNA4) HIP kernels of the IPLS aggregation path.
+//
+// Design:
+//  * The hot kernel is a fixed-order elementwise fold over K peer buckets.
+//    Each lane owns 16 contiguous bytes (2 doubles) per step and walks the
+//    peers in order, so every element is ((+0.0 + b0) + b1) + ... exactly as
+//    Updater.java:115-117 / IPLS.java:1740 compute it.  No shuffle or tree
+//    reduction touches the peer axis: that would reassociate the sum and
+//    break bit parity (SURVEY.md §7 "Order vs. shuffles").
+//  * Memory-level parallelism comes from issuing the loads of G peers
+//    (G x 16 B per lane) before folding them; bucket base pointers are
+//    wave-uniform (scalar loads from a device table).
+//  * Wavefront DPP reductions + LDS staging are used where the reduction is
+//    order-free: the integer checksum kernel (exact, any association).
+//  * Compiled with -ffp-contract=off; double division is the IEEE-correct
+//    v_div_scale/v_div_fmas/v_div_fixup sequence (no fast-math).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ipls {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+
+constexpr int kBlock = 256;
+
+enum Start : int { kAccum = 0, kZero = 1, kFirst = 2 };
+
+struct PartDesc {
+  int64_t len;      // L_p incl. count slot
+  int64_t dst_off;  // offset (doubles) of the target array in the arena
+};
+
+// Global-address-space views.  Bucket pointers come from a device table, so
+// the compiler cannot infer their address space and would emit flat_load with
+// a vmcnt(0)+lgkmcnt(0) wait after EVERY load (fully serialised).  Casting to
+// addrspace(1) gives global_load and counted vmcnt waits.
+#define IPLS_GLOBAL __attribute__((address_space(1)))
+typedef const IPLS_GLOBAL u2* gcu2;
+typedef IPLS_GLOBAL u2* gu2;
+typedef const IPLS_GLOBAL unsigned long long* gcu64;
+typedef IPLS_GLOBAL unsigned long long* gu64;
+
+// NOTE: never __builtin_bit_cast(double, v.y) on an ext_vector element: hipcc
+// (ROCm 7.2) lowers it to element 0 (measured in the ISA).  Copy the element
+// to a scalar first, or bit_cast the whole vector.
+__device__ __forceinline__ double be_to_f64(unsigned long long v) {
+  return __builtin_bit_cast(double, __builtin_bswap64(v));
+}
+__device__ __forceinline__ unsigned long long f64_to_be(double v) {
+  return __builtin_bswap64(__builtin_bit_cast(unsigned long long, v));
+}
+
+template <bool NT>
+__device__ __forceinline__ u2 ld16(const unsigned long long* p) {
+  if constexpr (NT) return __builtin_nontemporal_load((gcu2)p);
+  else return *(gcu2)p;
+}
+__device__ __forceinline__ unsigned long long ld8(const unsigned long long* p) { return *(gcu64)p; }
+__device__ __forceinline__ void st8(unsigned long long* p, unsigned long long v) { *(gu64)p = v; }
+
+template <bool BE>
+__device__ __forceinline__ d2 decode2(u2 raw) {
+  if constexpr (BE) {
+    const unsigned long long a = raw.x, b = raw.y;
+    u2 s;
+    s.x = __builtin_bswap64(a);
+    s.y = __builtin_bswap64(b);
+    return __builtin_bit_cast(d2, s);
+  } else {
+    return __builtin_bit_cast(d2, raw);
+  }
+}
+template <bool BE>
+__device__ __forceinline__ u2 encode2(d2 v) {
+  u2 raw = __builtin_bit_cast(u2, v);
+  if constexpr (BE) {
+    const unsigned long long a = raw.x, b = raw.y;
+    raw.x = __builtin_bswap64(a);
+    raw.y = __builtin_bswap64(b);
+  }
+  return raw;
+}
+template <bool BE>
+__device__ __forceinline__ double decode1(unsigned long long raw) {
+  if constexpr (BE) return be_to_f64(raw);
+  else return __builtin_bit_cast(double, raw);
+}
+
+// ---------------------------------------------------------------------------
+// k_reduce: target[q] = fold(start; bufs[q*k + 0..k-1]) for the partitions of
+// one batch.  Grid = n_parts * tiles_per_part blocks of 256 lanes; a tile is
+// 256 * 2 * R doubles.  Full tiles take the vector path; the one partial tile
+// per partition takes a scalar path (odd lengths, e.g. ETHModel's 147,869).
+//   BE_IN  : buckets hold big-endian doubles (IPFS file bytes) -> bswap fused
+//   BE_OUT : write the sum as big-endian bytes (update_file), else doubles
+//   G      : peers whose loads are in flight together per lane
+//   R      : 16-byte vectors per lane per tile
+//   NT     : non-temporal loads (each byte is read exactly once)
+// ---------------------------------------------------------------------------
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT>
+__global__ __launch_bounds__(kBlock) void k_reduce(
+    const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
+    unsigned long long* __restrict__ dst_base, int k, int tiles_per_part) {
+  constexpr int64_t kTile = (int64_t)kBlock * 2 * R;
+  const int q = blockIdx.x / tiles_per_part;
+  const int t = blockIdx.x - q * tiles_per_part;
+  const int64_t L = parts[q].len;
+  const int64_t base = (int64_t)t * kTile;
+  if (base >= L) return;
+  unsigned long long* __restrict__ dst = dst_base + parts[q].dst_off;
+  const unsigned long long* const* __restrict__ pb = bufs + (size_t)q * k;
+  const int tid = threadIdx.x;
+  const int j0 = (START == kFirst) ? 1 : 0;
+
+  if (base + kTile <= L) {
+    // ---------------- vector path: R x 16 B per lane ----------------
+    int64_t off[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * kBlock + tid);
+
+    d2 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (START == kZero) {
+        acc[r] = d2{0.0, 0.0};
+      } else if constexpr (START == kFirst) {
+        acc[r] = decode2<BE_IN>(ld16<NT>(pb[0] + off[r]));
+      } else {  // kAccum: the target holds native doubles (or BE if BE_OUT)
+        acc[r] = decode2<BE_OUT>(ld16<false>(dst + off[r]));
+      }
+    }
+    int j = j0;
+    for (; j + G <= k; j += G) {
+      u2 v[G][R];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const unsigned long long* __restrict__ src = pb[j + g];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[g][r] = ld16<NT>(src + off[r]);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          d2 x = decode2<BE_IN>(v[g][r]);
+          acc[r].x = acc[r].x + x.x;
+          acc[r].y = acc[r].y + x.y;
+        }
+      }
+    }
+    for (; j < k; ++j) {
+      const unsigned long long* __restrict__ src = pb[j];
+      u2 v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = ld16<NT>(src + off[r]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        d2 x = decode2<BE_IN>(v[r]);
+        acc[r].x = acc[r].x + x.x;
+        acc[r].y = acc[r].y + x.y;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
+  } else {
+    // ---------------- scalar path: the partial last tile ----------------
+    const int64_t end = L;
+    for (int64_t i = base + tid; i < end; i += kBlock) {
+      double acc;
+      if constexpr (START == kZero) acc = 0.0;
+      else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + i));
+      else acc = decode1<BE_OUT>(ld8(dst + i));
+      for (int jj = j0; jj < k; ++jj) acc = acc + decode1<BE_IN>(ld8(pb[jj] + i));
+      st8(dst + i, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
+    }
+  }
+}
+
+// Same fold for buckets that are only 8-byte aligned (e.g. a device view into
+// a frame payload): one double per lane per step.
+template <bool BE_IN, int START>
+__global__ __launch_bounds__(kBlock) void k_reduce_scalar(
+    const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
+    unsigned long long* __restrict__ dst_base, int k, int tiles_per_part, int64_t tile) {
+  const int q = blockIdx.x / tiles_per_part;
+  const int t = blockIdx.x - q * tiles_per_part;
+  const int64_t L = parts[q].len;
+  const int64_t base = (int64_t)t * tile;
+  if (base >= L) return;
+  unsigned long long* __restrict__ dst = dst_base + parts[q].dst_off;
+  const unsigned long long* const* __restrict__ pb = bufs + (size_t)q * k;
+  const int64_t end = (base + tile < L) ? base + tile : L;
+  const int j0 = (START == kFirst) ? 1 : 0;
+  for (int64_t i = base + threadIdx.x; i < end; i += kBlock) {
+    double acc;
+    if constexpr (START == kZero) acc = 0.0;
+    else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + i));
+    else acc = __builtin_bit_cast(double, ld8(dst + i));
+    for (int j = j0; j < k; ++j) acc = acc + decode1<BE_IN>(ld8(pb[j] + i));
+    st8(dst + i, __builtin_bit_cast(unsigned long long, acc));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_finalize: AggregatePartition (IPLS.java:1255-1270) over a batch.
+//   W[i] = AGG[i] + REP[i]  (REP_ZERO: AGG[i] + 0.0 without reading REP)
+//   Weight_Address is the same array as Weights (IPLS.java:1141 aliases them).
+//   AGG/REP are zeroed unless the host marks them "logically zero" instead.
+// ---------------------------------------------------------------------------
+struct FinDesc {
+  int64_t len;
+  int64_t agg_off, rep_off, w_off;
+};
+
+template <bool REP_ZERO, bool ZERO_ACC>
+__global__ __launch_bounds__(kBlock) void k_finalize(const FinDesc* __restrict__ parts,
+                                                     double* __restrict__ arena,
+                                                     int tiles_per_part) {
+  constexpr int64_t kTile = (int64_t)kBlock * 8;
+  const int q = blockIdx.x / tiles_per_part;
+  const int t = blockIdx.x - q * tiles_per_part;
+  const FinDesc d = parts[q];
+  const int64_t base = (int64_t)t * kTile;
+  if (base >= d.len) return;
+  const int64_t end = (base + kTile < d.len) ? base + kTile : d.len;
+  double* agg = arena + d.agg_off;
+  double* rep = arena + d.rep_off;
+  double* w = arena + d.w_off;
+  for (int64_t i = base + threadIdx.x; i < end; i += kBlock) {
+    const double a = agg[i];
+    const double r = REP_ZERO ? 0.0 : rep[i];
+    w[i] = a + r;
+    if constexpr (ZERO_ACC) {
+      agg[i] = 0.0;
+      if constexpr (!REP_ZERO) rep[i] = 0.0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_divide: GetPartitions (IPLS.java:1159-1174) -> flat model.
+//   out[m] = cnt == 0.0 ? W[p][j] : W[p][j] / cnt      (secure: / (1e12*cnt))
+//   m = p*chunk + j.  OUT_BE writes DataOutputStream.writeDouble bytes
+//   (big-endian, NaN canonicalised, Middleware.java:164-170).
+// ---------------------------------------------------------------------------
+struct DivDesc {
+  int64_t len;    // L_p
+  int64_t w_off;  // arena offset of Weights[p]
+  int64_t out_off;
+};
+
+template <bool OUT_BE, bool SECURE>
+__global__ __launch_bounds__(kBlock) void k_divide(const DivDesc* __restrict__ parts,
+                                                   const double* __restrict__ arena,
+                                                   unsigned long long* __restrict__ out,
+                                                   int tiles_per_part) {
+  constexpr int64_t kTile = (int64_t)kBlock * 8;
+  const int q = blockIdx.x / tiles_per_part;
+  const int t = blockIdx.x - q * tiles_per_part;
+  const DivDesc d = parts[q];
+  const int64_t n = d.len - 1;
+  const int64_t base = (int64_t)t * kTile;
+  if (base >= n) return;
+  const int64_t end = (base + kTile < n) ? base + kTile : n;
+  const double* w = arena + d.w_off;
+  const double cnt = w[d.len - 1];
+  // Math.pow(10,12) * W[last] (IPLS.java:1167): 1e12 is exact, product rounded once.
+  const double den = SECURE ? 1e12 * cnt : cnt;
+  for (int64_t i = base + threadIdx.x; i < end; i += kBlock) {
+    const double x = w[i];
+    const double y = (cnt == 0.0) ? x : x / den;
+    unsigned long long bits = __builtin_bit_cast(unsigned long long, y);
+    if constexpr (OUT_BE) {
+      if (y != y) bits = 0x7ff8000000000000ULL;
+      bits = __builtin_bswap64(bits);
+    }
+    out[d.out_off + i] = bits;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_split: OrganizeGradients (IPLS.java:1018-1040) for one partition:
+//   dst[j] = flat[p*chunk + j] for j < min(chunk, n - p*chunk) (guarded),
+//   dst[stop] = 1.0, rest 0.0.  Optional fused fold into an accumulator
+//   (UpdateGradient own-accumulate, IPLS.java:1737-1743).
+// ---------------------------------------------------------------------------
+template <bool BE_IN, bool BE_OUT, bool FOLD>
+__global__ __launch_bounds__(kBlock) void k_split(const unsigned long long* __restrict__ flat,
+                                                  int64_t lo, int64_t ncopy, int64_t L,
+                                                  unsigned long long* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= L) return;
+  double v;
+  if (i < ncopy) v = decode1<BE_IN>(flat[lo + i]);
+  else if (i == ncopy) v = 1.0;
+  else v = 0.0;
+  if constexpr (FOLD) {
+    const double a = __builtin_bit_cast(double, dst[i]);
+    dst[i] = __builtin_bit_cast(unsigned long long, a + v);
+  } else {
+    dst[i] = BE_OUT ? f64_to_be(v) : __builtin_bit_cast(unsigned long long, v);
+  }
+}
+
+// Layout conversion between native and big-endian doubles (pack / unpack).
+__global__ __launch_bounds__(kBlock) void k_bswap64(const unsigned long long* __restrict__ in,
+                                                    unsigned long long* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock)
+    out[i] = __builtin_bswap64(in[i]);
+}
+
+// Strided model load (InitializeWeights(List<Double>), IPLS.java:1880-1901):
+// dst[j] = flat[lo + j] for j < ncopy, dst[L-1] = 0.0.
+template <bool BE_IN>
+__global__ __launch_bounds__(kBlock) void k_load_model(const unsigned long long* __restrict__ flat,
+                                                       int64_t lo, int64_t ncopy, int64_t L,
+                                                       double* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= L) return;
+  dst[i] = (i < ncopy) ? decode1<BE_IN>(flat[lo + i]) : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic workload and checksum.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long v) {
+  unsigned long long z = v + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+template <bool BE_OUT>
+__global__ __launch_bounds__(kBlock) void k_synth(unsigned long long* __restrict__ dst, int64_t L,
+                                                  unsigned long long key) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < L;
+       i += (int64_t)gridDim.x * kBlock) {
+    double x;
+    if (i == L - 1) {
+      x = 1.0;
+    } else {
+      const double u = (double)(splitmix64(key ^ (unsigned long long)i) >> 11) * 0x1.0p-53;
+      double tt = 2.0 * u;
+      tt = tt - 1.0;
+      x = tt * 1e-2;
+    }
+    dst[i] = BE_OUT ? f64_to_be(x) : __builtin_bit_cast(unsigned long long, x);
+  }
+}
+
+// 64-bit wave sum with DPP row shifts + row broadcasts (gfx9 DPP controls):
+// inclusive scan inside each 16-lane row, then row_bcast:15 / row_bcast:31
+// carry the row totals up; lane 63 ends with the wave total.  The sum is an
+// exact integer (mod 2^64), so association does not matter here.
+__device__ __forceinline__ unsigned long long dpp_shift(unsigned long long v, int ctrl_id) {
+  const int lo = (int)(unsigned)v, hi = (int)(unsigned)(v >> 32);
+  int rl, rh;
+  switch (ctrl_id) {
+    case 0: rl = __builtin_amdgcn_update_dpp(0, lo, 0x111, 0xF, 0xF, true);
+            rh = __builtin_amdgcn_update_dpp(0, hi, 0x111, 0xF, 0xF, true); break;  // row_shr:1
+    case 1: rl = __builtin_amdgcn_update_dpp(0, lo, 0x112, 0xF, 0xF, true);
+            rh = __builtin_amdgcn_update_dpp(0, hi, 0x112, 0xF, 0xF, true); break;  // row_shr:2
+    case 2: rl = __builtin_amdgcn_update_dpp(0, lo, 0x114, 0xF, 0xF, true);
+            rh = __builtin_amdgcn_update_dpp(0, hi, 0x114, 0xF, 0xF, true); break;  // row_shr:4
+    case 3: rl = __builtin_amdgcn_update_dpp(0, lo, 0x118, 0xF, 0xF, true);
+            rh = __builtin_amdgcn_update_dpp(0, hi, 0x118, 0xF, 0xF, true); break;  // row_shr:8
+    case 4: rl = __builtin_amdgcn_update_dpp(0, lo, 0x142, 0xA, 0xF, false);
+            rh = __builtin_amdgcn_update_dpp(0, hi, 0x142, 0xA, 0xF, false); break; // row_bcast:15
+    default: rl = __builtin_amdgcn_update_dpp(0, lo, 0x143, 0xC, 0xF, false);
+             rh = __builtin_amdgcn_update_dpp(0, hi, 0x143, 0xC, 0xF, false); break; // row_bcast:31
+  }
+  return ((unsigned long long)(unsigned)rh << 32) | (unsigned)rl;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) v += dpp_shift(v, c);
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, 63);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+template <bool BE_IN>
+__global__ __launch_bounds__(kBlock) void k_checksum(const unsigned long long* __restrict__ x,
+                                                     int64_t n, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long lds[kBlock / 64];
+  unsigned long long s = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    unsigned long long b = BE_IN ? __builtin_bswap64(x[i]) : x[i];
+    s += splitmix64(b + (unsigned long long)i * 0x9E3779B97F4A7C15ULL);
+  }
+  s = wave_sum_u64(s);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += lds[w];
+    atomicAdd(out, t);
+  }
+}
+
+}  // namespace ipls

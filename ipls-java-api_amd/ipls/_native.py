@@ -1,0 +1,121 @@
+"""ctypes binding of libipls_agg.so (include/ipls_agg.h).
+
+This is the Python twin of the JNI shim in INTEGRATION.md: one Python call
+per C entry point, plain pointers and sizes.  There is no fallback: if the
+library is missing or a call fails, an exception is raised (the product path
+never computes on the CPU).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # ipls-java-api_amd/
+LIB_PATH = Path(os.environ.get("IPLS_AGG_LIB", PKG_ROOT / "lib" / "libipls_agg.so"))
+HEADER = PKG_ROOT.parent / "include" / "ipls_agg.h"
+
+# ---- constants (mirrors include/ipls_agg.h) ----
+IPLS_OK = 0
+IPLS_E_INVAL, IPLS_E_RANGE, IPLS_E_NEGSIZE, IPLS_E_NOMEM = -1, -2, -3, -4
+IPLS_E_DEVICE, IPLS_E_FORMAT, IPLS_E_NODEV = -5, -6, -7
+
+TGT_AGG, TGT_REP, TGT_WEIGHTS, TGT_WADDR = 0, 1, 2, 3
+HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON = 0, 1, 2, 3, 4, 5
+START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
+ALL_PARTITIONS = -1
+
+ERROR_NAMES = {
+    IPLS_E_INVAL: "IllegalArgument",
+    IPLS_E_RANGE: "ArrayIndexOutOfBounds",
+    IPLS_E_NEGSIZE: "NegativeArraySize",
+    IPLS_E_NOMEM: "OutOfMemory",
+    IPLS_E_DEVICE: "DeviceError",
+    IPLS_E_FORMAT: "BufferUnderflow",
+    IPLS_E_NODEV: "NoDevice",
+}
+
+
+class IplsError(RuntimeError):
+    """A negative return code from the C-ABI (the Java exception it stands for
+    is in ``java_name``)."""
+
+    def __init__(self, code: int, msg: str):
+        self.code = code
+        self.java_name = ERROR_NAMES.get(code, "Error")
+        super().__init__(f"[{code} {self.java_name}] {msg}")
+
+
+class AggCfg(ctypes.Structure):
+    _fields_ = [
+        ("model_size", ctypes.c_int64),
+        ("n_partitions", ctypes.c_int32),
+        ("max_peers", ctypes.c_int32),
+        ("partial_aggregation", ctypes.c_int32),
+        ("secure", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("bucket_len", ctypes.c_int64),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/ipls_agg.h
+_vp, _i, _i64, _u64, _i32, _i16 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int16
+_P = ctypes.POINTER
+SIGNATURES = {
+    "ipls_agg_abi_version": (_i, []),
+    "ipls_agg_open": (_i, [_P(AggCfg), _P(_vp)]),
+    "ipls_agg_close": (_i, [_vp]),
+    "ipls_agg_last_error": (ctypes.c_char_p, [_vp]),
+    "ipls_agg_partition_len": (_i, [_vp, _i, _P(_i64)]),
+    "ipls_agg_partition_offset": (_i, [_vp, _i, _P(_i64)]),
+    "ipls_agg_load_model": (_i, [_vp, _vp, _i64, _i]),
+    "ipls_agg_split": (_i, [_vp, _vp, _i64, _i, _i, _vp, _i]),
+    "ipls_agg_update_gradient": (_i, [_vp, _vp, _i64, _i, _P(_i32), _i]),
+    "ipls_agg_accumulate": (_i, [_vp, _i, _i, _vp, _i64, _i]),
+    "ipls_agg_reduce_batch": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _i]),
+    "ipls_agg_finalize": (_i, [_vp, _i, _vp, _i, _P(ctypes.c_double)]),
+    "ipls_agg_set_weights": (_i, [_vp, _i, _vp, _i64, _i]),
+    "ipls_agg_get_partitions": (_i, [_vp, _vp, _i64, _i]),
+    "ipls_agg_read": (_i, [_vp, _i, _i, _vp, _i64, _i]),
+    "ipls_agg_reset": (_i, [_vp, _i]),
+    "ipls_agg_device_ptr": (_i, [_vp, _i, _i, _P(_vp)]),
+    "ipls_agg_stream": (_vp, [_vp]),
+    "ipls_agg_sync": (_i, [_vp]),
+    "ipls_agg_checksum": (_i, [_vp, _i, _i, _P(_u64)]),
+    "ipls_synth_fill": (_i, [_vp, _i64, _u64, _i, _i, _i, _vp]),
+    "ipls_checksum_dev": (_i, [_vp, _i64, _i, _P(_u64), _vp]),
+    "ipls_frame_parse": (_i64, [_vp, _i64, _P(_i16), _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
+    "ipls_frame_encode": (_i64, [_vp, _i64, _i, _i32, _i32, _i16, _vp, _i32, _vp, _i64]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the in-tree HIP library.  Raises if it has not been built --
+    there is deliberately no CPU path behind this package."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(
+                f"{LIB_PATH} not found: build it with `make -C ipls-java-api_amd` "
+                "(or __graft_entry__.build()); the aggregator has no CPU fallback")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error(h=None) -> str:
+    msg = lib().ipls_agg_last_error(h)
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int, h=None) -> int:
+    if rc < 0:
+        raise IplsError(rc, last_error(h))
+    return rc

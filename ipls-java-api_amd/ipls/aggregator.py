@@ -1,0 +1,326 @@
+"""Host-side mirror of the reference's aggregation interface, over the C-ABI.
+
+The reference keeps the aggregator state in static maps (PeerData.java:137-189)
+and reduces inside IPLS / Updater methods.  ``Aggregator`` owns the same state
+on one GPU (one ``ipls_agg`` handle) and exposes the reference's operations
+under the reference's names, with the reference's argument meaning:
+
+=====================================  =========================================
+reference (src/main/java/)             here
+=====================================  =========================================
+IPLS.InitializeWeights(List) 1880      ``InitializeWeights(model)``
+IPLS.OrganizeGradients 1018            ``OrganizeGradients(gradients)``
+IPLS.UpdateGradient 1703 (1737-1743)   ``UpdateGradient(gradients, auth_list)``
+Updater._Update 31 (from_clients)      ``Update(gradient, partition, from_clients)``
+IPLS.Collect_Replicas 1217             ``Collect_Replicas(partition, buckets)``
+Decentralized_Storage_Receiver 239     ``Merge(partition, buckets)``
+IPLS.AggregatePartition 1248           ``AggregatePartition(partition)``
+Download_Scheduler.cache_partition 752 ``cache_partition(partition, data)``
+IPLS.GetPartitions 1080 (1140-1174)    ``GetPartitions()``
+=====================================  =========================================
+
+Host buffers are numpy arrays (``float64`` for doubles, ``uint8``/bytes for the
+big-endian IPFS file format and pubsub frames).  Device buffers may be passed
+as ``DeviceBuffer`` (raw pointer + length) -- e.g. ``torch`` CUDA tensors via
+``DeviceBuffer.from_tensor``.  Every call goes to the HIP library; a missing
+library raises at construction.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+
+@dataclass
+class DeviceBuffer:
+    """A device-resident operand: address, element count, big-endian or not."""
+    ptr: int
+    n: int
+    big_endian: bool = False
+
+    @classmethod
+    def from_tensor(cls, t, big_endian: bool = False) -> "DeviceBuffer":
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("need a contiguous device tensor")
+        return cls(int(t.data_ptr()), t.numel() * t.element_size() // 8, big_endian)
+
+    @property
+    def kind(self) -> int:
+        return N.DEV_BE if self.big_endian else N.DEV_F64
+
+
+def _host_operand(x, big_endian: bool):
+    """(pointer, n_doubles, kind, keepalive) for a host operand."""
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(x, dtype=np.uint8)
+        big_endian = True
+    else:
+        a = np.asarray(x)
+    if a.dtype == np.uint8:
+        if not big_endian:
+            raise ValueError("byte buffers carry big-endian doubles (IPFS file format)")
+        a = np.ascontiguousarray(a)
+        return a.ctypes.data, a.nbytes // 8, N.HOST_BE, a
+    if a.dtype.byteorder == ">":
+        a = np.ascontiguousarray(a)
+        return a.ctypes.data, a.size, N.HOST_BE, a
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a.ctypes.data, a.size, N.HOST_F64, a
+
+
+def _operand(x, big_endian: bool = False):
+    if isinstance(x, DeviceBuffer):
+        return x.ptr, x.n, x.kind, x
+    return _host_operand(x, big_endian)
+
+
+class Aggregator:
+    """One aggregator's partition accumulators on one MI355X.
+
+    ``model_size``/``n_partitions`` follow Middleware's ``-pa`` semantics and the
+    reference chunk rule (IPLS.java:1019-1028).  ``bucket_len`` (with
+    model_size=0) selects the synthetic geometry of SURVEY.md §8: every
+    partition ``bucket_len`` doubles including the count slot."""
+
+    def __init__(self, model_size: int = 0, n_partitions: int = 1, *, max_peers: int = 0,
+                 partial_aggregation: int = 0, secure: bool = False, device: int = 0,
+                 bucket_len: int = 0):
+        self._lib = N.lib()
+        cfg = N.AggCfg(model_size=model_size, n_partitions=n_partitions, max_peers=max_peers,
+                       partial_aggregation=partial_aggregation, secure=int(bool(secure)),
+                       device=device, flags=0, bucket_len=bucket_len)
+        h = ctypes.c_void_p()
+        N.check(self._lib.ipls_agg_open(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.model_size = model_size
+        self.n_partitions = n_partitions
+        self.secure = bool(secure)
+        self.device = device
+        self.lengths = [self.partition_len(p) for p in range(n_partitions)]
+        self.offsets = [self.partition_offset(p) for p in range(n_partitions)]
+        self.flat_size = max(o + L - 1 for o, L in zip(self.offsets, self.lengths))
+
+    # ---- lifetime ----
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ipls_agg_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        return N.check(rc, self._h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return int(self._lib.ipls_agg_stream(self._h) or 0)
+
+    def sync(self):
+        self._chk(self._lib.ipls_agg_sync(self._h))
+
+    # ---- geometry (IPLS.java:1019-1028) ----
+    def partition_len(self, p: int) -> int:
+        v = ctypes.c_int64()
+        self._chk(self._lib.ipls_agg_partition_len(self._h, p, ctypes.byref(v)))
+        return v.value
+
+    def partition_offset(self, p: int) -> int:
+        v = ctypes.c_int64()
+        self._chk(self._lib.ipls_agg_partition_offset(self._h, p, ctypes.byref(v)))
+        return v.value
+
+    # ---- reference operations ----
+    def InitializeWeights(self, model, big_endian: bool = False):
+        """IPLS.java:1880-1901 (model = List<Double>, or read_file's raw BE bytes)."""
+        ptr, n, kind, keep = _operand(model, big_endian)
+        self._chk(self._lib.ipls_agg_load_model(self._h, ptr, n, kind))
+
+    def OrganizeGradients(self, gradients, big_endian_out: bool = False) -> dict[int, np.ndarray]:
+        """IPLS.java:1018-1040: {p: double[L_p]} with the count slot 1.0."""
+        ptr, n, kind, keep = _operand(gradients)
+        out = {}
+        for p in range(self.n_partitions):
+            L = self.lengths[p]
+            if big_endian_out:
+                buf = np.empty(8 * L, dtype=np.uint8)
+                dk = N.HOST_BE
+            else:
+                buf = np.empty(L, dtype=np.float64)
+                dk = N.HOST_F64
+            self._chk(self._lib.ipls_agg_split(self._h, ptr, n, kind, p, buf.ctypes.data, dk))
+            out[p] = buf
+        return out
+
+    def UpdateGradient(self, gradients, auth_list):
+        """Own-partition accumulate of IPLS.UpdateGradient (IPLS.java:1737-1743).
+        ``gradients=None`` is the "did not train in time" call (no-op)."""
+        owned = np.ascontiguousarray(np.asarray(list(auth_list), dtype=np.int32))
+        if gradients is None:
+            return
+        ptr, n, kind, keep = _operand(gradients)
+        self._chk(self._lib.ipls_agg_update_gradient(
+            self._h, ptr, n, kind, owned.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(owned)))
+
+    def Update(self, gradient, partition: int, from_clients: bool = True, *, frame: bool = False):
+        """Updater._Update: client buckets fold into Aggregated_Gradients
+        (Updater.java:115-117), replica partial sums into Replicas_Gradients
+        (Updater.java:40-44).  ``gradient`` may be doubles, big-endian file
+        bytes (GetParameters input), a pubsub frame (``frame=True``) or a
+        DeviceBuffer.  ``None`` is a no-op, as in the reference."""
+        if gradient is None:
+            return
+        target = N.TGT_AGG if from_clients else N.TGT_REP
+        if frame:
+            a = np.frombuffer(bytes(gradient), dtype=np.uint8)
+            self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, a.ctypes.data,
+                                                    a.size, N.HOST_FRAME))
+            return
+        ptr, n, kind, keep = _operand(gradient)
+        self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
+
+    def Collect_Replicas(self, partition: int, buckets):
+        """IPLS.java:1217-1241: fold locally downloaded replica buckets into REP."""
+        for b in buckets:
+            self.Update(b, partition, from_clients=False)
+
+    def reduce_batch(self, p_first: int, buckets, *, start_mode: int = N.START_ZERO,
+                     target: int = N.TGT_AGG, big_endian: bool = False):
+        """One launch over len(buckets) partitions; buckets[q] is the list of
+        device pointers (ints or DeviceBuffers) for partition p_first+q."""
+        n_parts = len(buckets)
+        k = len(buckets[0]) if n_parts else 0
+        flat = []
+        for row in buckets:
+            if len(row) != k:
+                raise ValueError("every partition needs the same number of buckets")
+            for b in row:
+                flat.append(b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
+        kind = N.DEV_BE if big_endian else N.DEV_F64
+        self._chk(self._lib.ipls_agg_reduce_batch(self._h, p_first, n_parts, arr, k, kind,
+                                                  start_mode, target))
+
+    def Merge(self, partition: int, buckets, *, big_endian: bool = True, target: int = N.TGT_REP):
+        """Storage-node merge (Decentralized_Storage_Receiver.java:239-247):
+        S = g0; S += g_i -- a FIRST-start fold (it overwrites ``target``, so call
+        it on the storage node's own Aggregator), returned as BE file bytes
+        (the ``<p>_partial_aggregation`` file, :258)."""
+        self.reduce_batch(partition, [list(buckets)], start_mode=N.START_FIRST, target=target,
+                          big_endian=big_endian)
+        return self.read(partition, target, big_endian=True)
+
+    def AggregatePartition(self, partition: int, *, with_sum: bool = False, sum_big_endian: bool = True,
+                           with_average: bool = False):
+        """IPLS.java:1248-1274.  Optionally returns the committed sum (the
+        update_file bytes of IPLS_Comm.commit_update) and the averaged values."""
+        L = self.lengths[partition] if partition >= 0 else 0
+        s = a = None
+        sp, sk = None, N.HOST_F64
+        if with_sum:
+            s = np.empty(8 * L, dtype=np.uint8) if sum_big_endian else np.empty(L)
+            sp, sk = s.ctypes.data, (N.HOST_BE if sum_big_endian else N.HOST_F64)
+        ap = None
+        if with_average:
+            a = np.empty(max(0, L - 1))
+            ap = a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        self._chk(self._lib.ipls_agg_finalize(self._h, partition, sp, sk, ap))
+        return s, a
+
+    def cache_partition(self, partition: int, data):
+        """Download_Scheduler.cache_partition: Weight_Address[p] = GetParameters(hash)."""
+        ptr, n, kind, keep = _operand(data)
+        self._chk(self._lib.ipls_agg_set_weights(self._h, partition, ptr, n, kind))
+
+    def GetPartitions(self, *, wire: bool = False, out=None):
+        """IPLS.java:1140-1174: the averaged flat model.  ``wire=True`` returns
+        the Middleware task-3 byte stream (DataOutputStream.writeDouble)."""
+        n = self.flat_size
+        if isinstance(out, DeviceBuffer):
+            self._chk(self._lib.ipls_agg_get_partitions(self._h, out.ptr, out.n, N.DEV_F64))
+            return out
+        if wire:
+            buf = np.empty(8 * n, dtype=np.uint8)
+            self._chk(self._lib.ipls_agg_get_partitions(self._h, buf.ctypes.data, n, N.HOST_BE_CANON))
+            return buf.tobytes()
+        buf = np.empty(n)
+        self._chk(self._lib.ipls_agg_get_partitions(self._h, buf.ctypes.data, n, N.HOST_F64))
+        return buf
+
+    # ---- state access ----
+    def read(self, partition: int, target: int = N.TGT_AGG, *, big_endian: bool = False):
+        L = self.lengths[partition]
+        if big_endian:
+            buf = np.empty(8 * L, dtype=np.uint8)
+            self._chk(self._lib.ipls_agg_read(self._h, partition, target, buf.ctypes.data, L, N.HOST_BE))
+            return buf.tobytes()
+        buf = np.empty(L)
+        self._chk(self._lib.ipls_agg_read(self._h, partition, target, buf.ctypes.data, L, N.HOST_F64))
+        return buf
+
+    def reset(self, partition: int = N.ALL_PARTITIONS):
+        self._chk(self._lib.ipls_agg_reset(self._h, partition))
+
+    def device_ptr(self, partition: int, target: int = N.TGT_AGG) -> int:
+        p = ctypes.c_void_p()
+        self._chk(self._lib.ipls_agg_device_ptr(self._h, partition, target, ctypes.byref(p)))
+        return int(p.value)
+
+    def checksum(self, partition: int, target: int = N.TGT_AGG) -> int:
+        v = ctypes.c_uint64()
+        self._chk(self._lib.ipls_agg_checksum(self._h, partition, target, ctypes.byref(v)))
+        return int(v.value)
+
+
+# ---- handle-free device utilities ----
+def synth_fill(buf: DeviceBuffer, p: int, k: int, seed: int, stream: int = 0):
+    N.check(N.lib().ipls_synth_fill(buf.ptr, buf.n, seed, p, k, buf.kind, stream or None))
+
+
+def checksum_dev(buf: DeviceBuffer, n: int | None = None, stream: int = 0) -> int:
+    v = ctypes.c_uint64()
+    N.check(N.lib().ipls_checksum_dev(buf.ptr, buf.n if n is None else n, buf.kind,
+                                      ctypes.byref(v), stream or None))
+    return int(v.value)
+
+
+def frame_parse(frame: bytes):
+    """Header of a pubsub frame: (pid, n, a, b, payload_off, origin_off)."""
+    a = np.frombuffer(bytes(frame), dtype=np.uint8)
+    pid, x, y = ctypes.c_int16(), ctypes.c_int32(), ctypes.c_int32()
+    po, oo = ctypes.c_int64(), ctypes.c_int64()
+    n = N.check(N.lib().ipls_frame_parse(a.ctypes.data, a.size, ctypes.byref(pid), ctypes.byref(x),
+                                         ctypes.byref(y), ctypes.byref(po), ctypes.byref(oo)))
+    return pid.value, n, x.value, y.value, po.value, oo.value
+
+
+def frame_encode(gradient, a: int, b: int, pid: int, origin: bytes) -> bytes:
+    """Marshall_Packet(double[],...) before base64 (MyIPFSClass.java:990-1017)."""
+    if isinstance(gradient, DeviceBuffer):
+        ptr, n, kind = gradient.ptr, gradient.n, N.DEV_F64
+        keep = None
+    else:
+        keep = np.ascontiguousarray(np.zeros(0) if gradient is None else gradient, dtype=np.float64)
+        ptr, n, kind = keep.ctypes.data, keep.size, N.HOST_F64
+    o = np.frombuffer(bytes(origin), dtype=np.uint8)
+    out = np.empty(14 + 8 * n + o.size, dtype=np.uint8)
+    nb = N.check(N.lib().ipls_frame_encode(ptr, n, kind, a, b, pid, o.ctypes.data if o.size else None,
+                                           o.size, out.ctypes.data, out.size))
+    return out[:nb].tobytes()

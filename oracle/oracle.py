@@ -1,0 +1,361 @@
+"""Python/numpy restatement of the IPLS aggregation path -- TEST INFRASTRUCTURE ONLY.
+
+A second, independent restatement next to ipls_oracle.c (the C one is the
+fast checker; this one is the readable spec and cross-checks the C one).
+Each function cites the reference Java it follows (paths relative to the
+reference root, src/main/java/).  Parity status: see oracle/__init__.py.
+
+numpy elementwise ``+`` and ``/`` on float64 are IEEE-754 round-to-nearest,
+identical to Java ``double``.  Peer folds are explicit loops over peers,
+never ``np.sum`` (pairwise summation would change the association).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+SEED = 0x1B5_2026
+GOLDEN_GAMMA = 0x9E3779B97F4A7C15
+M64 = (1 << 64) - 1
+
+START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
+
+
+# --------------------------------------------------------------------------
+# partition geometry
+# --------------------------------------------------------------------------
+def chunk_size(model_size: int, n_partitions: int) -> int:
+    """IPLS.java:1019 -- ``(int)(_MODEL_SIZE/_PARTITIONS) + 1``."""
+    return int(model_size // n_partitions) + 1
+
+
+def partition_len(model_size: int, n_partitions: int, i: int) -> int:
+    """IPLS.java:1023-1028 (InitializeWeights 1862-1868 uses the same rule)."""
+    c = chunk_size(model_size, n_partitions)
+    if (i + 1) * c > model_size:
+        return model_size - i * c + 1
+    return c + 1
+
+
+def organize_gradients(flat, model_size: int, n_partitions: int) -> dict[int, np.ndarray]:
+    """OrganizeGradients, IPLS.java:1018-1040.
+
+    Raises ValueError where Java throws (negative array size / index out of
+    bounds)."""
+    flat = np.asarray(flat, dtype=np.float64)
+    c = chunk_size(model_size, n_partitions)
+    out = {}
+    for i in range(n_partitions):
+        L = partition_len(model_size, n_partitions, i)
+        if L < 0:
+            raise ValueError("NegativeArraySizeException (IPLS.java:1024)")
+        part = np.zeros(L, dtype=np.float64)
+        lo = i * c
+        hi = min((i + 1) * c, len(flat))
+        j = lo
+        if hi > lo:
+            if hi - lo > L:
+                raise ValueError("ArrayIndexOutOfBoundsException (IPLS.java:1030)")
+            part[: hi - lo] = flat[lo:hi]
+            j = hi
+        if j - lo >= L:
+            raise ValueError("ArrayIndexOutOfBoundsException (IPLS.java:1033)")
+        part[j - lo] = 1.0
+        out[i] = part
+    return out
+
+
+# --------------------------------------------------------------------------
+# arithmetic
+# --------------------------------------------------------------------------
+def fold(acc: np.ndarray, g: np.ndarray) -> np.ndarray:
+    """Updater.java:115-117: ``Agg[i] = Agg[i] + Gradient[i]`` for i < len(Agg)."""
+    L = len(acc)
+    acc[:] = acc + np.asarray(g[:L], dtype=np.float64)
+    return acc
+
+
+def reduce(bufs, L: int, start_mode: int = START_ZERO, acc=None) -> np.ndarray:
+    """Fixed-order fold of buckets (peer index ascending).
+
+    ZERO : fresh accumulator +0.0 (IPLS.java:1888,1896; reset 1268)
+    ACCUM: fold into ``acc`` (Updater arrival order)
+    FIRST: start from bucket 0 (Decentralized_Storage_Receiver.java:240-246)
+    """
+    if start_mode == START_ACCUM:
+        out = np.array(acc, dtype=np.float64, copy=True)
+        first = 0
+    elif start_mode == START_ZERO:
+        out = np.zeros(L, dtype=np.float64)
+        first = 0
+    else:
+        out = np.array(bufs[0][:L], dtype=np.float64, copy=True)
+        first = 1
+    for b in bufs[first:]:
+        fold(out, b)
+    return out
+
+
+def aggregate_partition(agg, rep, w, wa):
+    """AggregatePartition, IPLS.java:1255-1270 (non-secure): W = AGG + REP;
+    WA = W; AGG = REP = 0.0 (in place)."""
+    w[:] = agg + rep
+    wa[:] = w
+    agg[:] = 0.0
+    rep[:] = 0.0
+
+
+def divide(w: np.ndarray, secure: bool = False) -> np.ndarray:
+    """GetPartitions, IPLS.java:1159-1174, one partition -> len(w)-1 values."""
+    w = np.asarray(w, dtype=np.float64)
+    cnt = w[-1]
+    body = w[:-1]
+    if cnt == 0.0:                       # also true for -0.0, as in Java
+        return body.copy()
+    if secure:
+        return body / (10.0 ** 12 * cnt)  # Math.pow(10,12)*W[last]
+    return body / cnt
+
+
+def get_partitions(weights: list[np.ndarray], secure: bool = False) -> np.ndarray:
+    """IPLS.java:1159-1174: concatenate the per-partition divides."""
+    return np.concatenate([divide(w, secure) for w in weights]) if weights else np.zeros(0)
+
+
+def encode_secure(x) -> np.ndarray:
+    """Middleware.Encode, Middleware.java:196-210."""
+    x = np.asarray(x, dtype=np.float64)
+    out = x * 10.0 ** 12
+    out = np.where(x > 10.0, 10 * 10.0 ** 12, out)
+    out = np.where(x < -10.0, -10 * 10.0 ** 12, out)
+    return out
+
+
+# --------------------------------------------------------------------------
+# byte codecs
+# --------------------------------------------------------------------------
+def be_decode(data: bytes) -> np.ndarray:
+    """GetParameters, MyIPFSClass.java:444-455: ``len/8`` BE doubles."""
+    n = len(data) // 8
+    return np.frombuffer(bytes(data[: 8 * n]), dtype=">f8").astype(np.float64)
+
+
+def be_encode(x) -> bytes:
+    """update_file(double[]), MyIPFSClass.java:105-116 (putDouble keeps raw NaN bits)."""
+    return np.asarray(x, dtype=np.float64).astype(">f8").tobytes()
+
+
+def be_encode_canonical(x) -> bytes:
+    """Middleware.Serialize, Middleware.java:164-170 (writeDouble ->
+    doubleToLongBits: every NaN becomes 0x7ff8000000000000)."""
+    a = np.asarray(x, dtype=np.float64).copy()
+    bits = a.view(np.uint64)
+    bits[np.isnan(a)] = np.uint64(0x7FF8000000000000)
+    return bits.view(np.float64).astype(">f8").tobytes()
+
+
+def frame_encode(g, a: int, b: int, pid: int, origin: bytes) -> bytes:
+    """Marshall_Packet(double[],origin,partition,iteration,pid) before base64,
+    MyIPFSClass.java:990-1017."""
+    g = np.zeros(0) if g is None else np.asarray(g, dtype=np.float64)
+    head = struct.pack(">hiii", pid, len(g), a, b)
+    return head + be_encode(g) + bytes(origin)
+
+
+def frame_decode(frame: bytes):
+    """GET_GRADIENTS / Get_Replica_Model, MyIPFSClass.java:1437-1481 (the pid
+    short is read first by ThreadReceiver.process, IPLS.java:405).  Returns
+    (pid, n, a, b, gradients-or-None, origin)."""
+    if len(frame) < 14:
+        raise ValueError("BufferUnderflowException")
+    pid, n, a, b = struct.unpack(">hiii", frame[:14])
+    if n < 0 or 14 + 8 * n > len(frame):
+        raise ValueError("BufferUnderflowException")
+    g = be_decode(frame[14:14 + 8 * n]) if n else None   # arr_len == 0 -> null (1449-1451)
+    return pid, n, a, b, g, bytes(frame[14 + 8 * n:])
+
+
+# --------------------------------------------------------------------------
+# synthetic workload and checksum
+# --------------------------------------------------------------------------
+def splitmix64(v: np.ndarray) -> np.ndarray:
+    v = np.asarray(v, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = v + np.uint64(GOLDEN_GAMMA)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_bucket(L: int, p: int, k: int, seed: int = SEED) -> np.ndarray:
+    """x_i = (2u-1)*1e-2, u = (splitmix64(seed ^ p<<40 ^ k<<32 ^ i) >> 11) * 2^-53;
+    element L-1 is the count slot 1.0."""
+    i = np.arange(L, dtype=np.uint64)
+    key = np.uint64(seed) ^ np.uint64((p << 40) & M64) ^ np.uint64((k << 32) & M64) ^ i
+    u = (splitmix64(key) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    t = 2.0 * u
+    t = t - 1.0
+    x = t * 1e-2
+    if L:
+        x[L - 1] = 1.0
+    return x
+
+
+def checksum(x) -> int:
+    """sum_i splitmix64(bits(x_i) + i*0x9E3779B97F4A7C15) mod 2^64 (order independent)."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    i = np.arange(len(x), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        terms = splitmix64(x.view(np.uint64) + i * np.uint64(GOLDEN_GAMMA))
+    return int(terms.sum(dtype=np.uint64))
+
+
+# --------------------------------------------------------------------------
+# ETHModel (reference fixture) -- a Java-serialised
+# org.nd4j.shade.guava.primitives.Doubles$DoubleArrayAsList.  Parsed by hand;
+# nothing in the file is executed.
+# --------------------------------------------------------------------------
+def parse_ethmodel(data: bytes) -> np.ndarray:
+    def u16(o):
+        return struct.unpack_from(">H", data, o)[0]
+
+    o = 0
+    if data[:4] != b"\xac\xed\x00\x05":
+        raise ValueError("not a Java serialization stream")
+    o = 4
+    if data[o] != 0x73 or data[o + 1] != 0x72:          # TC_OBJECT TC_CLASSDESC
+        raise ValueError("unexpected stream layout")
+    o += 2
+    n = u16(o); o += 2
+    cname = data[o:o + n].decode(); o += n
+    if not cname.endswith("Doubles$DoubleArrayAsList"):
+        raise ValueError(f"unexpected class {cname}")
+    o += 8 + 1                                          # serialVersionUID, flags
+    nf = u16(o); o += 2
+    prims = []
+    for _ in range(nf):
+        tc = chr(data[o]); o += 1
+        ln = u16(o); o += 2
+        fname = data[o:o + ln].decode(); o += ln
+        if tc in "[L":
+            o += 1                                      # TC_STRING
+            ln = u16(o); o += 2 + ln
+        else:
+            prims.append((tc, fname))
+    if data[o] != 0x78 or data[o + 1] != 0x70:          # TC_ENDBLOCKDATA, TC_NULL super
+        raise ValueError("unexpected class annotation")
+    o += 2
+    vals = {}
+    for tc, fname in prims:
+        if tc != "I":
+            raise ValueError("unexpected primitive field")
+        vals[fname] = struct.unpack_from(">i", data, o)[0]; o += 4
+    if data[o] != 0x75 or data[o + 1] != 0x72:          # TC_ARRAY TC_CLASSDESC
+        raise ValueError("expected [D array")
+    o += 2
+    n = u16(o); o += 2
+    if data[o:o + n] != b"[D":
+        raise ValueError("expected [D")
+    o += n + 8 + 1
+    if u16(o) != 0 or data[o + 2] != 0x78 or data[o + 3] != 0x70:
+        raise ValueError("unexpected [D descriptor")
+    o += 4
+    count = struct.unpack_from(">i", data, o)[0]; o += 4
+    arr = np.frombuffer(data[o:o + 8 * count], dtype=">f8").astype(np.float64)
+    start, end = vals.get("start", 0), vals.get("end", count)
+    return arr[start:end].copy()
+
+
+# --------------------------------------------------------------------------
+# C oracle (ctypes)
+# --------------------------------------------------------------------------
+_C = None
+
+
+def c_oracle():
+    """Load oracle/build/libipls_oracle.so (built by oracle/Makefile)."""
+    global _C
+    if _C is None:
+        path = HERE / "build" / "libipls_oracle.so"
+        if not path.exists():
+            import subprocess
+            subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+        lib = ctypes.CDLL(str(path))
+        D = ctypes.POINTER(ctypes.c_double)
+        U8 = ctypes.POINTER(ctypes.c_uint8)
+        i64, i32, u64 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64
+        lib.ipls_oracle_chunk.restype = i64
+        lib.ipls_oracle_chunk.argtypes = [i64, i32]
+        lib.ipls_oracle_partition_len.restype = i64
+        lib.ipls_oracle_partition_len.argtypes = [i64, i32, i32]
+        lib.ipls_oracle_organize.restype = ctypes.c_int
+        lib.ipls_oracle_organize.argtypes = [D, i64, i64, i32, i32, D]
+        lib.ipls_oracle_reduce.argtypes = [D, ctypes.POINTER(D), ctypes.c_int, i64, ctypes.c_int]
+        lib.ipls_oracle_divide.argtypes = [D, i64, ctypes.c_int, D]
+        lib.ipls_oracle_be_decode.argtypes = [U8, i64, D]
+        lib.ipls_oracle_be_encode.argtypes = [D, i64, U8]
+        lib.ipls_oracle_be_encode_canonical.argtypes = [D, i64, U8]
+        lib.ipls_oracle_synth_fill.argtypes = [D, i64, u64, i32, i32]
+        lib.ipls_oracle_checksum.restype = u64
+        lib.ipls_oracle_checksum.argtypes = [D, i64]
+        lib.ipls_oracle_synth_sum_checksum.restype = u64
+        lib.ipls_oracle_synth_sum_checksum.argtypes = [u64, i32, i32, i64]
+        lib.ipls_oracle_updater_loop.argtypes = [D, ctypes.POINTER(U8), ctypes.c_int, i64, D]
+        _C = lib
+    return _C
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def c_reduce(bufs, L: int, start_mode: int = START_ZERO, acc=None) -> np.ndarray:
+    lib = c_oracle()
+    out = np.zeros(L) if acc is None else np.array(acc, dtype=np.float64, copy=True)
+    bufs = [np.ascontiguousarray(b, dtype=np.float64) for b in bufs]
+    arr = (ctypes.POINTER(ctypes.c_double) * max(1, len(bufs)))(*[_dp(b) for b in bufs])
+    lib.ipls_oracle_reduce(_dp(out), arr, len(bufs), L, start_mode)
+    return out
+
+
+def c_synth_bucket(L: int, p: int, k: int, seed: int = SEED) -> np.ndarray:
+    out = np.empty(L)
+    c_oracle().ipls_oracle_synth_fill(_dp(out), L, seed, p, k)
+    return out
+
+
+def c_synth_sum_checksum(L: int, p: int, k: int, seed: int = SEED) -> int:
+    return int(c_oracle().ipls_oracle_synth_sum_checksum(seed, p, k, L))
+
+
+def c_checksum(x) -> int:
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return int(c_oracle().ipls_oracle_checksum(_dp(x), len(x)))
+
+
+def c_divide(w, secure=False) -> np.ndarray:
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    out = np.empty(max(0, len(w) - 1))
+    c_oracle().ipls_oracle_divide(_dp(w), len(w), int(secure), _dp(out))
+    return out
+
+
+def c_updater_loop(be_bufs, L: int) -> np.ndarray:
+    """CPU baseline: the reference's single-thread Updater decode+fold loop."""
+    lib = c_oracle()
+    U8 = ctypes.POINTER(ctypes.c_uint8)
+    agg = np.zeros(L)
+    scratch = np.empty(L)
+    arr = (U8 * len(be_bufs))(*[b.ctypes.data_as(U8) for b in be_bufs])
+    lib.ipls_oracle_updater_loop(_dp(agg), arr, len(be_bufs), L, _dp(scratch))
+    return agg
+
+
+def ethmodel_path() -> Path | None:
+    p = Path(os.environ.get("IPLS_REFERENCE", "/root/reference")) / "MNIST_Partitioned_Dataset" / "ETHModel"
+    return p if p.exists() else None

@@ -1,0 +1,344 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the
+committed golden fixtures.  Bit-exact for every element (NaN == NaN; payloads
+unspecified by Java).  Parity status of the oracle itself: unpinned
+ -- see oracle/__init__.py.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import assert_bits_equal
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ipls():
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    import ipls as _ipls
+    return _ipls
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+    return oracle
+
+
+def dev(a: np.ndarray):
+    """Host doubles -> device tensor (keeps the tensor alive) + DeviceBuffer."""
+    import ipls
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to("cuda")
+    return t, ipls.DeviceBuffer.from_tensor(t)
+
+
+def dev_be(a: np.ndarray):
+    import ipls
+    raw = np.frombuffer(np.asarray(a, dtype=np.float64).astype(">f8").tobytes(), dtype=np.uint8).copy()
+    t = torch.from_numpy(raw).to("cuda")
+    return t, ipls.DeviceBuffer(int(t.data_ptr()), raw.size // 8, big_endian=True)
+
+
+# ---------------------------------------------------------------------------
+# synthetic buckets: device generator == oracle generator
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("L,p,k", [(1, 0, 0), (2, 1, 3), (1031, 3, 7), (70001, 15, 63)])
+def test_synth_fill_matches_oracle(ipls, O, L, p, k):
+    t = torch.empty(L, dtype=torch.float64, device="cuda")
+    ipls.synth_fill(ipls.DeviceBuffer.from_tensor(t), p, k, O.SEED)
+    torch.cuda.synchronize()
+    assert_bits_equal(t.cpu().numpy(), O.synth_bucket(L, p, k), "synth")
+    tb = torch.empty(8 * L, dtype=torch.uint8, device="cuda")
+    ipls.synth_fill(ipls.DeviceBuffer(int(tb.data_ptr()), L, big_endian=True), p, k, O.SEED)
+    torch.cuda.synchronize()
+    assert bytes(tb.cpu().numpy()) == O.be_encode(O.synth_bucket(L, p, k))
+
+
+def test_checksum_kernel_matches_oracle(ipls, O):
+    rng = np.random.default_rng(7)
+    for n in (0, 1, 63, 64, 65, 1000, 262147):
+        x = rng.standard_normal(n)
+        t, b = dev(x)
+        assert ipls.checksum_dev(b) == O.checksum(x)
+        tb, bb = dev_be(x)
+        assert ipls.checksum_dev(bb) == O.checksum(x)
+
+
+# ---------------------------------------------------------------------------
+# batched reduce (the benchmarked kernel) vs golden synthetic cases
+# ---------------------------------------------------------------------------
+SMALL = [(3, 1, 2), (2, 2, 1), (4, 1031, 8), (2, 4096, 5), (1, 517, 33), (2, 70001, 3), (1, 262147, 12)]
+
+
+@pytest.mark.parametrize("P,L,K", SMALL)
+@pytest.mark.parametrize("be", [False, True])
+def test_reduce_batch_synth(ipls, O, golden, golden_meta, P, L, K, be):
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    keep, rows = [], []
+    for p in range(P):
+        row = []
+        for k in range(K):
+            t, b = (dev_be if be else dev)(O.synth_bucket(L, p, k))
+            keep.append(t)
+            row.append(b)
+        rows.append(row)
+    for mode, name in [(ipls.START_ZERO, "zero"), (ipls.START_FIRST, "first")]:
+        agg.reduce_batch(0, rows, start_mode=mode, big_endian=be)
+        for p in range(P):
+            got = agg.read(p)
+            key = f"synth_P{P}_L{L}_K{K}_p{p}_{name}"
+            if key in golden:
+                assert_bits_equal(got, golden[key], key)
+            else:
+                assert O.checksum(got) == golden_meta["synth_checksum"][key], key
+                assert agg.checksum(p) == golden_meta["synth_checksum"][key], key
+    agg.close()
+
+
+def test_reduce_batch_unaligned_buckets(ipls, O):
+    """8-byte aligned (not 16) bucket views take the scalar kernel."""
+    L, K = 3001, 4
+    bufs = [O.synth_bucket(L, 0, k) for k in range(K)]
+    big = torch.from_numpy(np.concatenate([np.zeros(1)] + [np.concatenate([b, [0.0]]) for b in bufs])).to("cuda")
+    base = int(big.data_ptr()) + 8
+    ptrs = [base + 8 * (L + 1) * k for k in range(K)]
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    agg.reduce_batch(0, [ptrs], start_mode=ipls.START_ZERO)
+    assert_bits_equal(agg.read(0), O.reduce(bufs, L), "unaligned")
+    agg.close()
+
+
+# ---------------------------------------------------------------------------
+# edge cases: signed zero, cancellation order, subnormals, inf/NaN
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("case", ["szero", "cancel", "special"])
+def test_edge_fold_host_and_device(ipls, O, golden, case):
+    bufs = golden[f"{case}_bufs"]
+    L = bufs.shape[1]
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    # host arrivals one by one (Updater._Update), accumulator starts at +0.0
+    for b in bufs:
+        agg.Update(b, 0, from_clients=True)
+    assert_bits_equal(agg.read(0), golden[f"{case}_zero"], f"{case} host")
+    # device batch, ZERO and FIRST
+    keep = [dev(b) for b in bufs]
+    agg.reduce_batch(0, [[d for _, d in keep]], start_mode=ipls.START_ZERO)
+    assert_bits_equal(agg.read(0), golden[f"{case}_zero"], f"{case} dev zero")
+    if f"{case}_first" in golden:
+        agg.reduce_batch(0, [[d for _, d in keep]], start_mode=ipls.START_FIRST)
+        assert_bits_equal(agg.read(0), golden[f"{case}_first"], f"{case} dev first")
+    # big-endian file bytes (GetParameters input)
+    agg.reset(0)
+    for b in bufs:
+        agg.Update(O.be_encode(b), 0)
+    assert_bits_equal(agg.read(0), golden[f"{case}_zero"], f"{case} BE")
+    agg.close()
+
+
+def test_accumulate_equals_batch(ipls, O):
+    """K arrivals via accumulate (ACCUM) == one ZERO batch == oracle."""
+    L, K = 9001, 11
+    bufs = [O.synth_bucket(L, 2, k) for k in range(K)]
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    keep = [dev(b) for b in bufs]
+    for _, d in keep:
+        agg.Update(d, 0)
+    a1 = agg.read(0)
+    agg.reduce_batch(0, [[d for _, d in keep]], start_mode=ipls.START_ZERO)
+    a2 = agg.read(0)
+    ref = O.reduce(bufs, L)
+    assert_bits_equal(a1, ref, "accum")
+    assert_bits_equal(a2, ref, "batch")
+    # ACCUM on top of an existing value
+    agg.reduce_batch(0, [[d for _, d in keep[:3]]], start_mode=ipls.START_ACCUM)
+    assert_bits_equal(agg.read(0), O.reduce(bufs[:3], L, O.START_ACCUM, acc=ref), "accum2")
+    agg.close()
+
+
+def test_frame_update(ipls, O, golden):
+    """Pubsub frame (MyIPFSClass.java:990-1017) decoded and folded."""
+    fr = bytes(golden["frame_bytes"])
+    g = golden["frame_g"]
+    assert ipls.frame_encode(g, 7, 42, 3, b"QmPeerOrigin") == fr
+    pid, n, a, b, po, oo = ipls.frame_parse(fr)
+    assert (pid, n, a, b, po, oo) == (3, 4, 7, 42, 14, 14 + 32)
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=4)
+    agg.Update(fr, 0, frame=True)
+    agg.Update(fr, 0, frame=True)
+    assert_bits_equal(agg.read(0), O.reduce([g, g], 4), "frame fold")
+    # empty frame -> null gradient -> no-op (MyIPFSClass.java:1449-1451)
+    agg.Update(O.frame_encode(None, 7, 42, 3, b"x"), 0, frame=True)
+    assert_bits_equal(agg.read(0), O.reduce([g, g], 4), "empty frame")
+    with pytest.raises(ipls.IplsError) as e:
+        agg.Update(fr[:20], 0, frame=True)
+    assert e.value.java_name == "BufferUnderflow"
+    agg.close()
+
+
+# ---------------------------------------------------------------------------
+# divide / finalize / GetPartitions
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("case,secure", [("div", False), ("div_zero", False), ("div_nzero", False),
+                                         ("div_secure", True)])
+def test_divide(ipls, golden, case, secure):
+    w = golden[f"{case}_w"]
+    L = len(w)
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L, secure=secure)
+    agg.cache_partition(0, w)
+    assert_bits_equal(agg.GetPartitions(), golden[f"{case}_out"], case)
+    agg.close()
+
+
+def test_finalize_with_replicas(ipls, O):
+    """W = AGG + REP (IPLS.java:1256), Weight_Address = W, then zeroed."""
+    L = 5003
+    own = [O.synth_bucket(L, 1, k) for k in range(4)]
+    reps = [O.synth_bucket(L, 9, k) for k in range(3)]
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    for b in own:
+        agg.Update(b, 0, from_clients=True)
+    for r in reps:
+        agg.Update(r, 0, from_clients=False)
+    s, a = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True, with_average=True)
+    S = O.reduce(own, L) + O.reduce(reps, L)
+    assert bytes(s) == O.be_encode(S)
+    assert_bits_equal(a, O.divide(S), "avg")
+    assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), S, "weights")
+    assert_bits_equal(agg.read(0, ipls.TGT_WADDR), S, "weight_address")
+    assert not agg.read(0, ipls.TGT_AGG).any() and not agg.read(0, ipls.TGT_REP).any()
+    # next round starts from +0.0
+    agg.Update(own[0], 0)
+    assert_bits_equal(agg.read(0), O.reduce(own[:1], L), "next round")
+    agg.close()
+
+
+def test_config_a_ethmodel(ipls, O, ethmodel, golden_meta):
+    """BASELINE configs[0]: ETHModel, -pa 3 -n 3, three peers, full API flow."""
+    meta = golden_meta["config_a"]
+    M = meta["model_size"]
+    peers = [ethmodel + O.synth_bucket(M + 1, 0, k)[:M] for k in range(3)]
+    agg = ipls.Aggregator(M, 3, max_peers=3)
+    assert agg.lengths == meta["partition_len"]
+    agg.InitializeWeights(ethmodel)
+    # before any aggregation the count slot is 0.0 -> model passes through
+    assert_bits_equal(agg.GetPartitions(), ethmodel, "initial model")
+    # peer 0 is this aggregator (UpdateGradient own-accumulate); 1, 2 arrive
+    agg.UpdateGradient(peers[0], auth_list=[0, 1, 2])
+    for k in (1, 2):
+        parts = agg.OrganizeGradients(peers[k], big_endian_out=(k == 2))
+        for p in range(3):
+            agg.Update(parts[p], p, from_clients=True)
+    for p in range(3):
+        s, _ = agg.AggregatePartition(p, with_sum=True)
+        assert hashlib.sha256(bytes(s)).hexdigest() == meta["sum_sha256"][p]
+    avg = agg.GetPartitions()
+    assert hashlib.sha256(avg.astype(">f8").tobytes()).hexdigest() == meta["avg_sha256"]
+    wire = agg.GetPartitions(wire=True)
+    assert hashlib.sha256(wire).hexdigest() == meta["wire_sha256"]
+    agg.close()
+
+
+def test_organize_gradients_geometry(ipls, O, golden):
+    for M, P, tag in [(10, 4, "org10x4"), (12, 4, "org12x4")]:
+        flat = np.arange(1.0, M + 1.0)
+        agg = ipls.Aggregator(M, P)
+        parts = agg.OrganizeGradients(flat)
+        for p in range(P):
+            assert_bits_equal(parts[p], golden[f"{tag}_p{p}"], f"{tag} p{p}")
+        agg.close()
+
+
+def test_split_device_and_be(ipls, O):
+    M, P = 100003, 7
+    flat = O.synth_bucket(M, 4, 4)
+    ref = O.organize_gradients(flat, M, P)
+    agg = ipls.Aggregator(M, P)
+    t, d = dev(flat)
+    for p in range(P):
+        L = agg.lengths[p]
+        out = torch.empty(L, dtype=torch.float64, device="cuda")
+        import ctypes
+        ipls.lib().ipls_agg_split(agg.handle, d.ptr, M, ipls.DEV_F64, p, ctypes.c_void_p(out.data_ptr()),
+                                  ipls.DEV_F64)
+        agg.sync()
+        assert_bits_equal(out.cpu().numpy(), ref[p], f"dev split {p}")
+    be = agg.OrganizeGradients(flat.astype(">f8"), big_endian_out=True)
+    for p in range(P):
+        assert bytes(be[p]) == O.be_encode(ref[p])
+    agg.close()
+
+
+def test_update_gradient_owned_subset(ipls, O):
+    M, P = 50001, 5
+    g1, g2 = O.synth_bucket(M, 0, 1), O.synth_bucket(M, 0, 2)
+    agg = ipls.Aggregator(M, P)
+    agg.UpdateGradient(g1, [1, 3])
+    agg.UpdateGradient(None, [1, 3])      # did not train in time: no-op
+    agg.UpdateGradient(g2, [3])
+    r1, r2 = O.organize_gradients(g1, M, P), O.organize_gradients(g2, M, P)
+    assert_bits_equal(agg.read(1), O.reduce([r1[1]], agg.lengths[1]), "p1")
+    assert_bits_equal(agg.read(3), O.reduce([r1[3], r2[3]], agg.lengths[3]), "p3")
+    assert not agg.read(0).any()
+    agg.close()
+
+
+def test_merge_first_start(ipls, O, golden):
+    """Storage-node merge starts from g0 (keeps -0.0), returns BE file bytes."""
+    bufs = golden["szero_bufs"]
+    st = ipls.Aggregator(n_partitions=1, bucket_len=bufs.shape[1])
+    keep = [dev_be(b) for b in bufs]
+    out = st.Merge(0, [d for _, d in keep])
+    assert out == O.be_encode(golden["szero_first"])
+    st.close()
+
+
+# ---------------------------------------------------------------------------
+# errors (the reference's exceptions)
+# ---------------------------------------------------------------------------
+def test_errors(ipls, O):
+    with pytest.raises(ipls.IplsError) as e:
+        ipls.Aggregator(10, 7)          # chunk 2, partition 6 length -1
+    assert e.value.java_name == "NegativeArraySize"
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=100)
+    with pytest.raises(ipls.IplsError) as e:
+        agg.Update(np.zeros(99), 0)
+    assert e.value.java_name == "ArrayIndexOutOfBounds"
+    with pytest.raises(ipls.IplsError):
+        agg.Update(np.zeros(100), 2)
+    with pytest.raises(ipls.IplsError):
+        agg.cache_partition(0, np.zeros(101))
+    agg.Update(np.ones(100), 1)            # still usable after errors
+    assert agg.read(1).sum() == 100.0
+    agg.close()
+
+
+# ---------------------------------------------------------------------------
+# full-size configs: size-independent property (checksum of the fixed-order
+# sum, computed by the C oracle from the counter formula at build time)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("cfg", ["B", "C"])
+def test_full_size_checksums(ipls, golden_meta, cfg):
+    m = golden_meta["full"][cfg]
+    P, L, K = m["partitions"], m["bucket_len"], m["peers"]
+    arena = torch.empty(P * K * L, dtype=torch.float64, device="cuda")
+    base = int(arena.data_ptr())
+    rows = []
+    for p in range(P):
+        row = []
+        for k in range(K):
+            b = ipls.DeviceBuffer(base + 8 * (p * K + k) * L, L)
+            ipls.synth_fill(b, p, k, golden_meta["seed"])
+            row.append(b)
+        rows.append(row)
+    torch.cuda.synchronize()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    got = [agg.checksum(p) for p in range(P)]
+    assert got == m["sum_checksum"]
+    agg.close()
+    del arena
+    torch.cuda.empty_cache()
