@@ -230,28 +230,46 @@ int d2h(ipls_agg* h, void* dst, const void* src, size_t bytes) {
 unsigned blocks_for(int64_t n, int64_t per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 
 // ---- kernel dispatch: k_reduce ----
-constexpr int kG = 8;  // peers in flight per lane
-constexpr int kR = 1;  // 16-byte vectors per lane per tile
+// Two shapes (tools/reduce_sweep.hip, profiles/r01/sweep*.txt):
+//  * big batches: 1 peer in flight x 16 x 16 B per lane (64 KiB contiguous per
+//    bucket per block), XCD-chunked block order -- 80-83 % of 8 TB/s on config
+//    C over every bucket layout tried, within ~3 % of a pure streaming read;
+//  * small batches (< kBigMinBlocks tiles of the big shape): 8 peers in flight
+//    x 16 B per lane, partition-major -- more blocks to fill 256 CUs.
+constexpr int kBigG = 1, kBigR = 16, kBigMap = 2;
+constexpr int kSmallG = 8, kSmallR = 1, kSmallMap = 0;
+constexpr int64_t kBigMinBlocks = 2048;
 
-template <bool BE_IN, bool BE_OUT, int START>
+template <bool BE_IN, int START, bool BIG>
 void launch_reduce_t(dim3 grid, hipStream_t st, const unsigned long long* const* bufs,
-                     const PartDesc* parts, unsigned long long* dst, int k, int tpp) {
-  hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kG, kR, true>), grid, dim3(kBlock), 0, st,
-                     bufs, parts, dst, k, tpp);
+                     const PartDesc* parts, unsigned long long* dst, int k, int tpp, int n_parts) {
+  if constexpr (BIG)
+    hipLaunchKernelGGL((k_reduce<BE_IN, false, START, kBigG, kBigR, true, kBigMap>), grid, dim3(kBlock), 0, st,
+                       bufs, parts, dst, k, tpp, n_parts);
+  else
+    hipLaunchKernelGGL((k_reduce<BE_IN, false, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
+                       st, bufs, parts, dst, k, tpp, n_parts);
 }
 
-void launch_reduce(bool be_in, int start, dim3 grid, hipStream_t st,
-                   const unsigned long long* const* bufs, const PartDesc* parts,
-                   unsigned long long* dst, int k, int tpp) {
+void launch_reduce(bool be_in, int start, int64_t maxL, int n_parts, hipStream_t st,
+                   const unsigned long long* const* bufs, const PartDesc* parts, unsigned long long* dst, int k) {
+  const int64_t big_tile = (int64_t)kBlock * 2 * kBigR;
+  const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
+  const bool big = big_tpp * n_parts >= kBigMinBlocks;
+  const int64_t tile = big ? big_tile : (int64_t)kBlock * 2 * kSmallR;
+  const int tpp = (int)((maxL + tile - 1) / tile);
+  const dim3 grid((unsigned)grid_blocks(big ? kBigMap : kSmallMap, (int64_t)tpp * n_parts));
+#define LR(BE, ST)                                                                         \
+  do {                                                                                     \
+    if (big) launch_reduce_t<BE, ST, true>(grid, st, bufs, parts, dst, k, tpp, n_parts);   \
+    else launch_reduce_t<BE, ST, false>(grid, st, bufs, parts, dst, k, tpp, n_parts);      \
+  } while (0)
   if (be_in) {
-    if (start == kZero) launch_reduce_t<true, false, kZero>(grid, st, bufs, parts, dst, k, tpp);
-    else if (start == kFirst) launch_reduce_t<true, false, kFirst>(grid, st, bufs, parts, dst, k, tpp);
-    else launch_reduce_t<true, false, kAccum>(grid, st, bufs, parts, dst, k, tpp);
+    if (start == kZero) LR(true, kZero); else if (start == kFirst) LR(true, kFirst); else LR(true, kAccum);
   } else {
-    if (start == kZero) launch_reduce_t<false, false, kZero>(grid, st, bufs, parts, dst, k, tpp);
-    else if (start == kFirst) launch_reduce_t<false, false, kFirst>(grid, st, bufs, parts, dst, k, tpp);
-    else launch_reduce_t<false, false, kAccum>(grid, st, bufs, parts, dst, k, tpp);
+    if (start == kZero) LR(false, kZero); else if (start == kFirst) LR(false, kFirst); else LR(false, kAccum);
   }
+#undef LR
 }
 
 void launch_reduce_scalar(bool be_in, int start, dim3 grid, hipStream_t st,
@@ -323,9 +341,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   auto dbufs = (const unsigned long long* const*)((char*)dtab + desc_bytes);
   auto dst = (unsigned long long*)h->arena;
   if (aligned16) {
-    const int64_t tile = (int64_t)kBlock * 2 * kR;
-    const int tpp = (int)((maxL + tile - 1) / tile);
-    launch_reduce(be_in, start, dim3((unsigned)tpp * n_parts), h->stream, dbufs, dparts, dst, k, tpp);
+    launch_reduce(be_in, start, maxL, n_parts, h->stream, dbufs, dparts, dst, k);
   } else {
     const int64_t tile = (int64_t)kBlock * 8;
     const int tpp = (int)((maxL + tile - 1) / tile);
@@ -948,7 +964,11 @@ int ipls_synth_fill(void* dst, int64_t len, uint64_t seed, int p, int k, int dst
 }
 
 int ipls_checksum_dev(const void* src, int64_t n, int src_kind, uint64_t* out, void* stream) {
-  if (!src || !out || n < 0) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  if (!out || n < 0 || (n > 0 && !src)) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  if (n == 0) {
+    *out = 0;
+    return IPLS_OK;
+  }
   hipStream_t st = (hipStream_t)stream;
   unsigned long long* d = nullptr;
   if (hipMallocAsync((void**)&d, 8, st) != hipSuccess) return fail(nullptr, IPLS_E_NOMEM, "hipMallocAsync failed");

@@ -99,14 +99,43 @@ __device__ __forceinline__ double decode1(unsigned long long raw) {
 //   G      : peers whose loads are in flight together per lane
 //   R      : 16-byte vectors per lane per tile
 //   NT     : non-temporal loads (each byte is read exactly once)
+//   MAP    : block -> (partition, tile) order.  0 = partition-major;
+//            1 = tile-major (consecutive blocks in different partitions);
+//            2 = XCD-chunked: blocks b, b+8, b+16.. (one XCD under the observed
+//                round-robin dispatch) walk one contiguous 1/8 of the work, so
+//                the 8 XCDs stream 8 distant regions (speed only, never
+//                correctness: any placement computes the same result).
 // ---------------------------------------------------------------------------
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT>
+//            MAP 2 needs gridDim.x padded to a multiple of 8 (grid_blocks());
+//            the padding blocks map past the last tile and exit.
+__host__ __device__ constexpr int64_t grid_blocks(int map, int64_t tiles) {
+  return map == 2 ? (tiles + 7) / 8 * 8 : tiles;
+}
+
+__device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_part, int n_parts, int& q, int& t) {
+  int b = blockIdx.x;
+  if (map == 2) {
+    const int per = nblocks >> 3;  // nblocks % 8 == 0 (grid_blocks)
+    b = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (b >= tiles_per_part * n_parts) { q = n_parts; t = 0; return; }
+  }
+  if (map == 1) {
+    q = b % n_parts;
+    t = b / n_parts;
+  } else {
+    q = b / tiles_per_part;
+    t = b - q * tiles_per_part;
+  }
+}
+
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void k_reduce(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
-    unsigned long long* __restrict__ dst_base, int k, int tiles_per_part) {
+    unsigned long long* __restrict__ dst_base, int k, int tiles_per_part, int n_parts) {
   constexpr int64_t kTile = (int64_t)kBlock * 2 * R;
-  const int q = blockIdx.x / tiles_per_part;
-  const int t = blockIdx.x - q * tiles_per_part;
+  int q, t;
+  map_block(MAP, gridDim.x, tiles_per_part, n_parts, q, t);
+  if (q >= n_parts) return;
   const int64_t L = parts[q].len;
   const int64_t base = (int64_t)t * kTile;
   if (base >= L) return;
@@ -166,15 +195,30 @@ __global__ __launch_bounds__(kBlock) void k_reduce(
 #pragma unroll
     for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
   } else {
-    // ---------------- scalar path: the partial last tile ----------------
-    const int64_t end = L;
-    for (int64_t i = base + tid; i < end; i += kBlock) {
-      double acc;
-      if constexpr (START == kZero) acc = 0.0;
-      else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + i));
-      else acc = decode1<BE_OUT>(ld8(dst + i));
-      for (int jj = j0; jj < k; ++jj) acc = acc + decode1<BE_IN>(ld8(pb[jj] + i));
-      st8(dst + i, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
+    // ------- partial last tile: 512-element vector steps, scalar remainder -------
+    for (int64_t sb = base; sb < L; sb += 2 * kBlock) {
+      const int64_t i = sb + 2 * tid;
+      if (sb + 2 * kBlock <= L) {
+        d2 acc;
+        if constexpr (START == kZero) acc = d2{0.0, 0.0};
+        else if constexpr (START == kFirst) acc = decode2<BE_IN>(ld16<NT>(pb[0] + i));
+        else acc = decode2<BE_OUT>(ld16<false>(dst + i));
+        for (int jj = j0; jj < k; ++jj) {
+          const d2 x = decode2<BE_IN>(ld16<NT>(pb[jj] + i));
+          acc.x = acc.x + x.x;
+          acc.y = acc.y + x.y;
+        }
+        __builtin_nontemporal_store(encode2<BE_OUT>(acc), (gu2)(dst + i));
+      } else {
+        for (int64_t e = sb + tid; e < L; e += kBlock) {
+          double acc;
+          if constexpr (START == kZero) acc = 0.0;
+          else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + e));
+          else acc = decode1<BE_OUT>(ld8(dst + e));
+          for (int jj = j0; jj < k; ++jj) acc = acc + decode1<BE_IN>(ld8(pb[jj] + e));
+          st8(dst + e, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
+        }
+      }
     }
   }
 }

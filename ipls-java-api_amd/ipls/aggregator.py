@@ -57,12 +57,9 @@ def _host_operand(x, big_endian: bool):
     """(pointer, n_doubles, kind, keepalive) for a host operand."""
     if isinstance(x, (bytes, bytearray, memoryview)):
         a = np.frombuffer(x, dtype=np.uint8)
-        big_endian = True
     else:
         a = np.asarray(x)
-    if a.dtype == np.uint8:
-        if not big_endian:
-            raise ValueError("byte buffers carry big-endian doubles (IPFS file format)")
+    if a.dtype == np.uint8:          # raw bytes are always BE doubles (IPFS file format)
         a = np.ascontiguousarray(a)
         return a.ctypes.data, a.nbytes // 8, N.HOST_BE, a
     if a.dtype.byteorder == ">":

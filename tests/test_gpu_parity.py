@@ -342,3 +342,28 @@ def test_full_size_checksums(ipls, golden_meta, cfg):
     agg.close()
     del arena
     torch.cuda.empty_cache()
+
+
+def test_big_shape_with_partial_tile(ipls, O):
+    """Batches large enough for the 64-KiB-per-block shape, with an odd
+    length: full tiles + 512-element vector steps + a scalar remainder."""
+    P, L, K = 4, 4200001, 3
+    arena = torch.empty(P * K * (L + 1), dtype=torch.float64, device="cuda")
+    base = int(arena.data_ptr())
+    rows = [[ipls.DeviceBuffer(base + 8 * (p * K + k) * (L + 1), L) for k in range(K)] for p in range(P)]
+    for p in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[p][k], p, k, O.SEED)
+    torch.cuda.synchronize()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    assert [agg.checksum(p) for p in range(P)] == [O.c_synth_sum_checksum(L, p, K) for p in range(P)]
+    # ACCUM on top: S + S (fold of the same buckets again) vs oracle on one partition
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ACCUM)
+    s0 = agg.read(0)
+    ref = O.reduce([O.synth_bucket(L, 0, k) for k in range(K)], L)
+    ref2 = O.reduce([O.synth_bucket(L, 0, k) for k in range(K)], L, O.START_ACCUM, acc=ref)
+    assert_bits_equal(s0, ref2, "accum twice")
+    agg.close()
+    del arena
+    torch.cuda.empty_cache()

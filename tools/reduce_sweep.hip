@@ -1,0 +1,177 @@
+// reduce_sweep.hip -- dev tool: time k_reduce variants on one MI355X.
+//
+// Usage: reduce_sweep P L K PAD REPS
+// Allocates P*K buckets of L doubles (PAD doubles between buckets), fills them
+// with the synthetic generator, then times every variant REPS times,
+// interleaved round-robin in one process (cdna_hip_programming.md §5.4 rule 24),
+// reporting median/min kernel time (hipEvents) and algorithmic GB/s.
+// Also times two HBM reference kernels on the same bytes: a pure streaming
+// read (ceiling for this access pattern) and a dwordx4 copy.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../ipls-java-api_amd/csrc/ipls_kernels.hpp"
+
+using namespace ipls;
+
+#define CK(x)                                                                     \
+  do {                                                                            \
+    hipError_t e = (x);                                                           \
+    if (e != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                    \
+    }                                                                             \
+  } while (0)
+
+// Streaming read of every bucket byte (no fold dependency), one store per lane.
+template <int G, int R>
+__global__ __launch_bounds__(kBlock) void k_readall(const unsigned long long* const* __restrict__ bufs,
+                                                    int n_bufs, int64_t L, unsigned long long* sink) {
+  const int64_t base = (int64_t)blockIdx.x * kBlock * 2 * R;
+  if (base + (int64_t)kBlock * 2 * R > L) return;
+  u2 acc = {0, 0};
+  int j = 0;
+  for (; j + G <= n_bufs; j += G) {
+    u2 v[G][R];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        v[g][r] = ld16<true>(bufs[blockIdx.y * n_bufs + j + g] + base + 2 * (r * kBlock + threadIdx.x));
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc ^= v[g][r];
+  }
+  if ((acc.x ^ acc.y) == 0x1234567ULL) sink[0] = acc.x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy(const u2* __restrict__ in, u2* __restrict__ out, int64_t n2) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (int64_t)gridDim.x * kBlock)
+    __builtin_nontemporal_store(__builtin_nontemporal_load((gcu2)(in + i)), (gu2)(out + i));
+}
+
+struct Var {
+  std::string name;
+  std::function<void(hipStream_t)> run;
+  double bytes;
+  std::vector<float> ms;
+};
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 16;
+  const int64_t L = argc > 2 ? atoll(argv[2]) : 4194304;
+  const int K = argc > 3 ? atoi(argv[3]) : 32;
+  const int64_t PAD = argc > 4 ? atoll(argv[4]) : 32;
+  const int REPS = argc > 5 ? atoi(argv[5]) : 10;
+  const bool separate = PAD < 0;
+  const int64_t stride = separate ? L : L + PAD;
+  unsigned long long* arena = nullptr;
+  unsigned long long* base = nullptr;
+  if (!separate) {
+    CK(hipMalloc(&arena, (size_t)P * K * stride * 8 + 4096));
+    base = (unsigned long long*)(((uintptr_t)arena + 255) / 256 * 256);
+  }
+  std::vector<const unsigned long long*> ptrs(P * K);
+  for (int p = 0; p < P; ++p)
+    for (int k = 0; k < K; ++k) {
+      unsigned long long* b;
+      if (separate) CK(hipMalloc(&b, (size_t)L * 8));   // one allocation per bucket (network arrivals)
+      else b = base + (int64_t)(p * K + k) * stride;
+      ptrs[p * K + k] = b;
+      const unsigned long long key = 0x1B52026ULL ^ ((unsigned long long)p << 40) ^ ((unsigned long long)k << 32);
+      hipLaunchKernelGGL(k_synth<false>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
+    }
+  const unsigned long long** d_ptrs;
+  CK(hipMalloc(&d_ptrs, ptrs.size() * 8));
+  CK(hipMemcpy(d_ptrs, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice));
+  std::vector<PartDesc> pd(P);
+  int64_t off = 0;
+  for (int p = 0; p < P; ++p) {
+    pd[p].len = L;
+    pd[p].dst_off = off;
+    off += (L + 31) / 32 * 32;
+  }
+  PartDesc* d_pd;
+  CK(hipMalloc(&d_pd, P * sizeof(PartDesc)));
+  CK(hipMemcpy(d_pd, pd.data(), P * sizeof(PartDesc), hipMemcpyHostToDevice));
+  unsigned long long* dst;
+  CK(hipMalloc(&dst, (size_t)off * 8));
+  unsigned long long* sink;
+  CK(hipMalloc(&sink, 64));
+  unsigned long long* copy_out;
+  const int64_t copy_n2 = (int64_t)P * K * stride / 2;
+  const bool do_copy = getenv("SWEEP_COPY") != nullptr && !separate;
+  if (do_copy) CK(hipMalloc(&copy_out, copy_n2 * 16));
+  CK(hipDeviceSynchronize());
+
+  const double alg = (double)P * (K + 1) * L * 8;
+  std::vector<Var> vars;
+#define ADD(G, R, NT, MAP)                                                                     \
+  vars.push_back(Var{"reduce G=" #G " R=" #R " NT=" #NT " MAP=" #MAP,                           \
+                     [=](hipStream_t s) {                                                       \
+                       const int64_t tile = (int64_t)kBlock * 2 * R;                            \
+                       const int tpp = (int)((L + tile - 1) / tile);                            \
+                       hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, NT, MAP>),       \
+                                          dim3((unsigned)grid_blocks(MAP, (int64_t)tpp * P)), dim3(kBlock), 0, s, \
+                                          (const unsigned long long* const*)d_ptrs, d_pd, dst, K, tpp, P); \
+                     },                                                                         \
+                     alg, {}})
+  ADD(8, 1, true, 0);
+  ADD(8, 1, true, 2);
+  ADD(2, 8, true, 2);
+  ADD(1, 16, true, 0);
+  ADD(1, 16, true, 2);
+  ADD(2, 16, true, 0);
+  ADD(2, 16, true, 2);
+  ADD(1, 32, true, 2);
+#undef ADD
+#define RA(G, R)                                                                                   \
+  vars.push_back(Var{"readall G=" #G " R=" #R " (read ceiling)",                                     \
+                     [=](hipStream_t s) {                                                            \
+                       hipLaunchKernelGGL((k_readall<G, R>), dim3((unsigned)(L / (2 * kBlock * R)), P), \
+                                          dim3(kBlock), 0, s, (const unsigned long long* const*)d_ptrs, K, L, sink); \
+                     },                                                                              \
+                     (double)P * K * (L / (2 * kBlock * R)) * (2 * kBlock * R) * 8, {}})
+  RA(8, 1);
+  RA(1, 16);
+  RA(2, 16);
+#undef RA
+  if (do_copy)
+    vars.push_back(Var{"copy dwordx4 nt (read+write)",
+                       [=](hipStream_t s) {
+                         hipLaunchKernelGGL(k_copy, dim3(8192), dim3(kBlock), 0, s, (const u2*)base, (u2*)copy_out, copy_n2);
+                       },
+                       (double)copy_n2 * 32, {}});
+
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& v : vars) v.run(0);  // warm
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < REPS; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(e0, 0));
+      v.run(0);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms);
+    }
+  printf("# P=%d L=%lld K=%d PAD=%lld REPS=%d  algorithmic bytes/launch=%.0f\n", P, (long long)L, K,
+         (long long)PAD, REPS, alg);
+  for (auto& v : vars) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
+    printf("%-36s median %8.4f ms  min %8.4f ms  %8.1f GB/s (median)  %5.1f%% of 8 TB/s\n", v.name.c_str(), med,
+           mn, v.bytes / med / 1e6, v.bytes / med / 1e6 / 80.0);
+  }
+  return 0;
+}
