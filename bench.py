@@ -52,7 +52,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
-    ap.add_argument("--be", action="store_true", help="buckets are big-endian IPFS bytes (fused unpack)")
+    ap.add_argument("--be", action="store_true",
+                    help="buckets are big-endian IPFS bytes and the sum is written as BE bytes "
+                         "(fused unpack + pack, config D's timed pack/unpack)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-inclusive (H2D+D2H) leg")
+    ap.add_argument("--e2e-reps", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-passes", type=int, default=16,
                     help="CPU baseline sample: passes over one partition's K buckets")
@@ -80,6 +84,42 @@ def cpu_baseline(L: int, K: int, passes: int) -> dict:
                       f"({nbytes / 1e9:.1f} GB algorithmic, {dt:.1f} s), BE decode + fold, "
                       f"oracle/ipls_oracle.c ipls_oracle_updater_loop (JDK absent: C restatement)",
             "host_cpus": os.cpu_count()}
+
+
+def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dict:
+    """Rate including the PCIe copies: K peers' BE byte buckets start in host
+    memory (as pulled from IPFS), each arrival is folded (Updater._Update),
+    then AggregatePartition writes the BE sum bytes back to host memory
+    (commit_update's update_file).  Pinned buffers (ipls_host_alloc, DMA
+    straight from them) and pageable numpy buffers (staged) are both timed."""
+    import torch
+    agg = agg_cls(n_partitions=1, bucket_len=L, device=device)
+    pinned = []
+    for k in range(K):
+        t = torch.empty(8 * L, dtype=torch.uint8, device="cuda")
+        ipls.synth_fill(ipls.DeviceBuffer(int(t.data_ptr()), L, big_endian=True), 0, k, ipls.SEED)
+        pb = ipls.PinnedBuffer(8 * L)
+        pb.view()[:] = t.cpu().numpy()
+        pinned.append(pb)
+    pageable = [pb.view().copy() for pb in pinned]
+    out = {}
+    for name, bufs in (("pinned", [pb.view() for pb in pinned]), ("pageable", pageable)):
+        for b in bufs:                                   # warm
+            agg.Update(b, 0)
+        agg.AggregatePartition(0, with_sum=True)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for b in bufs:
+                agg.Update(b, 0)
+            s, _ = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True)
+        dt = time.perf_counter() - t0
+        out[name] = round(reps * (K + 1) * L * 8 / dt / 1e9, 2)
+    agg.close()
+    for pb in pinned:
+        pb.close()
+    return {"unit": "GB/s", **out,
+            "sample": f"{reps} rounds x 1 partition x {K} peers x {L} doubles: H2D of each BE bucket + fold "
+                      f"+ finalize + D2H of the BE sum, algorithmic bytes (K+1)*L*8 per round"}
 
 
 def pmc_traffic(workload_key: str):
@@ -132,8 +172,18 @@ def main():
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=local)
     stream = torch.cuda.ExternalStream(agg.stream, device=torch.device("cuda", local))
 
-    def step():
-        agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO, big_endian=args.be)
+    if args.be:
+        # BE bytes in -> fold -> BE bytes out (the update_file image of each sum)
+        out_arena = torch.empty(P * elem + 32, dtype=torch.float64, device="cuda")
+        obase = (int(out_arena.data_ptr()) + 255) // 256 * 256
+        dsts = [obase + 8 * q * elem for q in range(P)]
+
+        def step():
+            agg.reduce_batch_out(0, rows, dsts, start_mode=ipls.START_ZERO, big_endian_in=True,
+                                 big_endian_out=True)
+    else:
+        def step():
+            agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
 
     for _ in range(args.warmup):
         step()
@@ -168,7 +218,11 @@ def main():
     verified = None
     if not args.no_verify and rank == 0:
         from oracle import oracle as O   # checker only: the oracle's checksum of the fixed-order sum
-        verified = agg.checksum(0) == O.c_synth_sum_checksum(L, p0, K)
+        if args.be:
+            got = ipls.checksum_dev(ipls.DeviceBuffer(dsts[0], L, big_endian=True))
+        else:
+            got = agg.checksum(0)
+        verified = got == O.c_synth_sum_checksum(L, p0, K)
 
     out = None
     if rank == 0:
@@ -190,7 +244,7 @@ def main():
             "data": "synthetic (splitmix64 counter buckets generated on device, SURVEY.md 8(d))",
             "config": {
                 "workload": f"{args.config}: {P} partitions x {L} doubles x {K} peers per GPU"
-                            + (" (big-endian IPFS bytes in, fused bswap)" if args.be else ""),
+                            + (" (BE IPFS bytes in, BE sum bytes out: fused unpack/pack)" if args.be else ""),
                 "partitions": P * world, "bucket_len": L, "peers": K,
                 "parallelism": f"partition-sharded x{world} (no data-path collective)",
             },
@@ -207,6 +261,8 @@ def main():
             },
             "verified_checksum_p0": verified,
         }
+        if world == 1 and not args.no_e2e:
+            out["host_inclusive"] = host_inclusive(ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, K, args.cpu_passes)
         print(json.dumps(out), flush=True)

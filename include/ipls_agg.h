@@ -143,6 +143,17 @@ int ipls_agg_reduce_batch(ipls_agg *h, int p_first, int n_parts,
                           const void *const *bufs, int k, int src_kind,
                           int start_mode, int target);
 
+/* The same batched fold written to caller device buffers, one per partition
+ * (dst[q], at least L_p doubles / 8*L_p bytes): dst_kind DEV_BE fuses the
+ * double->byte pack of update_file (MyIPFSClass.java:105-116) into the fold,
+ * src_kind DEV_BE the byte->double unpack of GetParameters (:444-455).  With
+ * START_FIRST this is the storage node's `-aggr 1` merge
+ * (Decentralized_Storage_Receiver.java:239-258: S = g0; S += g_i; write the
+ * `_partial_aggregation` file).  ACCUM reads dst in dst_kind's byte order. */
+int ipls_agg_reduce_batch_out(ipls_agg *h, int p_first, int n_parts,
+                              const void *const *bufs, int k, int src_kind,
+                              int start_mode, void *const *dst, int dst_kind);
+
 /* AggregatePartition (IPLS.java:1248-1274): W = AGG + REP, Weight_Address = W,
  * AGG = REP = 0.  p may be IPLS_ALL_PARTITIONS.  Optional host outputs for one
  * partition: sum_out (the commit_update file bytes, IPLS_Comm.java:27-37 ->
@@ -178,6 +189,14 @@ int ipls_agg_sync(ipls_agg *h);
  *   sum_i splitmix64(bits(x_i) + i*0x9E3779B97F4A7C15) mod 2^64
  * computed on the device (wave DPP + LDS reduction, exact integer sum). */
 int ipls_agg_checksum(ipls_agg *h, int p, int target, uint64_t *out);
+
+/* ---- host memory ---- */
+
+/* Pinned host memory for IPFS byte buffers / the Middleware stream (the Java
+ * side wraps it with JNI NewDirectByteBuffer).  Host operands that live in
+ * such memory are DMA'd to the device directly, without a staging copy. */
+int ipls_host_alloc(size_t bytes, void **ptr);
+int ipls_host_free(void *ptr);
 
 /* ---- device utilities (no handle) -- stream may be NULL (default stream) ---- */
 

@@ -204,9 +204,29 @@ int upload_table(ipls_agg* h, const void* data, size_t bytes, void** dev) {
 
 // Copy `bytes` of host memory to device `dst` through the pinned double buffer.
 // The caller's buffer is no longer referenced when this returns.
+bool is_pinned_host(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: clear the sticky error
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 int stage_h2d(ipls_agg* h, void* dst, const void* src, size_t bytes) {
   const char* s = (const char*)src;
   char* d = (char*)dst;
+  if (bytes >= (1u << 20) && is_pinned_host(src)) {
+    // Pinned (ipls_host_alloc / registered) source: DMA straight from it, and
+    // wait for that copy only -- the caller may reuse the buffer on return;
+    // kernels queued behind the copy keep running.
+    PinnedSlot& slot = h->stage[0];
+    if (!slot.ev) HIP_TRY(h, hipEventCreateWithFlags(&slot.ev, hipEventDisableTiming));
+    HIP_TRY(h, hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(slot.ev, h->stream));
+    HIP_TRY(h, hipEventSynchronize(slot.ev));
+    return IPLS_OK;
+  }
   for (size_t off = 0; off < bytes; off += kStageChunk) {
     const size_t n = std::min(kStageChunk, bytes - off);
     PinnedSlot& slot = h->stage[h->stage_next];
@@ -240,60 +260,74 @@ constexpr int kBigG = 1, kBigR = 16, kBigMap = 2;
 constexpr int kSmallG = 8, kSmallR = 1, kSmallMap = 0;
 constexpr int64_t kBigMinBlocks = 2048;
 
-template <bool BE_IN, int START, bool BIG>
+template <bool BE_IN, bool BE_OUT, int START, bool BIG>
 void launch_reduce_t(dim3 grid, hipStream_t st, const unsigned long long* const* bufs,
-                     const PartDesc* parts, unsigned long long* dst, int k, int tpp, int n_parts) {
+                     const PartDesc* parts, int k, int tpp, int n_parts) {
   if constexpr (BIG)
-    hipLaunchKernelGGL((k_reduce<BE_IN, false, START, kBigG, kBigR, true, kBigMap>), grid, dim3(kBlock), 0, st,
-                       bufs, parts, dst, k, tpp, n_parts);
+    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kBigR, true, kBigMap>), grid, dim3(kBlock), 0, st,
+                       bufs, parts, k, tpp, n_parts);
   else
-    hipLaunchKernelGGL((k_reduce<BE_IN, false, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
-                       st, bufs, parts, dst, k, tpp, n_parts);
+    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
+                       st, bufs, parts, k, tpp, n_parts);
 }
 
-void launch_reduce(bool be_in, int start, int64_t maxL, int n_parts, hipStream_t st,
-                   const unsigned long long* const* bufs, const PartDesc* parts, unsigned long long* dst, int k) {
+template <bool BE_IN, bool BE_OUT>
+void launch_reduce_io(bool big, int start, dim3 grid, hipStream_t st, const unsigned long long* const* bufs,
+                      const PartDesc* parts, int k, int tpp, int n_parts) {
+#define LR(ST)                                                                                  \
+  do {                                                                                          \
+    if (big) launch_reduce_t<BE_IN, BE_OUT, ST, true>(grid, st, bufs, parts, k, tpp, n_parts);  \
+    else launch_reduce_t<BE_IN, BE_OUT, ST, false>(grid, st, bufs, parts, k, tpp, n_parts);     \
+  } while (0)
+  if (start == kZero) LR(kZero);
+  else if (start == kFirst) LR(kFirst);
+  else LR(kAccum);
+#undef LR
+}
+
+void launch_reduce(bool be_in, bool be_out, int start, int64_t maxL, int n_parts, hipStream_t st,
+                   const unsigned long long* const* bufs, const PartDesc* parts, int k) {
   const int64_t big_tile = (int64_t)kBlock * 2 * kBigR;
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   const bool big = big_tpp * n_parts >= kBigMinBlocks;
   const int64_t tile = big ? big_tile : (int64_t)kBlock * 2 * kSmallR;
   const int tpp = (int)((maxL + tile - 1) / tile);
   const dim3 grid((unsigned)grid_blocks(big ? kBigMap : kSmallMap, (int64_t)tpp * n_parts));
-#define LR(BE, ST)                                                                         \
-  do {                                                                                     \
-    if (big) launch_reduce_t<BE, ST, true>(grid, st, bufs, parts, dst, k, tpp, n_parts);   \
-    else launch_reduce_t<BE, ST, false>(grid, st, bufs, parts, dst, k, tpp, n_parts);      \
-  } while (0)
   if (be_in) {
-    if (start == kZero) LR(true, kZero); else if (start == kFirst) LR(true, kFirst); else LR(true, kAccum);
+    if (be_out) launch_reduce_io<true, true>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
+    else launch_reduce_io<true, false>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
   } else {
-    if (start == kZero) LR(false, kZero); else if (start == kFirst) LR(false, kFirst); else LR(false, kAccum);
+    if (be_out) launch_reduce_io<false, true>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
+    else launch_reduce_io<false, false>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
   }
-#undef LR
 }
 
-void launch_reduce_scalar(bool be_in, int start, dim3 grid, hipStream_t st,
-                          const unsigned long long* const* bufs, const PartDesc* parts,
-                          unsigned long long* dst, int k, int tpp, int64_t tile) {
-#define RS(BE, ST) hipLaunchKernelGGL((k_reduce_scalar<BE, ST>), grid, dim3(kBlock), 0, st, bufs, parts, dst, k, tpp, tile)
-  if (be_in) {
-    if (start == kZero) RS(true, kZero); else if (start == kFirst) RS(true, kFirst); else RS(true, kAccum);
-  } else {
-    if (start == kZero) RS(false, kZero); else if (start == kFirst) RS(false, kFirst); else RS(false, kAccum);
-  }
+void launch_reduce_scalar(bool be_in, bool be_out, int start, dim3 grid, hipStream_t st,
+                          const unsigned long long* const* bufs, const PartDesc* parts, int k, int tpp,
+                          int64_t tile) {
+#define RS(BI, BO, ST) hipLaunchKernelGGL((k_reduce_scalar<BI, BO, ST>), grid, dim3(kBlock), 0, st, bufs, parts, k, tpp, tile)
+#define RS2(BI, BO) do { if (start == kZero) RS(BI, BO, kZero); else if (start == kFirst) RS(BI, BO, kFirst); else RS(BI, BO, kAccum); } while (0)
+  if (be_in) { if (be_out) RS2(true, true); else RS2(true, false); }
+  else { if (be_out) RS2(false, true); else RS2(false, false); }
+#undef RS2
 #undef RS
 }
 
-// Core of accumulate / reduce_batch: all pointers device-resident.
-int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k,
-               bool be_in, int start_mode, int target) {
+// Core of accumulate / reduce_batch: all pointers device-resident.  The
+// destination is the handle's `target` accumulators, or -- when ext_dst is
+// given -- one caller buffer per partition (doubles or, be_out, BE bytes).
+int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, bool be_in,
+               int start_mode, int target, void* const* ext_dst = nullptr, bool be_out = false) {
+  auto dst_of = [&](int q) -> unsigned long long* {
+    return ext_dst ? (unsigned long long*)ext_dst[q]
+                   : (unsigned long long*)(h->arena + target_off(h, p_first + q, target));
+  };
   if (k <= 0) {
     if (start_mode == IPLS_START_ZERO) {
       for (int q = 0; q < n_parts; ++q) {
-        uint8_t* f = zero_flag(h, p_first + q, target);
+        uint8_t* f = ext_dst ? nullptr : zero_flag(h, p_first + q, target);
         if (f) *f = 1;
-        else HIP_TRY(h, hipMemsetAsync(h->arena + target_off(h, p_first + q, target), 0,
-                                       (size_t)h->len[p_first + q] * 8, h->stream));
+        else HIP_TRY(h, hipMemsetAsync(dst_of(q), 0, (size_t)h->len[p_first + q] * 8, h->stream));
       }
     }
     return IPLS_OK;  // ACCUM / FIRST with no bucket: nothing to fold
@@ -301,7 +335,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   // Resolve start mode per the logically-zero flags: an ACCUM into a +0.0
   // accumulator is exactly a ZERO-start fold.
   int start = start_mode;
-  if (start_mode == IPLS_START_ACCUM) {
+  if (start_mode == IPLS_START_ACCUM && !ext_dst) {
     int nz = 0;
     for (int q = 0; q < n_parts; ++q) {
       uint8_t* f = zero_flag(h, p_first + q, target);
@@ -331,7 +365,10 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   PartDesc* pd = (PartDesc*)tbl.data();
   for (int q = 0; q < n_parts; ++q) {
     pd[q].len = h->len[p_first + q];
-    pd[q].dst_off = target_off(h, p_first + q, target);
+    pd[q].dst = dst_of(q);
+    if (!pd[q].dst) return fail(h, IPLS_E_INVAL, "destination %d is NULL", q);
+    if ((uintptr_t)pd[q].dst & 7) return fail(h, IPLS_E_INVAL, "destination %d not 8-byte aligned", q);
+    if ((uintptr_t)pd[q].dst & 15) aligned16 = false;
   }
   std::memcpy(tbl.data() + desc_bytes, bufs, sizeof(void*) * (size_t)n_parts * k);
   void* dtab = nullptr;
@@ -339,20 +376,20 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   if (rc) return rc;
   const PartDesc* dparts = (const PartDesc*)dtab;
   auto dbufs = (const unsigned long long* const*)((char*)dtab + desc_bytes);
-  auto dst = (unsigned long long*)h->arena;
   if (aligned16) {
-    launch_reduce(be_in, start, maxL, n_parts, h->stream, dbufs, dparts, dst, k);
+    launch_reduce(be_in, be_out, start, maxL, n_parts, h->stream, dbufs, dparts, k);
   } else {
     const int64_t tile = (int64_t)kBlock * 8;
     const int tpp = (int)((maxL + tile - 1) / tile);
-    launch_reduce_scalar(be_in, start, dim3((unsigned)tpp * n_parts), h->stream, dbufs, dparts, dst, k,
-                         tpp, tile);
+    launch_reduce_scalar(be_in, be_out, start, dim3((unsigned)tpp * n_parts), h->stream, dbufs, dparts, k, tpp,
+                         tile);
   }
   HIP_TRY(h, hipGetLastError());
-  for (int q = 0; q < n_parts; ++q) {
-    uint8_t* f = zero_flag(h, p_first + q, target);
-    if (f) *f = 0;
-  }
+  if (!ext_dst)
+    for (int q = 0; q < n_parts; ++q) {
+      uint8_t* f = zero_flag(h, p_first + q, target);
+      if (f) *f = 0;
+    }
   return IPLS_OK;
 }
 
@@ -985,6 +1022,43 @@ int ipls_checksum_dev(const void* src, int64_t n, int src_kind, uint64_t* out, v
   hipFreeAsync(d, st);
   if (e != hipSuccess) return fail(nullptr, IPLS_E_DEVICE, "checksum: %s", hipGetErrorString(e));
   *out = v;
+  return IPLS_OK;
+}
+
+int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+                              int start_mode, void* const* dst, int dst_kind) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_parts <= 0 || p_first < 0 || p_first + n_parts > h->P)
+    return fail(h, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, h->P);
+  if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE)
+    return fail(h, IPLS_E_INVAL, "reduce_batch_out takes device buckets (DEV_F64/DEV_BE)");
+  if (dst_kind != IPLS_DEV_F64 && dst_kind != IPLS_DEV_BE)
+    return fail(h, IPLS_E_INVAL, "reduce_batch_out writes device buffers (DEV_F64/DEV_BE)");
+  if (start_mode < IPLS_START_ACCUM || start_mode > IPLS_START_FIRST) return fail(h, IPLS_E_INVAL, "bad start mode");
+  if (!dst || k < 0 || (k > 0 && !bufs)) return fail(h, IPLS_E_INVAL, "bad bucket/destination list");
+  HIP_TRY(h, hipSetDevice(h->device));
+  return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, IPLS_TGT_AGG, dst,
+                    dst_kind == IPLS_DEV_BE);
+}
+
+int ipls_host_alloc(size_t bytes, void** ptr) {
+  if (!ptr) return fail(nullptr, IPLS_E_INVAL, "null ptr");
+  *ptr = nullptr;
+  if (bytes == 0) return IPLS_OK;
+  hipError_t e = hipHostMalloc(ptr, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *ptr = nullptr;
+    return fail(nullptr, e == hipErrorNoDevice ? IPLS_E_NODEV : IPLS_E_NOMEM, "hipHostMalloc(%zu): %s", bytes,
+                hipGetErrorString(e));
+  }
+  return IPLS_OK;
+}
+
+int ipls_host_free(void* ptr) {
+  if (!ptr) return IPLS_OK;
+  hipError_t e = hipHostFree(ptr);
+  if (e != hipSuccess) return fail(nullptr, IPLS_E_INVAL, "hipHostFree: %s", hipGetErrorString(e));
   return IPLS_OK;
 }
 

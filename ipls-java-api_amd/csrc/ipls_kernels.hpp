@@ -29,8 +29,8 @@ constexpr int kBlock = 256;
 enum Start : int { kAccum = 0, kZero = 1, kFirst = 2 };
 
 struct PartDesc {
-  int64_t len;      // L_p incl. count slot
-  int64_t dst_off;  // offset (doubles) of the target array in the arena
+  int64_t len;               // L_p incl. count slot
+  unsigned long long* dst;   // target: an arena accumulator or a caller buffer
 };
 
 // Global-address-space views.  Bucket pointers come from a device table, so
@@ -131,7 +131,7 @@ __device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_pa
 template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void k_reduce(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
-    unsigned long long* __restrict__ dst_base, int k, int tiles_per_part, int n_parts) {
+    int k, int tiles_per_part, int n_parts) {
   constexpr int64_t kTile = (int64_t)kBlock * 2 * R;
   int q, t;
   map_block(MAP, gridDim.x, tiles_per_part, n_parts, q, t);
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(
   const int64_t L = parts[q].len;
   const int64_t base = (int64_t)t * kTile;
   if (base >= L) return;
-  unsigned long long* __restrict__ dst = dst_base + parts[q].dst_off;
+  unsigned long long* __restrict__ dst = parts[q].dst;
   const unsigned long long* const* __restrict__ pb = bufs + (size_t)q * k;
   const int tid = threadIdx.x;
   const int j0 = (START == kFirst) ? 1 : 0;
@@ -225,16 +225,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce(
 
 // Same fold for buckets that are only 8-byte aligned (e.g. a device view into
 // a frame payload): one double per lane per step.
-template <bool BE_IN, int START>
+template <bool BE_IN, bool BE_OUT, int START>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
-    unsigned long long* __restrict__ dst_base, int k, int tiles_per_part, int64_t tile) {
+    int k, int tiles_per_part, int64_t tile) {
   const int q = blockIdx.x / tiles_per_part;
   const int t = blockIdx.x - q * tiles_per_part;
   const int64_t L = parts[q].len;
   const int64_t base = (int64_t)t * tile;
   if (base >= L) return;
-  unsigned long long* __restrict__ dst = dst_base + parts[q].dst_off;
+  unsigned long long* __restrict__ dst = parts[q].dst;
   const unsigned long long* const* __restrict__ pb = bufs + (size_t)q * k;
   const int64_t end = (base + tile < L) ? base + tile : L;
   const int j0 = (START == kFirst) ? 1 : 0;
@@ -242,9 +242,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(
     double acc;
     if constexpr (START == kZero) acc = 0.0;
     else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + i));
-    else acc = __builtin_bit_cast(double, ld8(dst + i));
+    else acc = decode1<BE_OUT>(ld8(dst + i));
     for (int j = j0; j < k; ++j) acc = acc + decode1<BE_IN>(ld8(pb[j] + i));
-    st8(dst + i, __builtin_bit_cast(unsigned long long, acc));
+    st8(dst + i, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
   }
 }
 

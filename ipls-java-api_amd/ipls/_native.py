@@ -74,6 +74,7 @@ SIGNATURES = {
     "ipls_agg_update_gradient": (_i, [_vp, _vp, _i64, _i, _P(_i32), _i]),
     "ipls_agg_accumulate": (_i, [_vp, _i, _i, _vp, _i64, _i]),
     "ipls_agg_reduce_batch": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _i]),
+    "ipls_agg_reduce_batch_out": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _P(_vp), _i]),
     "ipls_agg_finalize": (_i, [_vp, _i, _vp, _i, _P(ctypes.c_double)]),
     "ipls_agg_set_weights": (_i, [_vp, _i, _vp, _i64, _i]),
     "ipls_agg_get_partitions": (_i, [_vp, _vp, _i64, _i]),
@@ -83,6 +84,8 @@ SIGNATURES = {
     "ipls_agg_stream": (_vp, [_vp]),
     "ipls_agg_sync": (_i, [_vp]),
     "ipls_agg_checksum": (_i, [_vp, _i, _i, _P(_u64)]),
+    "ipls_host_alloc": (_i, [ctypes.c_size_t, _P(_vp)]),
+    "ipls_host_free": (_i, [_vp]),
     "ipls_synth_fill": (_i, [_vp, _i64, _u64, _i, _i, _i, _vp]),
     "ipls_checksum_dev": (_i, [_vp, _i64, _i, _P(_u64), _vp]),
     "ipls_frame_parse": (_i64, [_vp, _i64, _P(_i16), _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),

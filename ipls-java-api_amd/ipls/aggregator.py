@@ -215,6 +215,21 @@ class Aggregator:
         self._chk(self._lib.ipls_agg_reduce_batch(self._h, p_first, n_parts, arr, k, kind,
                                                   start_mode, target))
 
+    def reduce_batch_out(self, p_first: int, buckets, dsts, *, start_mode: int = N.START_ZERO,
+                         big_endian_in: bool = False, big_endian_out: bool = False):
+        """Batched fold into caller device buffers ``dsts[q]`` (one per
+        partition); ``big_endian_out`` fuses the update_file byte pack."""
+        n_parts = len(buckets)
+        k = len(buckets[0]) if n_parts else 0
+        flat = [b.ptr if isinstance(b, DeviceBuffer) else int(b) for row in buckets for b in row]
+        if len(flat) != n_parts * k or len(dsts) != n_parts:
+            raise ValueError("need k buckets and one destination per partition")
+        arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
+        darr = (ctypes.c_void_p * max(1, n_parts))(*[d.ptr if isinstance(d, DeviceBuffer) else int(d) for d in dsts])
+        self._chk(self._lib.ipls_agg_reduce_batch_out(
+            self._h, p_first, n_parts, arr, k, N.DEV_BE if big_endian_in else N.DEV_F64, start_mode,
+            darr, N.DEV_BE if big_endian_out else N.DEV_F64))
+
     def Merge(self, partition: int, buckets, *, big_endian: bool = True, target: int = N.TGT_REP):
         """Storage-node merge (Decentralized_Storage_Receiver.java:239-247):
         S = g0; S += g_i -- a FIRST-start fold (it overwrites ``target``, so call
@@ -284,6 +299,32 @@ class Aggregator:
         v = ctypes.c_uint64()
         self._chk(self._lib.ipls_agg_checksum(self._h, partition, target, ctypes.byref(v)))
         return int(v.value)
+
+
+class PinnedBuffer:
+    """Pinned host memory from ipls_host_alloc (what the Java side would wrap
+    as a direct ByteBuffer).  Host operands in it are DMA'd without staging."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        N.check(N.lib().ipls_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr = int(p.value or 0)
+        self.nbytes = nbytes
+
+    def view(self, dtype=np.uint8) -> np.ndarray:
+        buf = (ctypes.c_char * self.nbytes).from_address(self.ptr)
+        return np.frombuffer(buf, dtype=np.uint8).view(dtype)
+
+    def close(self):
+        if self.ptr:
+            N.lib().ipls_host_free(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ---- handle-free device utilities ----

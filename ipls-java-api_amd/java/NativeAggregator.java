@@ -1,0 +1,102 @@
+// NativeAggregator.java -- Java side of the JNI binding of libipls_agg
+// (include/ipls_agg.h).  A Java IPLS maintainer drops this class into
+// src/main/java/ next to IPLS.java and calls it from the patched loops listed
+// in INTEGRATION.md.  Not compiled in this image (no JDK); the C half is
+// ipls-java-api_amd/jni/ipls_jni.c.
+//
+// Arrays are passed as primitive arrays (pinned with GetPrimitiveArrayCritical)
+// or as direct ByteBuffers (zero copy; allocate them with hostAlloc() so the
+// library DMA's straight from them).
+
+import java.nio.ByteBuffer;
+
+public final class NativeAggregator implements AutoCloseable {
+    static { System.loadLibrary("ipls_jni"); }   // links libipls_agg.so
+
+    // include/ipls_agg.h constants
+    public static final int TGT_AGG = 0, TGT_REP = 1, TGT_WEIGHTS = 2, TGT_WADDR = 3;
+    public static final int START_ACCUM = 0, START_ZERO = 1, START_FIRST = 2;
+    public static final int ALL_PARTITIONS = -1;
+
+    private long handle;
+
+    /** IPLS.init -> InitializeWeights(): -pa, -n, -aggr from Middleware.parse_arguments. */
+    public NativeAggregator(long modelSize, int partitions, int minPeers, boolean partialAggregation,
+                            boolean secure, int device) {
+        handle = open(modelSize, partitions, minPeers, partialAggregation ? 1 : 0, secure ? 1 : 0, device);
+    }
+
+    public int partitionLength(int p) { return (int) partitionLen(handle, p); }
+
+    /** InitializeWeights(List<Double> Model) (IPLS.java:1880-1901). */
+    public void initializeWeights(double[] model) { loadModel(handle, model); }
+
+    /** UpdateGradient own accumulate (IPLS.java:1737-1743); gradients == null is a no-op. */
+    public void updateGradient(double[] gradients, int[] authList) {
+        if (gradients != null) updateGradient(handle, gradients, authList);
+    }
+
+    /** OrganizeGradients (IPLS.java:1018-1040) for partition p (count slot 1.0). */
+    public double[] organize(double[] gradients, int p) {
+        double[] out = new double[partitionLength(p)];
+        split(handle, gradients, p, out);
+        return out;
+    }
+
+    /** Updater._Update: client buckets -> TGT_AGG, replica partials -> TGT_REP. */
+    public void update(double[] gradient, int p, boolean fromClients) {
+        if (gradient != null) accumulate(handle, p, fromClients ? TGT_AGG : TGT_REP, gradient);
+    }
+
+    /** Updater indirect mode: the bytes of an IPFS gradient file (GetParameters input). */
+    public void updateFromFile(ByteBuffer beDoubles, int p, boolean fromClients) {
+        accumulateDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
+    }
+
+    /** ThreadReceiver pid 3: a decoded (base64) pubsub frame. */
+    public void updateFromFrame(byte[] frame, int p, boolean fromClients) {
+        accumulateFrame(handle, p, fromClients ? TGT_AGG : TGT_REP, frame);
+    }
+
+    /** AggregatePartition (IPLS.java:1248-1274); returns the commit_update file bytes. */
+    public byte[] aggregatePartition(int p) {
+        byte[] sum = new byte[8 * partitionLength(p)];
+        finalizePartition(handle, p, sum);
+        return sum;
+    }
+
+    /** Download_Scheduler.cache_partition: Weight_Address[p] = GetParameters(hash). */
+    public void cachePartition(int p, ByteBuffer beDoubles) {
+        setWeightsDirect(handle, p, beDoubles, beDoubles.remaining() / 8);
+    }
+
+    /** GetPartitions (IPLS.java:1140-1174). */
+    public double[] getPartitions(int modelSize) {
+        double[] out = new double[modelSize];
+        getPartitions(handle, out);
+        return out;
+    }
+
+    /** Middleware task 3: the writeDouble stream in one bulk write. */
+    public void getPartitionsWire(ByteBuffer direct) { getPartitionsWire(handle, direct); }
+
+    public static ByteBuffer hostAlloc(int bytes) { return hostAllocDirect(bytes); }
+
+    @Override public void close() { if (handle != 0) { close(handle); handle = 0; } }
+
+    // ---- natives (ipls_jni.c) ----
+    private static native long open(long modelSize, int partitions, int maxPeers, int aggr, int secure, int device);
+    private static native void close(long h);
+    private static native long partitionLen(long h, int p);
+    private static native void loadModel(long h, double[] model);
+    private static native void split(long h, double[] flat, int p, double[] out);
+    private static native void updateGradient(long h, double[] flat, int[] owned);
+    private static native void accumulate(long h, int p, int target, double[] g);
+    private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
+    private static native void accumulateFrame(long h, int p, int target, byte[] frame);
+    private static native void finalizePartition(long h, int p, byte[] sumOut);
+    private static native void setWeightsDirect(long h, int p, ByteBuffer buf, long n);
+    private static native void getPartitions(long h, double[] out);
+    private static native void getPartitionsWire(long h, ByteBuffer direct);
+    private static native ByteBuffer hostAllocDirect(int bytes);
+}

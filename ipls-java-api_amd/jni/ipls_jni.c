@@ -1,0 +1,153 @@
+/*
+ * ipls_jni.c -- JNI half of NativeAggregator (ipls-java-api_amd/java/).
+ * A 1:1 map onto include/ipls_agg.h: no arithmetic here.  Negative return
+ * codes become the Java exception the reference would have thrown.
+ *
+ * Built only where a JDK exists (make -C ipls-java-api_amd jni); this image
+ * has none, so it is compiled on the Java side's build host.
+ */
+#include <jni.h>
+#include <string.h>
+
+#include "../../include/ipls_agg.h"
+
+static void throw_for(JNIEnv *env, int rc, ipls_agg *h) {
+    const char *cls = "java/lang/RuntimeException";
+    switch (rc) {
+        case IPLS_E_RANGE: cls = "java/lang/ArrayIndexOutOfBoundsException"; break;
+        case IPLS_E_NEGSIZE: cls = "java/lang/NegativeArraySizeException"; break;
+        case IPLS_E_FORMAT: cls = "java/nio/BufferUnderflowException"; break;
+        case IPLS_E_INVAL: cls = "java/lang/IllegalArgumentException"; break;
+        case IPLS_E_NOMEM: cls = "java/lang/OutOfMemoryError"; break;
+        default: break;
+    }
+    jclass c = (*env)->FindClass(env, cls);
+    if (c) (*env)->ThrowNew(env, c, ipls_agg_last_error(h));
+}
+
+#define H(x) ((ipls_agg *)(intptr_t)(x))
+#define CHECK(rc, h) do { int rc_ = (rc); if (rc_ < 0) { throw_for(env, rc_, (h)); } } while (0)
+
+JNIEXPORT jlong JNICALL Java_NativeAggregator_open(JNIEnv *env, jclass c, jlong m, jint pa, jint n,
+                                                     jint aggr, jint secure, jint dev) {
+    (void)c;
+    ipls_agg_cfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.model_size = m; cfg.n_partitions = pa; cfg.max_peers = n;
+    cfg.partial_aggregation = aggr; cfg.secure = secure; cfg.device = dev;
+    ipls_agg *h = NULL;
+    int rc = ipls_agg_open(&cfg, &h);
+    if (rc < 0) { throw_for(env, rc, NULL); return 0; }
+    return (jlong)(intptr_t)h;
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_close(JNIEnv *env, jclass c, jlong h) {
+    (void)env; (void)c;
+    ipls_agg_close(H(h));
+}
+
+JNIEXPORT jlong JNICALL Java_NativeAggregator_partitionLen(JNIEnv *env, jclass c, jlong h, jint p) {
+    (void)c;
+    int64_t L = 0;
+    CHECK(ipls_agg_partition_len(H(h), p, &L), H(h));
+    return (jlong)L;
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_loadModel(JNIEnv *env, jclass c, jlong h, jdoubleArray a) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, a);
+    void *p = (*env)->GetPrimitiveArrayCritical(env, a, NULL);
+    int rc = ipls_agg_load_model(H(h), p, n, IPLS_HOST_F64);
+    (*env)->ReleasePrimitiveArrayCritical(env, a, p, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_split(JNIEnv *env, jclass c, jlong h, jdoubleArray flat, jint part,
+                                                     jdoubleArray out) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, flat);
+    void *src = (*env)->GetPrimitiveArrayCritical(env, flat, NULL);
+    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    int rc = ipls_agg_split(H(h), src, n, IPLS_HOST_F64, part, dst, IPLS_HOST_F64);
+    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, flat, src, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_updateGradient(JNIEnv *env, jclass c, jlong h, jdoubleArray flat,
+                                                              jintArray owned) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, flat), no = (*env)->GetArrayLength(env, owned);
+    void *src = (*env)->GetPrimitiveArrayCritical(env, flat, NULL);
+    void *own = (*env)->GetPrimitiveArrayCritical(env, owned, NULL);
+    int rc = ipls_agg_update_gradient(H(h), src, n, IPLS_HOST_F64, (const int32_t *)own, no);
+    (*env)->ReleasePrimitiveArrayCritical(env, owned, own, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, flat, src, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
+                                                          jdoubleArray g) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, g);
+    void *src = (*env)->GetPrimitiveArrayCritical(env, g, NULL);
+    int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_F64);
+    (*env)->ReleasePrimitiveArrayCritical(env, g, src, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
+                                                                jobject buf, jlong n, jint kind) {
+    (void)c;
+    void *src = (*env)->GetDirectBufferAddress(env, buf);
+    CHECK(ipls_agg_accumulate(H(h), p, tgt, src, n, kind), H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_accumulateFrame(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
+                                                               jbyteArray frame) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, frame);
+    void *src = (*env)->GetPrimitiveArrayCritical(env, frame, NULL);
+    int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_FRAME);
+    (*env)->ReleasePrimitiveArrayCritical(env, frame, src, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jclass c, jlong h, jint p,
+                                                                 jbyteArray sum) {
+    (void)c;
+    void *dst = (*env)->GetPrimitiveArrayCritical(env, sum, NULL);
+    int rc = ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL);
+    (*env)->ReleasePrimitiveArrayCritical(env, sum, dst, 0);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclass c, jlong h, jint p, jobject buf,
+                                                                jlong n) {
+    (void)c;
+    CHECK(ipls_agg_set_weights(H(h), p, (*env)->GetDirectBufferAddress(env, buf), n, IPLS_HOST_BE), H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c, jlong h, jdoubleArray out) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, out);
+    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    int rc = ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64);
+    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf) {
+    (void)c;
+    jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    CHECK(ipls_agg_get_partitions(H(h), (*env)->GetDirectBufferAddress(env, buf), cap / 8, IPLS_HOST_BE_CANON),
+          H(h));
+}
+
+JNIEXPORT jobject JNICALL Java_NativeAggregator_hostAllocDirect(JNIEnv *env, jclass c, jint bytes) {
+    (void)c;
+    void *p = NULL;
+    int rc = ipls_host_alloc((size_t)bytes, &p);
+    if (rc < 0) { throw_for(env, rc, NULL); return NULL; }
+    return (*env)->NewDirectByteBuffer(env, p, bytes);
+}

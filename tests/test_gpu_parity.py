@@ -367,3 +367,55 @@ def test_big_shape_with_partial_tile(ipls, O):
     agg.close()
     del arena
     torch.cuda.empty_cache()
+
+
+def test_reduce_batch_out_fused_pack(ipls, O):
+    """BE buckets in, BE sum bytes out (config D's pack/unpack) and the
+    storage-node merge (FIRST start) into caller buffers."""
+    P, L, K = 3, 20001, 5
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    keep, rows, outs = [], [], []
+    for p in range(P):
+        row = []
+        for k in range(K):
+            t, b = dev_be(O.synth_bucket(L, p, k))
+            keep.append(t)
+            row.append(b)
+        rows.append(row)
+        o = torch.empty(8 * L, dtype=torch.uint8, device="cuda")
+        outs.append(o)
+    for mode in (ipls.START_ZERO, ipls.START_FIRST):
+        agg.reduce_batch_out(0, rows, [int(o.data_ptr()) for o in outs], start_mode=mode,
+                             big_endian_in=True, big_endian_out=True)
+        agg.sync()
+        for p in range(P):
+            ref = O.reduce([O.synth_bucket(L, p, k) for k in range(K)], L, mode)
+            assert bytes(outs[p].cpu().numpy()) == O.be_encode(ref)
+    # native doubles out, ACCUM on top of the previous FIRST result
+    o64 = [torch.from_numpy(O.reduce([O.synth_bucket(L, p, k) for k in range(K)], L)).to("cuda") for p in range(P)]
+    agg.reduce_batch_out(0, rows, [int(o.data_ptr()) for o in o64], start_mode=ipls.START_ACCUM,
+                         big_endian_in=True)
+    agg.sync()
+    for p in range(P):
+        s = O.reduce([O.synth_bucket(L, p, k) for k in range(K)], L)
+        assert_bits_equal(o64[p].cpu().numpy(), O.reduce([O.synth_bucket(L, p, k) for k in range(K)], L,
+                                                         O.START_ACCUM, acc=s), "accum out")
+    agg.close()
+
+
+def test_pinned_host_operands(ipls, O):
+    """Host buckets in pinned memory (ipls_host_alloc) take the direct DMA path."""
+    L, K = 300007, 4                       # > 1 MiB per bucket
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    bufs = []
+    for k in range(K):
+        pb = ipls.PinnedBuffer(8 * L)
+        pb.view()[:] = np.frombuffer(O.be_encode(O.synth_bucket(L, 0, k)), dtype=np.uint8)
+        bufs.append(pb)
+    for pb in bufs:
+        agg.Update(pb.view(), 0)
+        pb.view()[:] = 0                     # caller may reuse the buffer at once
+    assert_bits_equal(agg.read(0), O.reduce([O.synth_bucket(L, 0, k) for k in range(K)], L), "pinned")
+    for pb in bufs:
+        pb.close()
+    agg.close()
