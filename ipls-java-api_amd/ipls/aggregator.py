@@ -276,6 +276,23 @@ class Aggregator:
         self._chk(self._lib.ipls_agg_get_partitions(self._h, buf.ctypes.data, n, N.HOST_F64))
         return buf
 
+    # ---- replica exchange hooks (ipls.distributed) ----
+    def export_partial(self, partition: int, tensor):
+        """Copy this aggregator's partial sum AGG[p] into a device tensor (the
+        published partial of IPLS.java:1423-1431) and wait for it."""
+        d = DeviceBuffer.from_tensor(tensor)
+        self._chk(self._lib.ipls_agg_read(self._h, partition, N.TGT_AGG, d.ptr, d.n, N.DEV_F64))
+        self.sync()
+
+    def import_partial(self, partition: int, tensor, *, replace_agg: bool = False):
+        """Fold a replica's partial (a device tensor that has landed) into
+        REP[p] (Updater.java:40-44); replace_agg stores it as AGG[p] instead."""
+        d = DeviceBuffer.from_tensor(tensor)
+        if replace_agg:
+            self.reduce_batch(partition, [[d]], start_mode=N.START_FIRST, target=N.TGT_AGG)
+        else:
+            self.Update(d, partition, from_clients=False)
+
     # ---- state access ----
     def read(self, partition: int, target: int = N.TGT_AGG, *, big_endian: bool = False):
         L = self.lengths[partition]

@@ -1,0 +1,233 @@
+"""The Middleware loopback protocol (Middleware.java:26-268): flags, the task
+1/2/3 byte stream, and a single-aggregator loopback server.
+
+Wire format (Java DataInput/OutputStream, big-endian):
+  task 1  [i16 1][i16 bootstrapper][i16 n]{[i16 len][bytes]}*n [i16 len][path]
+          [i16 len][file name][i32 model_size]                (Middleware.java:128-154)
+  task 2  [i16 2][model_size x f64]                            (:156-160)
+  task 3  [i16 3]  -> reply model_size x f64 (writeDouble)      (:164-170, 253-258)
+  ack     writeChar('A') = 00 41                                (:188-194)
+
+MI355X path. Java reads task 2 one ``readDouble`` at a time and writes task 3
+one ``writeDouble`` at a time on an unbuffered stream. Here the M doubles of
+task 2 are received as one byte buffer (pinned, when a PinnedBuffer is
+supplied) and handed to the GPU still big-endian: the fold kernel does the
+byte swap. The task-3 reply is one ``sendall`` of the bytes produced on the
+GPU by ``GetPartitions(wire=True)``, with NaN canonicalised as
+``writeDouble`` does.
+
+``LoopbackAggregator`` plays the aggregator of BASELINE configs[0] ("-pa 3
+-n 3 loopback: the aggregator averages 3 peers' List<Double>"). Each task 2 is
+one peer's update, folded into every partition as an arrival. After ``-n``
+updates the round closes: AggregatePartition for every partition. Task 3
+returns GetPartitions' averaged model. The IPFS transport, the schedule and
+the responsibility protocol are out of scope.
+"""
+from __future__ import annotations
+
+import socket
+import struct
+import threading
+from dataclasses import dataclass, field
+
+import numpy as np
+
+
+class MissingOptionError(SystemExit):
+    pass
+
+
+@dataclass
+class Options:
+    """Middleware.parse_arguments (Middleware.java:26-110)."""
+    port: int
+    partitions: int                 # -pa   PeerData._PARTITIONS
+    min_partitions: int             # -mp   PeerData._MIN_PARTITIONS
+    min_peers: int                  # -n    PeerData.Min_Members
+    indirect_communication: bool    # -i    > 0
+    training: int                   # -training
+    partial_aggregation: bool       # -aggr > 0
+    ipns: bool = False              # -IPNS "true"
+    synchronous: bool = True        # -async "true" -> False
+    extra: dict = field(default_factory=dict)
+
+
+_FLAGS = {  # short, long, required
+    "p": ("port_number", True), "pa": ("partitions", True), "mp": ("minimum_partitions", True),
+    "n": ("min_peers", True), "i": ("indirect_communication", True), "training": ("training", True),
+    "aggr": ("partial_aggregation", True), "IPNS": ("IPNS", False), "async": ("Async", False),
+}
+
+
+def parse_arguments(argv: list[str]) -> Options:
+    """Same flags as commons-cli in Middleware.java:30-65 (``-x v`` or
+    ``--long v``).  A missing required flag or a non-integer value exits with
+    status 1, as Middleware does (:104-109)."""
+    vals = {}
+    it = iter(argv)
+    for a in it:
+        if not a.startswith("-"):
+            continue
+        key = a.lstrip("-")
+        short = next((s for s, (lng, _) in _FLAGS.items() if key in (s, lng)), None)
+        if short is None:
+            raise MissingOptionError(1)
+        try:
+            vals[short] = next(it)
+        except StopIteration:
+            raise MissingOptionError(1)
+    missing = [s for s, (_, req) in _FLAGS.items() if req and s not in vals]
+    if missing:
+        raise MissingOptionError(1)
+    try:
+        return Options(
+            port=int(vals["p"]), partitions=int(vals["pa"]), min_partitions=int(vals["mp"]),
+            min_peers=int(vals["n"]), indirect_communication=int(vals["i"]) > 0,
+            training=int(vals["training"]), partial_aggregation=int(vals["aggr"]) > 0,
+            ipns=vals.get("IPNS") == "true", synchronous=vals.get("async") != "true")
+    except ValueError:
+        raise MissingOptionError(1)
+
+
+# ---------------------------------------------------------------------------
+# task frames
+# ---------------------------------------------------------------------------
+def _jstr(s: str | bytes) -> bytes:
+    b = s.encode() if isinstance(s, str) else bytes(s)
+    return struct.pack(">h", len(b)) + b
+
+
+def encode_init(is_bootstrapper: bool, bootstrappers: list[str], path: str, file_name: str,
+                model_size: int) -> bytes:
+    out = struct.pack(">hhh", 1, 1 if is_bootstrapper else 0, len(bootstrappers))
+    for b in bootstrappers:
+        out += _jstr(b)
+    return out + _jstr(path) + _jstr(file_name) + struct.pack(">i", model_size)
+
+
+def encode_update(gradients) -> bytes:
+    return struct.pack(">h", 2) + np.asarray(gradients, dtype=np.float64).astype(">f8").tobytes()
+
+
+def encode_get() -> bytes:
+    return struct.pack(">h", 3)
+
+
+ACK = struct.pack(">H", ord("A"))   # DataOutputStream.writeChar('A')
+
+
+def _recv_exact(sock: socket.socket, n: int, into=None) -> memoryview:
+    buf = into if into is not None else bytearray(n)
+    mv = memoryview(buf)[:n]
+    got = 0
+    while got < n:
+        k = sock.recv_into(mv[got:], n - got)
+        if k == 0:
+            raise EOFError("socket closed mid-message")
+        got += k
+    return mv
+
+
+def read_task(sock: socket.socket, model_size: int, payload_buffer=None):
+    """Deserialize (Middleware.java:121-162).  Returns (task, data): task 1 ->
+    dict of the init fields; task 2 -> the model_size*8 BE bytes (a memoryview
+    into payload_buffer when one is supplied, e.g. a PinnedBuffer view);
+    task 3 -> None."""
+    (task,) = struct.unpack(">h", _recv_exact(sock, 2))
+    if task == 1:
+        boot, nb = struct.unpack(">hh", _recv_exact(sock, 4))
+        bs = []
+        for _ in range(nb):
+            (ln,) = struct.unpack(">h", _recv_exact(sock, 2))
+            bs.append(bytes(_recv_exact(sock, ln)).decode())
+        (ln,) = struct.unpack(">h", _recv_exact(sock, 2))
+        path = bytes(_recv_exact(sock, ln)).decode()
+        (ln,) = struct.unpack(">h", _recv_exact(sock, 2))
+        fname = bytes(_recv_exact(sock, ln)).decode()
+        (ms,) = struct.unpack(">i", _recv_exact(sock, 4))
+        return 1, {"is_bootstrapper": boot != 0, "bootstrappers": bs, "path": path, "file_name": fname,
+                   "model_size": ms}
+    if task == 2:
+        return 2, _recv_exact(sock, 8 * model_size, payload_buffer)
+    return task, None
+
+
+# ---------------------------------------------------------------------------
+# loopback aggregator + server
+# ---------------------------------------------------------------------------
+class LoopbackAggregator:
+    """One aggregator that owns every partition and closes a round after
+    ``min_peers`` updates (see module docstring)."""
+
+    def __init__(self, opts: Options, model_size: int, device: int = 0, initial_model=None):
+        from .aggregator import Aggregator, PinnedBuffer
+        self.opts = opts
+        self.model_size = model_size
+        self.agg = Aggregator(model_size, opts.partitions, max_peers=opts.min_peers,
+                              partial_aggregation=int(opts.partial_aggregation), device=device)
+        if initial_model is not None:
+            self.agg.InitializeWeights(initial_model)
+        self.staging = PinnedBuffer(8 * model_size)   # task-2 payload lands here (DMA source)
+        self.pending = 0
+        self.rounds = 0
+        self.lock = threading.Lock()
+
+    def update_model(self, be_bytes):
+        """Task 2: one peer's update vector (BE bytes) folded into every
+        partition as an arrival (Updater._Update / UpdateGradient fold)."""
+        with self.lock:
+            flat = np.frombuffer(be_bytes, dtype=np.uint8)
+            self.agg.UpdateGradient(flat, range(self.opts.partitions))
+            self.pending += 1
+            if self.pending >= self.opts.min_peers:
+                for p in range(self.opts.partitions):
+                    self.agg.AggregatePartition(p)
+                self.pending = 0
+                self.rounds += 1
+
+    def get_partitions_wire(self) -> bytes:
+        with self.lock:
+            return self.agg.GetPartitions(wire=True)
+
+    def close(self):
+        self.agg.close()
+        self.staging.close()
+
+
+def serve(opts: Options, max_connections: int | None = None, device: int = 0, initial_model=None,
+          ready: threading.Event | None = None, host: str = "127.0.0.1"):
+    """Middleware.main (Middleware.java:212-268): one connection per task."""
+    srv = socket.socket()
+    srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    srv.bind((host, opts.port))
+    srv.listen(16)
+    if ready is not None:
+        ready.set()
+    daemon = None
+    served = 0
+    try:
+        while max_connections is None or served < max_connections:
+            conn, _ = srv.accept()
+            served += 1
+            with conn:
+                ms = daemon.model_size if daemon else 0
+                task, data = read_task(conn, ms, daemon.staging.view() if daemon else None)
+                if task == 1:
+                    daemon = LoopbackAggregator(opts, data["model_size"], device, initial_model)
+                    conn.sendall(ACK)
+                elif task == 2:
+                    daemon.update_model(data)
+                    conn.sendall(ACK)
+                elif task == 3:
+                    conn.sendall(daemon.get_partitions_wire())
+    finally:
+        srv.close()
+        if daemon is not None:
+            daemon.close()
+
+
+def client_call(port: int, payload: bytes, reply_bytes: int, host: str = "127.0.0.1") -> bytes:
+    """What the Python IPLS API does per task: connect, send, read the reply."""
+    with socket.create_connection((host, port)) as s:
+        s.sendall(payload)
+        return bytes(_recv_exact(s, reply_bytes)) if reply_bytes else b""

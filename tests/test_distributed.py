@@ -1,0 +1,149 @@
+"""CPU: world-size 2 and 4 `gloo` runs of the partition sharding and the
+replica exchange (ipls.distributed).  The exchange code is the product code;
+the aggregator behind it is a numpy stand-in built on the oracle (test
+infrastructure), because the HIP aggregator needs a GPU.  The GPU half of the
+exchange (export/import of partials through the C-ABI) is in
+test_gpu_parity.py::test_export_import_partial."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import assert_bits_equal
+from oracle import oracle as O
+
+
+class NumpyAggregator:
+    """Stand-in with the Aggregator surface the exchange uses (test only)."""
+
+    def __init__(self, P, L):
+        self.lengths = [L] * P
+        self.agg = [np.zeros(L) for _ in range(P)]
+        self.rep = [np.zeros(L) for _ in range(P)]
+
+    def Update(self, g, p, from_clients=True):
+        O.fold(self.agg[p] if from_clients else self.rep[p], np.asarray(g))
+
+    def export_partial(self, p, t):
+        t.copy_(torch.from_numpy(self.agg[p]))
+
+    def import_partial(self, p, t, replace_agg=False):
+        if replace_agg:
+            self.agg[p] = t.numpy().copy()
+        else:
+            O.fold(self.rep[p], t.numpy())
+
+    def finalize(self, p):
+        return self.agg[p] + self.rep[p]
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def bucket(p, k, L):
+    x = O.synth_bucket(L, p, k)
+    x[0] = [1e16, 1.0, -1e16, 3.0][k % 4]        # order-sensitive element
+    return x
+
+
+def worker(rank, world, port, P, L, K, replicas, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ipls.distributed import ReplicaPlan, combine_replicas
+    plan = ReplicaPlan.build(P, world, replicas)
+    agg = NumpyAggregator(P, L)
+    # each holder of partition p folds its own peers' buckets: holder h gets peers k with k % len == idx
+    for p, hs in plan.holders.items():
+        if rank in hs:
+            idx = hs.index(rank)
+            for k in range(K):
+                if k % len(hs) == idx:
+                    agg.Update(bucket(p, k, L), p)
+    filled = combine_replicas(agg, plan, rank, device="cpu", mode=mode)
+    res = {p: agg.finalize(p) for p in filled}
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def expected(P, L, K, world, replicas):
+    from ipls.distributed import ReplicaPlan, owner_of
+    plan = ReplicaPlan.build(P, world, replicas)
+    out = {}
+    for p, hs in plan.holders.items():
+        if len(hs) == 1:
+            continue
+        parts = {}
+        for idx, h in enumerate(hs):
+            parts[h] = O.reduce([bucket(p, k, L) for k in range(K) if k % len(hs) == idx], L)
+        own = owner_of(p, P, world)
+        rep = O.reduce([parts[r] for r in hs if r != own], L)     # (+0.0 + R1) + R2 ...
+        out[p] = parts[own] + rep                                  # AGG + REP (IPLS.java:1256)
+    return out
+
+
+@pytest.mark.parametrize("world,replicas", [
+    (2, {0: [1], 3: [0]}),
+    (4, {0: [1, 2, 3], 5: [0, 3], 6: [1]}),
+])
+def test_replica_exchange_fixed_order(world, replicas):
+    P, L, K = 8, 1031, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, P, L, K, replicas, "fixed_order", q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = {}
+    for _ in range(world):
+        rank, res = q.get(timeout=120)
+        got.update(res)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    exp = expected(P, L, K, world, replicas)
+    assert sorted(got) == sorted(exp)
+    for p in exp:
+        assert_bits_equal(got[p], exp[p], f"partition {p}")
+
+
+def test_owner_mapping():
+    from ipls.distributed import owned_partitions, owner_of
+    # config E: 64 partitions on 4 GPUs -> 16 per GPU; F: 128 on 8
+    assert [len(owned_partitions(r, 64, 4)) for r in range(4)] == [16] * 4
+    assert owner_of(127, 128, 8) == 7 and owner_of(16, 128, 8) == 1
+    assert sum(len(owned_partitions(r, 10, 4)) for r in range(4)) == 10
+
+
+def test_replica_exchange_rccl_reduce_mode_two_ranks():
+    """The RCCL-reduce comparison mode (here over gloo): with 2 contributors a
+    single add, so it still matches AGG_own + R exactly."""
+    P, L, K, world = 4, 257, 4, 2
+    replicas = {1: [1]}   # owner of 1 is rank 0 -> rank 1 replica
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, P, L, K, replicas, "rccl_reduce", q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = {}
+    for _ in range(world):
+        rank, res = q.get(timeout=120)
+        got.update(res)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    exp = expected(P, L, K, world, replicas)
+    for p in exp:
+        assert np.array_equal(got[p], exp[p]) or np.allclose(got[p], exp[p], rtol=0, atol=4e-16 * np.abs(exp[p]).max())

@@ -419,3 +419,34 @@ def test_pinned_host_operands(ipls, O):
     for pb in bufs:
         pb.close()
     agg.close()
+
+
+def test_export_import_partial(ipls, O):
+    """The GPU half of the replica exchange: a replica's partial leaves through
+    export_partial (AGG -> device tensor) and the owner folds it into REP;
+    finalize gives AGG_own + ((+0.0 + R1) + R2) (IPLS.java:1256)."""
+    L = 70003
+    owner = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    reps = [ipls.Aggregator(n_partitions=1, bucket_len=L) for _ in range(2)]
+    own_b = [O.synth_bucket(L, 5, k) for k in range(3)]
+    rep_b = [[O.synth_bucket(L, 6 + r, k) for k in range(2)] for r in range(2)]
+    for b in own_b:
+        owner.Update(b, 0)
+    partials = []
+    for r, agg in enumerate(reps):
+        for b in rep_b[r]:
+            agg.Update(b, 0)
+        t = torch.empty(L, dtype=torch.float64, device="cuda")
+        agg.export_partial(0, t)
+        partials.append(t)
+    for t in partials:
+        owner.import_partial(0, t)
+    s, _ = owner.AggregatePartition(0, with_sum=True, sum_big_endian=False)
+    R = [O.reduce(rb, L) for rb in rep_b]
+    assert_bits_equal(s, O.reduce(own_b, L) + O.reduce(R, L), "replica combine")
+    # replace_agg: the partial becomes AGG exactly (FIRST start keeps -0.0)
+    neg = torch.full((L,), -0.0, dtype=torch.float64, device="cuda")
+    owner.import_partial(0, neg, replace_agg=True)
+    assert np.signbit(owner.read(0)).all()
+    for a in [owner, *reps]:
+        a.close()

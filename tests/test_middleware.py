@@ -1,0 +1,75 @@
+"""Middleware protocol (Middleware.java:26-268): flags, task frames, and the
+config-A loopback (GPU)."""
+import hashlib
+import socket
+import struct
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import assert_bits_equal
+
+
+def test_parse_arguments_required_and_values():
+    from ipls.middleware import MissingOptionError, parse_arguments
+    o = parse_arguments("-p 5000 -pa 3 -mp 1 -n 3 -i 0 -training 60 -aggr 1".split())
+    assert (o.port, o.partitions, o.min_partitions, o.min_peers) == (5000, 3, 1, 3)
+    assert o.indirect_communication is False and o.partial_aggregation is True
+    assert o.synchronous and not o.ipns
+    o = parse_arguments("--port_number 1 --partitions 16 -mp 2 -n 8 -i 1 -training 5 -aggr 0 -async true -IPNS true".split())
+    assert o.partitions == 16 and o.indirect_communication and not o.synchronous and o.ipns
+    with pytest.raises(MissingOptionError):
+        parse_arguments("-p 5000 -pa 3 -mp 1 -n 3 -i 0 -training 60".split())   # no -aggr
+    with pytest.raises(MissingOptionError):
+        parse_arguments("-p x -pa 3 -mp 1 -n 3 -i 0 -training 60 -aggr 0".split())
+
+
+def test_task_frames_roundtrip():
+    from ipls.middleware import ACK, encode_get, encode_init, encode_update, read_task
+    a, b = socket.socketpair()
+    with a, b:
+        a.sendall(encode_init(False, ["/ip4/1.2.3.4/tcp/4001/ipfs/QmX"], "/ip4/127.0.0.1/tcp/5001", "ETHModel", 443610))
+        t, d = read_task(b, 0)
+        assert t == 1 and d == {"is_bootstrapper": False, "bootstrappers": ["/ip4/1.2.3.4/tcp/4001/ipfs/QmX"],
+                                "path": "/ip4/127.0.0.1/tcp/5001", "file_name": "ETHModel", "model_size": 443610}
+        g = np.array([1.5, -0.0, np.inf, 2.0 ** -1074])
+        a.sendall(encode_update(g))
+        t, d = read_task(b, 4)
+        assert t == 2 and bytes(d) == g.astype(">f8").tobytes()
+        a.sendall(encode_get())
+        assert read_task(b, 4) == (3, None)
+    assert ACK == b"\x00A"
+    # the exact DataOutputStream layout of task 1 (Middleware.java:128-154)
+    raw = encode_init(True, [], "p", "f", 7)
+    assert raw == struct.pack(">hhhh", 1, 1, 0, 1) + b"p" + struct.pack(">h", 1) + b"f" + struct.pack(">i", 7)
+
+
+@pytest.mark.gpu
+def test_config_a_loopback_over_tcp(ethmodel, golden_meta):
+    """BASELINE configs[0]: -pa 3 -n 3 loopback.  Three peers send task 2 over
+    TCP, the round closes, task 3 returns the averaged model as the
+    writeDouble stream -- compared with the golden wire SHA-256."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    from oracle import oracle as O
+    from ipls.middleware import client_call, encode_get, encode_init, encode_update, parse_arguments, serve
+    M = golden_meta["config_a"]["model_size"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    opts = parse_arguments(f"-p {port} -pa 3 -mp 1 -n 3 -i 0 -training 60 -aggr 0".split())
+    ready = threading.Event()
+    th = threading.Thread(target=serve, kwargs=dict(opts=opts, max_connections=5, initial_model=ethmodel,
+                                                    ready=ready), daemon=True)
+    th.start()
+    assert ready.wait(30)
+    assert client_call(port, encode_init(False, [], "/ip4/127.0.0.1/tcp/5001", "ETHModel", M), 2) == b"\x00A"
+    for k in range(3):
+        peer = ethmodel + O.synth_bucket(M + 1, 0, k)[:M]
+        assert client_call(port, encode_update(peer), 2) == b"\x00A"
+    wire = client_call(port, encode_get(), 8 * M)
+    th.join(60)
+    assert hashlib.sha256(wire).hexdigest() == golden_meta["config_a"]["wire_sha256"]
