@@ -196,6 +196,9 @@ int ipls_agg_checksum(ipls_agg *h, int p, int target, uint64_t *out);
  * side wraps it with JNI NewDirectByteBuffer).  Host operands that live in
  * such memory are DMA'd to the device directly, without a staging copy. */
 int ipls_host_alloc(size_t bytes, void **ptr);
+/* (Such buffers are also valid DEV_F64 / DEV_BE bucket pointers for
+ * ipls_agg_reduce_batch: the fold kernel then reads them over PCIe directly,
+ * zero copy.  ipls_agg_accumulate does this by itself for pinned sources.) */
 int ipls_host_free(void *ptr);
 
 /* ---- device utilities (no handle) -- stream may be NULL (default stream) ---- */

@@ -204,13 +204,21 @@ int upload_table(ipls_agg* h, const void* data, size_t bytes, void** dev) {
 
 // Copy `bytes` of host memory to device `dst` through the pinned double buffer.
 // The caller's buffer is no longer referenced when this returns.
-bool is_pinned_host(const void* p) {
+bool is_pinned_host(const void* p, void** dev_alias = nullptr) {
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory: clear the sticky error
     return false;
   }
-  return a.type == hipMemoryTypeHost;
+  if (a.type != hipMemoryTypeHost) return false;
+  if (dev_alias) {
+    // device address of the same bytes (== p for hipHostMalloc; may differ
+    // for hipHostRegister'ed memory)
+    const char* base_h = (const char*)a.hostPointer;
+    const char* base_d = (const char*)a.devicePointer;
+    *dev_alias = (base_h && base_d) ? (void*)(base_d + ((const char*)p - base_h)) : nullptr;
+  }
+  return true;
 }
 
 int stage_h2d(ipls_agg* h, void* dst, const void* src, size_t bytes) {
@@ -591,10 +599,20 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
     case IPLS_HOST_F64:
     case IPLS_HOST_BE: {
       if (int rc = host_decode_count(src_kind, n, L, h)) return rc;
+      be = src_kind == IPLS_HOST_BE;
+      void* alias = nullptr;
+      if (((uintptr_t)src & 7) == 0 && (size_t)L * 8 >= (1u << 16) && is_pinned_host(src, &alias) && alias) {
+        // Zero copy: the fold kernel reads the pinned bucket over PCIe (no
+        // staging copy, no second pass).  The call returns once the kernel
+        // is done with the caller's bytes.
+        const void* bl[1] = {alias};
+        if (int rc = reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target)) return rc;
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        return IPLS_OK;
+      }
       if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
       if (int rc = stage_h2d(h, h->d_scratch, src, (size_t)L * 8)) return rc;
       dptr = h->d_scratch;
-      be = src_kind == IPLS_HOST_BE;
       break;
     }
     case IPLS_HOST_FRAME: {
