@@ -79,10 +79,16 @@ def cpu_baseline(L: int, K: int, passes: int) -> dict:
         O.c_updater_loop(be, L)
     dt = time.perf_counter() - t0
     nbytes = passes * (K + 1) * L * 8
+    # N-thread partition-parallel variant (OMP_NUM_THREADS threads, 16 on the GPU box)
+    t1 = time.perf_counter()
+    _, threads = O.c_updater_loop_parts(be, L, passes)
+    dt_mt = time.perf_counter() - t1
     return {"value": round(nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"{passes} passes x 1 partition x {K} peers x {L} doubles "
                       f"({nbytes / 1e9:.1f} GB algorithmic, {dt:.1f} s), BE decode + fold, "
                       f"oracle/ipls_oracle.c ipls_oracle_updater_loop (JDK absent: C restatement)",
+            "multi_thread": {"value": round(nbytes / dt_mt / 1e9, 3), "cores": threads,
+                             "sample": f"{passes} partitions in parallel, one thread each"},
             "host_cpus": os.cpu_count()}
 
 

@@ -8,7 +8,11 @@
 #include "ipls_oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 /* IPLS.java:1019  int chunk_size = (int)(PeerData._MODEL_SIZE/PeerData._PARTITIONS) + 1;
  * _MODEL_SIZE is a long, _PARTITIONS an int: long division, then (int). */
@@ -213,4 +217,32 @@ void ipls_oracle_updater_loop(double *agg, const uint8_t *const *be_bufs, int k,
         ipls_oracle_be_decode(be_bufs[j], L, scratch);       /* GetParameters(Hash,Gradient_Buff) */
         for (int64_t i = 0; i < L; i++) agg[i] = agg[i] + scratch[i];
     }
+}
+
+/* Partition-parallel variant of the Updater loop (CPU baseline, N threads):
+ * n_parts independent partitions, each folded by one thread exactly as the
+ * single-thread loop does (own accumulator + reused decode buffer).  All
+ * partitions read the same k BE buckets (a bounded input sample).  Returns
+ * the number of threads used. */
+int ipls_oracle_updater_loop_parts(int n_parts, const uint8_t *const *be_bufs, int k, int64_t L,
+                                   double *agg0) {
+    int threads = 1;
+#pragma omp parallel
+    {
+#ifdef _OPENMP
+#pragma omp single
+        threads = omp_get_num_threads();
+#endif
+        double *agg = (double *)malloc((size_t)L * sizeof(double));
+        double *scratch = (double *)malloc((size_t)L * sizeof(double));
+#pragma omp for schedule(dynamic, 1)
+        for (int q = 0; q < n_parts; q++) {
+            memset(agg, 0, (size_t)L * sizeof(double));
+            ipls_oracle_updater_loop(agg, be_bufs, k, L, scratch);
+            if (q == 0 && agg0) memcpy(agg0, agg, (size_t)L * sizeof(double));
+        }
+        free(scratch);
+        free(agg);
+    }
+    return threads;
 }

@@ -111,6 +111,10 @@ uint64_t ipls_oracle_synth_sum_checksum(uint64_t seed, int32_t p, int32_t k, int
 void ipls_oracle_updater_loop(double *agg, const uint8_t *const *be_bufs, int k,
                               int64_t L, double *scratch);
 
+/* N-thread, partition-parallel variant (OpenMP); returns threads used. */
+int ipls_oracle_updater_loop_parts(int n_parts, const uint8_t *const *be_bufs, int k, int64_t L,
+                                   double *agg0);
+
 #ifdef __cplusplus
 }
 #endif

@@ -306,6 +306,8 @@ def c_oracle():
         lib.ipls_oracle_synth_sum_checksum.restype = u64
         lib.ipls_oracle_synth_sum_checksum.argtypes = [u64, i32, i32, i64]
         lib.ipls_oracle_updater_loop.argtypes = [D, ctypes.POINTER(U8), ctypes.c_int, i64, D]
+        lib.ipls_oracle_updater_loop_parts.restype = ctypes.c_int
+        lib.ipls_oracle_updater_loop_parts.argtypes = [ctypes.c_int, ctypes.POINTER(U8), ctypes.c_int, i64, D]
         _C = lib
     return _C
 
@@ -354,6 +356,17 @@ def c_updater_loop(be_bufs, L: int) -> np.ndarray:
     arr = (U8 * len(be_bufs))(*[b.ctypes.data_as(U8) for b in be_bufs])
     lib.ipls_oracle_updater_loop(_dp(agg), arr, len(be_bufs), L, _dp(scratch))
     return agg
+
+
+def c_updater_loop_parts(be_bufs, L: int, n_parts: int):
+    """CPU baseline, N threads: n_parts partitions folded in parallel (each
+    one the single-thread Updater loop).  Returns (partition 0 sum, threads)."""
+    lib = c_oracle()
+    U8 = ctypes.POINTER(ctypes.c_uint8)
+    agg0 = np.zeros(L)
+    arr = (U8 * len(be_bufs))(*[b.ctypes.data_as(U8) for b in be_bufs])
+    t = lib.ipls_oracle_updater_loop_parts(n_parts, arr, len(be_bufs), L, _dp(agg0))
+    return agg0, t
 
 
 def ethmodel_path() -> Path | None:

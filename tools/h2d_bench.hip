@@ -84,6 +84,47 @@ int main(int argc, char** argv) {
     }
     printf("zero-copy fold from pinned host, grid %4d: %7.2f GB/s\n", grid, bytes * K / best / 1e9);
   }
+  // pageable sources (a Java heap byte[] pinned by GetPrimitiveArrayCritical)
+  {
+    std::vector<char*> pg(K);
+    for (int k = 0; k < K; ++k) {
+      pg[k] = (char*)malloc(bytes);
+      std::memset(pg[k], 0x22, bytes);
+    }
+    double best = 1e30;
+    for (int r = 0; r < REPS; ++r) {
+      CK(hipDeviceSynchronize());
+      const double t0 = now();
+      for (int k = 0; k < K; ++k)
+        CK(hipMemcpyAsync((char*)dev + (size_t)k * bytes, pg[k], bytes, hipMemcpyHostToDevice, st[0]));
+      CK(hipStreamSynchronize(st[0]));
+      best = std::min(best, now() - t0);
+    }
+    printf("hipMemcpyAsync H2D from pageable (HIP staging): %7.2f GB/s\n", bytes * K / best / 1e9);
+    best = 1e30;
+    for (int r = 0; r < REPS; ++r) {
+      const double t0 = now();
+      for (int k = 0; k < K; ++k) std::memcpy(host[k], pg[k], bytes);
+      best = std::min(best, now() - t0);
+    }
+    printf("host memcpy pageable -> pinned, 1 thread: %7.2f GB/s\n", bytes * K / best / 1e9);
+    best = 1e30;
+    for (int r = 0; r < REPS; ++r) {
+      CK(hipDeviceSynchronize());
+      const double t0 = now();
+      for (int k = 0; k < K; ++k) {
+        CK(hipHostRegister(pg[k], bytes, hipHostRegisterDefault));
+        void* d = nullptr;
+        CK(hipHostGetDevicePointer(&d, pg[k], 0));
+        hipLaunchKernelGGL(k_fold_from_host, dim3(256), dim3(256), 0, st[0], (const u2*)d, (u2*)acc, (int64_t)(L / 2));
+        CK(hipStreamSynchronize(st[0]));
+        CK(hipHostUnregister(pg[k]));
+      }
+      best = std::min(best, now() - t0);
+    }
+    printf("register + zero-copy fold + unregister per bucket: %7.2f GB/s\n", bytes * K / best / 1e9);
+    for (int k = 0; k < K; ++k) free(pg[k]);
+  }
   {
     double best = 1e30;
     for (int r = 0; r < REPS; ++r) {
