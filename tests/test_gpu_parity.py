@@ -450,3 +450,69 @@ def test_export_import_partial(ipls, O):
     assert np.signbit(owner.read(0)).all()
     for a in [owner, *reps]:
         a.close()
+
+
+def test_concurrent_threads_one_handle(ipls, O):
+    """The Updater thread and the daemon thread share one handle (PeerData.mtx
+    in the reference): concurrent Update calls on different partitions and
+    own-accumulates must give the sequential result per partition."""
+    import threading
+    M, P = 40003, 4
+    agg = ipls.Aggregator(M, P)
+    peers = [O.synth_bucket(M, 9, k) for k in range(6)]
+    parts = [O.organize_gradients(g, M, P) for g in peers]
+    errs = []
+
+    def arrivals(p):
+        try:
+            for k in range(6):
+                agg.Update(parts[k][p], p)
+        except Exception as e:   # pragma: no cover
+            errs.append(e)
+
+    ths = [threading.Thread(target=arrivals, args=(p,)) for p in range(P)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs
+    for p in range(P):
+        assert_bits_equal(agg.read(p), O.reduce([parts[k][p] for k in range(6)], agg.lengths[p]), f"p{p}")
+    agg.close()
+
+
+def test_degenerate_batches(ipls, O):
+    L = 1001
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    t, d = dev(O.synth_bucket(L, 0, 0))
+    agg.Update(np.ones(L), 0)
+    agg.reduce_batch(0, [[], []], start_mode=ipls.START_ACCUM)          # k=0 ACCUM: unchanged
+    assert (agg.read(0) == 1.0).all()
+    agg.reduce_batch(0, [[], []], start_mode=ipls.START_ZERO)           # k=0 ZERO: +0.0
+    assert not agg.read(0).any() and not np.signbit(agg.read(0)).any()
+    agg.reduce_batch(1, [[d]], start_mode=ipls.START_FIRST)             # k=1 FIRST: exact copy
+    assert_bits_equal(agg.read(1), O.synth_bucket(L, 0, 0), "first k=1")
+    agg.reset()
+    assert not agg.read(1).any()
+    # GetPartitions before any aggregation: all-zero weights, count 0.0 -> zeros
+    assert not agg.GetPartitions().any()
+    agg.close()
+
+
+def test_many_partitions_small_buckets(ipls, O):
+    """-pa much larger than the GPU: 300 partitions of an odd model size in
+    one batch launch (small shape), vs the oracle."""
+    M, P, K = 100003, 300, 3
+    agg = ipls.Aggregator(M, P)
+    flats = [O.synth_bucket(M, 1, k) for k in range(K)]
+    for k in range(K):
+        agg.UpdateGradient(flats[k], range(P))
+    ref = [O.organize_gradients(f, M, P) for f in flats]
+    for p in (0, 1, 150, P - 1):
+        assert_bits_equal(agg.read(p), O.reduce([ref[k][p] for k in range(K)], agg.lengths[p]), f"p{p}")
+    for p in range(P):
+        agg.AggregatePartition(p)
+    got = agg.GetPartitions()
+    exp = O.get_partitions([O.reduce([ref[k][p] for k in range(K)], agg.lengths[p]) for p in range(P)])
+    assert_bits_equal(got, exp, "average")
+    agg.close()
