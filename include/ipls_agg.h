@@ -154,6 +154,23 @@ int ipls_agg_reduce_batch_out(ipls_agg *h, int p_first, int n_parts,
                               const void *const *bufs, int k, int src_kind,
                               int start_mode, void *const *dst, int dst_kind);
 
+/* Pubsub ingest on the device (ThreadReceiver.run/process, IPLS.java:851-866,
+ * 399-465; Utils.getRawMessage, Utils.java:8-17).  msgs[i] / lens[i] are the
+ * JSON "data" texts of n_msgs pubsub messages: `layers` (1 or 2) rounds of
+ * java.util.Base64 URL encoding of a Marshall_Packet frame
+ * (MyIPFSClass.java:990-1017).  They are copied to the device, decoded there
+ * (alphabet and '=' rules of Base64.getUrlDecoder), parsed as GET_GRADIENTS
+ * frames (MyIPFSClass.java:1437-1459), and each payload is folded (BE decode
+ * fused) into target[p] in message order.  p = parts[i], or the frame's
+ * partition field when parts is NULL.  A bad message is dropped and reported,
+ * as the Java receiver drops it after printing the exception:
+ * status[i] = 0 folded, 1 null gradient (n == 0, no fold), IPLS_E_FORMAT
+ * (bad base64 / short frame), IPLS_E_RANGE (partition out of range or
+ * payload shorter than L_p).  Returns the number of messages folded. */
+int ipls_agg_ingest_pubsub(ipls_agg *h, int target, const uint8_t *const *msgs,
+                           const int64_t *lens, int n_msgs, int layers,
+                           const int32_t *parts, int32_t *status);
+
 /* AggregatePartition (IPLS.java:1248-1274): W = AGG + REP, Weight_Address = W,
  * AGG = REP = 0.  p may be IPLS_ALL_PARTITIONS.  Optional host outputs for one
  * partition: sum_out (the commit_update file bytes, IPLS_Comm.java:27-37 ->

@@ -34,6 +34,10 @@ constexpr int kRingSlots = 4;
 
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
+uint32_t rd_be32_host(const uint8_t* b) {
+  return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+}
+
 struct PinnedSlot {
   void* host = nullptr;
   size_t cap = 0;
@@ -1039,6 +1043,148 @@ int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void*
   HIP_TRY(h, hipSetDevice(h->device));
   return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, IPLS_TGT_AGG, dst,
                     dst_kind == IPLS_DEV_BE);
+}
+
+// ---- pubsub ingest: base64url (x layers) -> frame -> fold, on the device ----
+namespace {
+
+// Strip and validate the '=' tail of a java.util.Base64 URL text (the rules
+// Decoder.decode0 enforces) -> data chars, or -1 (IllegalArgumentException).
+int64_t b64_data_chars(const uint8_t* t, int64_t n) {
+  int64_t pad = 0;
+  while (pad < n && pad < 3 && t[n - 1 - pad] == '=') ++pad;
+  const int64_t d = n - pad;
+  const int64_t r = d % 4;
+  if (r == 1) return -1;                       // dangling single char
+  if (pad == 0) return d;
+  if (pad == 1 && r == 3) return d;            // "xxx="
+  if (pad == 2 && r == 2) return d;            // "xx=="
+  return -1;                                   // "=" / "x=" / "xx=" / "===" ...
+}
+
+int64_t b64_out_len(int64_t d) { return 3 * (d / 4) + (d % 4 == 2 ? 1 : d % 4 == 3 ? 2 : 0); }
+
+}  // namespace
+
+int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
+                           int layers, const int32_t* parts, int32_t* status) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_msgs < 0 || (n_msgs > 0 && (!msgs || !lens))) return fail(h, IPLS_E_INVAL, "bad message list");
+  if (layers < 1 || layers > 2) return fail(h, IPLS_E_INVAL, "layers must be 1 or 2");
+  if (target_off(h, 0, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (n_msgs == 0) return 0;
+  HIP_TRY(h, hipSetDevice(h->device));
+  std::vector<int32_t> st(n_msgs, 0);
+  std::vector<int64_t> cur_len(n_msgs), text_off(n_msgs), mid_off(n_msgs), frame_off(n_msgs);
+  // layout in scratch: [texts][layer-1 output][frames]; every region 256-B aligned per message
+  int64_t off = 0;
+  for (int i = 0; i < n_msgs; ++i) {
+    text_off[i] = off;
+    off = align_up(off + std::max<int64_t>(lens[i], 0) + 16, 256);
+  }
+  const int64_t text_total = off;
+  for (int i = 0; i < n_msgs; ++i) {
+    mid_off[i] = off;
+    off = align_up(off + lens[i] + 16, 256);
+  }
+  for (int i = 0; i < n_msgs; ++i) {     // frames start 2 bytes in: the payload (frame byte 14) is 16-B aligned
+    frame_off[i] = off + 2;
+    off = align_up(off + 2 + lens[i] + 16, 256);
+  }
+  if (int rc = ensure_scratch(h, (size_t)off + 64 * (size_t)n_msgs + 4096)) return rc;
+  unsigned char* base = (unsigned char*)h->d_scratch;
+  int* d_err = (int*)(base + off);
+  HIP_TRY(h, hipMemsetAsync(d_err, 0, sizeof(int) * n_msgs, h->stream));
+  for (int i = 0; i < n_msgs; ++i)
+    if (lens[i] > 0) HIP_TRY(h, hipMemcpyAsync(base + text_off[i], msgs[i], lens[i], hipMemcpyHostToDevice, h->stream));
+  (void)text_total;
+
+  // host-side tail rules for the layer we can see (the caller's text)
+  std::vector<B64Desc> desc(n_msgs);
+  std::vector<int64_t> out_len(n_msgs, 0);
+  auto decode_layer = [&](const std::vector<int64_t>& src_off, const std::vector<int64_t>& dst_off,
+                          const std::vector<int64_t>& data_chars) -> int {
+    int64_t max_units = 0;
+    for (int i = 0; i < n_msgs; ++i) {
+      const int64_t d = st[i] ? 0 : data_chars[i];
+      desc[i] = B64Desc{src_off[i], d / 4, dst_off[i], (int32_t)(d % 4), 0};
+      out_len[i] = st[i] ? 0 : b64_out_len(d);
+      max_units = std::max(max_units, d / 4);
+    }
+    void* dtab = nullptr;
+    if (int rc = upload_table(h, desc.data(), sizeof(B64Desc) * n_msgs, &dtab)) return rc;
+    const dim3 grid(blocks_for(max_units / 4 + 1, kBlock), (unsigned)n_msgs);
+    hipLaunchKernelGGL(k_b64url_decode, grid, dim3(kBlock), 0, h->stream, (const unsigned char*)base,
+                       (const B64Desc*)dtab, base, d_err);
+    HIP_TRY(h, hipGetLastError());
+    return IPLS_OK;
+  };
+  std::vector<int64_t> dc(n_msgs);
+  for (int i = 0; i < n_msgs; ++i) {
+    dc[i] = lens[i] >= 0 ? b64_data_chars(msgs[i], lens[i]) : -1;
+    if (dc[i] < 0) st[i] = IPLS_E_FORMAT;
+  }
+  std::vector<int> herr(n_msgs);
+  if (layers == 2) {
+    if (int rc = decode_layer(text_off, mid_off, dc)) return rc;
+    // the inner text's tail is on the device: fetch its last 4 chars
+    std::vector<unsigned char> tails(4 * (size_t)n_msgs, 'A');
+    for (int i = 0; i < n_msgs; ++i) {
+      const int64_t n = out_len[i];
+      if (st[i] || n == 0) continue;
+      const int64_t k = std::min<int64_t>(4, n);
+      HIP_TRY(h, hipMemcpyAsync(&tails[4 * i + (4 - k)], base + mid_off[i] + n - k, k, hipMemcpyDeviceToHost,
+                                h->stream));
+    }
+    HIP_TRY(h, hipMemcpyAsync(herr.data(), d_err, sizeof(int) * n_msgs, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    std::vector<int64_t> dc2(n_msgs, 0);
+    for (int i = 0; i < n_msgs; ++i) {
+      if (st[i]) continue;
+      if (herr[i]) { st[i] = IPLS_E_FORMAT; continue; }
+      const int64_t n = out_len[i];
+      // only the last (up to 4) chars matter for the '=' rules
+      const int64_t k = std::min<int64_t>(4, n);
+      int64_t d = b64_data_chars(&tails[4 * i + (4 - k)], k);
+      if (d < 0) { st[i] = IPLS_E_FORMAT; continue; }
+      dc2[i] = n - k + d;
+      if (dc2[i] % 4 == 1) st[i] = IPLS_E_FORMAT;
+    }
+    if (int rc = decode_layer(mid_off, frame_off, dc2)) return rc;
+  } else {
+    if (int rc = decode_layer(text_off, frame_off, dc)) return rc;
+  }
+  // frame headers (14 bytes) + error flags back to the host
+  std::vector<uint8_t> hdr(16 * (size_t)n_msgs, 0);
+  for (int i = 0; i < n_msgs; ++i)
+    if (!st[i] && out_len[i] >= 14)
+      HIP_TRY(h, hipMemcpyAsync(&hdr[16 * i], base + frame_off[i], 14, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipMemcpyAsync(herr.data(), d_err, sizeof(int) * n_msgs, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  // route + validate (GET_GRADIENTS, MyIPFSClass.java:1437-1459)
+  std::vector<std::vector<const void*>> per_part(h->P);
+  for (int i = 0; i < n_msgs; ++i) {
+    if (st[i]) continue;
+    if (herr[i]) { st[i] = IPLS_E_FORMAT; continue; }
+    // [i16 pid][i32 n][i32 partition][i32 iteration] -- n against the real frame length
+    const int32_t n = (int32_t)rd_be32_host(&hdr[16 * i + 2]);
+    if (out_len[i] < 14 || n < 0 || 14 + 8 * (int64_t)n > out_len[i]) { st[i] = IPLS_E_FORMAT; continue; }
+    if (n == 0) { st[i] = 1; continue; }          // arr_len == 0 -> null gradient: no fold
+    const int p = parts ? parts[i] : (int32_t)rd_be32_host(&hdr[16 * i + 6]);
+    if (p < 0 || p >= h->P || n < h->len[p]) { st[i] = IPLS_E_RANGE; continue; }
+    per_part[p].push_back(base + frame_off[i] + 14);
+  }
+  int folded = 0;
+  for (int p = 0; p < h->P; ++p) {
+    if (per_part[p].empty()) continue;
+    if (int rc = reduce_dev(h, p, 1, per_part[p].data(), (int)per_part[p].size(), true, IPLS_START_ACCUM, target))
+      return rc;
+    folded += (int)per_part[p].size();
+  }
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  if (status) std::memcpy(status, st.data(), sizeof(int32_t) * n_msgs);
+  return folded;
 }
 
 int ipls_host_alloc(size_t bytes, void** ptr) {

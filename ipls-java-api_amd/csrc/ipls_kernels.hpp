@@ -450,4 +450,86 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const unsigned long long* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_b64url_decode: java.util.Base64 URL decoding of a batch of messages
+// (ThreadReceiver.run / process, IPLS.java:855-859, 399; Utils.java:14-15).
+// The host strips and validates the '=' tail; the kernel decodes every full
+// 4-char unit (16 chars per lane: one dwordx4 load -> 12 bytes) plus the
+// partial last unit, and flags any byte outside A-Z a-z 0-9 - _ (Java's
+// IllegalArgumentException) in err[msg].  blockIdx.y = message.
+// ---------------------------------------------------------------------------
+struct B64Desc {
+  int64_t src_off;  // byte offset of the text in src (16-B aligned)
+  int64_t units;    // full 4-char units
+  int64_t dst_off;  // byte offset of the decoded bytes in dst
+  int32_t tail;     // data chars in the partial last unit: 0, 2 or 3
+  int32_t pad;
+};
+
+__device__ __forceinline__ unsigned b64url_val(unsigned c) {
+  // A-Z 0-25, a-z 26-51, 0-9 52-61, '-' 62, '_' 63, else 0x100 (invalid)
+  if (c - 'A' < 26u) return c - 'A';
+  if (c - 'a' < 26u) return c - 'a' + 26;
+  if (c - '0' < 10u) return c - '0' + 52;
+  if (c == '-') return 62;
+  if (c == '_') return 63;
+  return 0x100;
+}
+
+// 4 chars (little-endian packed in a dword) -> 24 bits; bit 24+ set if invalid.
+__device__ __forceinline__ unsigned b64url_unit(unsigned w) {
+  const unsigned a = b64url_val(w & 0xFF), b = b64url_val((w >> 8) & 0xFF);
+  const unsigned c = b64url_val((w >> 16) & 0xFF), d = b64url_val(w >> 24);
+  return (a << 18) | (b << 12) | (c << 6) | d | ((a | b | c | d) & 0x100 ? 0x1000000u : 0u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_b64url_decode(const unsigned char* __restrict__ src,
+                                                          const B64Desc* __restrict__ descs,
+                                                          unsigned char* __restrict__ dst,
+                                                          int* __restrict__ err) {
+  const int m = blockIdx.y;
+  const B64Desc d = descs[m];
+  const unsigned char* s = src + d.src_off;
+  unsigned char* o = dst + d.dst_off;
+  const int64_t u0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;   // first unit of this lane
+  if (u0 > d.units) return;
+  unsigned bad = 0;
+  if (u0 + 4 <= d.units) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 w = *(const IPLS_GLOBAL u4*)(s + 4 * u0);
+    const unsigned v[4] = {b64url_unit(w.x), b64url_unit(w.y), b64url_unit(w.z), b64url_unit(w.w)};
+    bad = (v[0] | v[1] | v[2] | v[3]) & 0x1000000u;
+    unsigned char* q = o + 3 * u0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      q[3 * i] = (unsigned char)(v[i] >> 16);
+      q[3 * i + 1] = (unsigned char)(v[i] >> 8);
+      q[3 * i + 2] = (unsigned char)v[i];
+    }
+  } else {
+    for (int64_t u = u0; u < d.units; ++u) {
+      const unsigned char* c = s + 4 * u;
+      const unsigned w = c[0] | (c[1] << 8) | (c[2] << 16) | ((unsigned)c[3] << 24);
+      const unsigned v = b64url_unit(w);
+      bad |= v & 0x1000000u;
+      o[3 * u] = (unsigned char)(v >> 16);
+      o[3 * u + 1] = (unsigned char)(v >> 8);
+      o[3 * u + 2] = (unsigned char)v;
+    }
+    if (d.tail && u0 + 4 > d.units) {   // the lane that ends the full units does the tail
+      const unsigned char* c = s + 4 * d.units;
+      unsigned v = 0, inval = 0;
+      for (int i = 0; i < d.tail; ++i) {
+        const unsigned x = b64url_val(c[i]);
+        inval |= x;
+        v |= (x & 63u) << (18 - 6 * i);
+      }
+      bad |= inval & 0x100;
+      o[3 * d.units] = (unsigned char)(v >> 16);
+      if (d.tail == 3) o[3 * d.units + 1] = (unsigned char)(v >> 8);
+    }
+  }
+  if (bad) atomicOr(err + m, 1);
+}
+
 }  // namespace ipls

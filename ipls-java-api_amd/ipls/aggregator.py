@@ -193,6 +193,22 @@ class Aggregator:
         ptr, n, kind, keep = _operand(gradient)
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
 
+    def ingest_pubsub(self, messages, *, from_clients: bool = True, layers: int = 2, partitions=None):
+        """ThreadReceiver (IPLS.java:851-866, 453-465): a batch of pubsub
+        'data' texts -> base64url x layers -> GET_GRADIENTS frame -> fold, all
+        on the GPU.  Returns (number folded, per-message status)."""
+        msgs = [np.frombuffer(bytes(m), dtype=np.uint8) for m in messages]
+        n = len(msgs)
+        ptrs = (ctypes.c_void_p * max(1, n))(*[m.ctypes.data if m.size else None for m in msgs])
+        lens = (ctypes.c_int64 * max(1, n))(*[m.size for m in msgs])
+        st = (ctypes.c_int32 * max(1, n))()
+        parts = None
+        if partitions is not None:
+            parts = (ctypes.c_int32 * max(1, n))(*partitions)
+        target = N.TGT_AGG if from_clients else N.TGT_REP
+        k = self._chk(self._lib.ipls_agg_ingest_pubsub(self._h, target, ptrs, lens, n, layers, parts, st))
+        return k, list(st)[:n]
+
     def Collect_Replicas(self, partition: int, buckets):
         """IPLS.java:1217-1241: fold locally downloaded replica buckets into REP."""
         for b in buckets:

@@ -372,3 +372,75 @@ def c_updater_loop_parts(be_bufs, L: int, n_parts: int):
 def ethmodel_path() -> Path | None:
     p = Path(os.environ.get("IPLS_REFERENCE", "/root/reference")) / "MNIST_Partitioned_Dataset" / "ETHModel"
     return p if p.exists() else None
+
+
+# --------------------------------------------------------------------------
+# java.util.Base64 URL decoder (JDK 8+, RFC 4648 §5 alphabet, not MIME).
+# The reference decodes every pubsub message twice with
+# Base64.getUrlDecoder().decode (IPLS.java:855-859 + 399, Utils.java:14-15);
+# the JDK is absent here, so its published decoding rules are restated:
+#   * alphabet A-Z a-z 0-9 - _ ; any other byte -> IllegalArgumentException
+#   * '=' padding is optional; if present it must complete the 4-char unit
+#     ("xx==" or "xxx=") and nothing may follow it
+#   * a dangling single char in the last unit is an error
+#   * unused low bits of a partial last unit are ignored
+# Encoding (Base64.getUrlEncoder(), MyIPFSClass.java:986,1015) pads with '='.
+# --------------------------------------------------------------------------
+_B64URL = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
+_B64VAL = {c: i for i, c in enumerate(_B64URL)}
+
+
+class JavaIllegalArgument(ValueError):
+    pass
+
+
+def java_b64url_encode(data: bytes) -> bytes:
+    import base64
+    return base64.urlsafe_b64encode(bytes(data))
+
+
+def java_b64url_decode(src: bytes) -> bytes:
+    src = bytes(src)
+    out = bytearray()
+    bits = 0
+    shiftto = 18
+    sp, sl = 0, len(src)
+    while sp < sl:
+        b = src[sp]
+        sp += 1
+        if b == ord("="):
+            # "=" shiftto==18 unnecessary padding; "x=" shiftto==12; "xx=" needs a 2nd '='
+            if (shiftto == 6 and (sp == sl or src[sp] != ord("="))) or shiftto == 18:
+                raise JavaIllegalArgument("Input byte array has wrong 4-byte ending unit")
+            if shiftto == 6:
+                sp += 1
+            break
+        v = _B64VAL.get(b)
+        if v is None:
+            raise JavaIllegalArgument(f"Illegal base64 character {b:#x}")
+        bits |= v << shiftto
+        shiftto -= 6
+        if shiftto < 0:
+            out += bytes([(bits >> 16) & 0xFF, (bits >> 8) & 0xFF, bits & 0xFF])
+            shiftto = 18
+            bits = 0
+    if shiftto == 6:
+        out.append((bits >> 16) & 0xFF)
+    elif shiftto == 0:
+        out += bytes([(bits >> 16) & 0xFF, (bits >> 8) & 0xFF])
+    elif shiftto == 12:
+        raise JavaIllegalArgument("Last unit does not have enough valid bits")
+    if sp < sl:
+        raise JavaIllegalArgument("Input byte array has incorrect ending byte")
+    return bytes(out)
+
+
+def pubsub_message(frame: bytes) -> bytes:
+    """The 'data' text a receiver sees for a Marshall_Packet frame: the
+    packet is base64url'd by Marshall_Packet and decoded twice on receipt."""
+    return java_b64url_encode(java_b64url_encode(frame))
+
+
+def pubsub_decode(msg: bytes) -> bytes:
+    """ThreadReceiver.run + process (IPLS.java:855-859, 399)."""
+    return java_b64url_decode(java_b64url_decode(msg))

@@ -516,3 +516,76 @@ def test_many_partitions_small_buckets(ipls, O):
     exp = O.get_partitions([O.reduce([ref[k][p] for k in range(K)], agg.lengths[p]) for p in range(P)])
     assert_bits_equal(got, exp, "average")
     agg.close()
+
+
+def test_ingest_pubsub_double_base64(ipls, O):
+    """ThreadReceiver path on the GPU: pubsub 'data' texts (base64url of the
+    base64url of a Marshall_Packet frame) decoded, parsed and folded, routed
+    by the frame's partition field, in message order."""
+    M, P, K = 30011, 3, 4
+    agg = ipls.Aggregator(M, P)
+    peers = [O.synth_bucket(M, 2, k) for k in range(K)]
+    parts = [O.organize_gradients(g, M, P) for g in peers]
+    msgs = []
+    for k in range(K):
+        for p in range(P):
+            fr = O.frame_encode(parts[k][p], p, 17, 3, f"QmPeer{k}".encode())
+            m = O.pubsub_message(fr)
+            if k % 2:
+                m = m.rstrip(b"=")             # Java accepts unpadded text too
+            msgs.append(m)
+    n, st = agg.ingest_pubsub(msgs)
+    assert n == K * P and st == [0] * (K * P)
+    for p in range(P):
+        assert_bits_equal(agg.read(p), O.reduce([parts[k][p] for k in range(K)], agg.lengths[p]), f"p{p}")
+    agg.close()
+
+
+def test_ingest_pubsub_errors_dropped(ipls, O):
+    M, P = 1000, 2
+    agg = ipls.Aggregator(M, P)
+    L0 = agg.lengths[0]
+    g = O.synth_bucket(L0, 0, 0)
+    good = O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmA"))
+    bad_char = good[:10] + b"+" + good[11:]                    # '+' is not in the URL alphabet
+    bad_pad = good.rstrip(b"=") + b"="                          # wrong '=' tail (if it was unpadded)
+    inner = O.java_b64url_encode(O.frame_encode(g, 0, 1, 3, b"QmA"))
+    bad_inner = O.java_b64url_encode(inner[:5] + b"*" + inner[6:])
+    short = O.pubsub_message(O.frame_encode(g[:10], 0, 1, 3, b"QmA"))     # n < L_p
+    null = O.pubsub_message(O.frame_encode(None, 0, 1, 3, b"QmA"))         # arr_len 0 -> null
+    wrong_p = O.pubsub_message(O.frame_encode(g, 7, 1, 3, b"QmA"))         # partition 7 of 2
+    trunc = O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmA")[:20])      # n says more than it holds
+    msgs = [good, bad_char, bad_inner, short, null, wrong_p, trunc, good]
+    exp_ok = []
+    for m in msgs:
+        try:
+            fr = O.pubsub_decode(m)
+            pid, nn, a, b, gg, origin = O.frame_decode(fr)
+            exp_ok.append(gg is not None and 0 <= a < P and nn >= agg.lengths[a])
+        except ValueError:
+            exp_ok.append(False)
+    n, st = agg.ingest_pubsub(msgs)
+    assert n == 2 and [s == 0 for s in st] == exp_ok
+    assert st[1] == -6 and st[2] == -6 and st[3] == -2 and st[4] == 1 and st[5] == -2 and st[6] == -6
+    assert_bits_equal(agg.read(0), O.reduce([g, g], L0), "two good")
+    # bad_pad only differs when the text had no padding to begin with
+    n2, st2 = agg.ingest_pubsub([bad_pad])
+    try:
+        O.pubsub_decode(bad_pad)
+        assert st2 == [0]
+    except ValueError:
+        assert st2 == [-6] and n2 == 0
+    agg.close()
+
+
+def test_ingest_pubsub_single_layer_large(ipls, O):
+    """One base64 layer (Marshall_Packet text as published), 1M-double
+    payloads (vector decode path), replica frames routed by caller partitions."""
+    L = 1 << 20
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    bufs = [O.synth_bucket(L, 1, k) for k in range(3)]
+    msgs = [O.java_b64url_encode(O.frame_encode(b, 5, 2, 3, b"QmRep")) for b in bufs]
+    n, st = agg.ingest_pubsub(msgs, layers=1, partitions=[1, 1, 1], from_clients=False)
+    assert n == 3
+    assert_bits_equal(agg.read(1, ipls.TGT_REP), O.reduce(bufs, L), "replica frames")
+    agg.close()
