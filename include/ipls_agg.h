@@ -171,6 +171,15 @@ int ipls_agg_ingest_pubsub(ipls_agg *h, int target, const uint8_t *const *msgs,
                            const int64_t *lens, int n_msgs, int layers,
                            const int32_t *parts, int32_t *status);
 
+/* Variants (-async true / leaving peers):
+ *   blend: target[p][i] = a*target[p][i] + b*g[i]  (products rounded, then the sum)
+ *     async replica fold  a = 0.75, b = 1        Updater.java:57-59
+ *     leaving-peer blend  a = 0.6,  b = 1 - 0.6  Updater.java:65-69
+ *   scale: dst[p][i] = c * src[p][i]             Updater.java:197-199 (0.25 * W) */
+int ipls_agg_blend(ipls_agg *h, int p, int target, const void *src, int64_t n, int src_kind,
+                   double a, double b);
+int ipls_agg_scale(ipls_agg *h, int p, int dst_target, int src_target, double c);
+
 /* AggregatePartition (IPLS.java:1248-1274): W = AGG + REP, Weight_Address = W,
  * AGG = REP = 0.  p may be IPLS_ALL_PARTITIONS.  Optional host outputs for one
  * partition: sum_out (the commit_update file bytes, IPLS_Comm.java:27-37 ->
@@ -228,6 +237,11 @@ int ipls_synth_fill(void *dst, int64_t len, uint64_t seed, int p, int k, int dst
 
 /* Checksum (as above) of n device doubles (DEV_F64) or BE doubles (DEV_BE). */
 int ipls_checksum_dev(const void *src, int64_t n, int src_kind, uint64_t *out, void *stream);
+
+/* Middleware.Encode (secure mode, Middleware.java:196-210) on n device
+ * doubles: clip to +-10 then scale by 1e12 (dst may equal src). */
+int ipls_encode_secure(const void *src, void *dst, int64_t n, int src_kind, int dst_kind,
+                       void *stream);
 
 /* Pubsub frame header parse (MyIPFSClass.java:1437-1446 / 1462-1469).
  * Returns the number of doubles n, or IPLS_E_FORMAT. */

@@ -1187,6 +1187,67 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
   return folded;
 }
 
+int ipls_agg_blend(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind, double a, double b) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (!src) return IPLS_OK;
+  const int64_t L = h->len[p];
+  if (n < L) return fail(h, IPLS_E_RANGE, "bucket of %lld doubles shorter than partition length %lld", (long long)n, (long long)L);
+  HIP_TRY(h, hipSetDevice(h->device));
+  const void* d = src;
+  bool be = src_kind == IPLS_HOST_BE || src_kind == IPLS_DEV_BE;
+  if (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE) {
+    if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+    if (int rc = stage_h2d(h, h->d_scratch, src, (size_t)L * 8)) return rc;
+    d = h->d_scratch;
+  } else if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE) {
+    return fail(h, IPLS_E_INVAL, "bad src_kind %d", src_kind);
+  }
+  if (int rc = materialize(h, p, target)) return rc;
+  double* t = h->arena + target_off(h, p, target);
+  const dim3 g(std::min<unsigned>(blocks_for(L, kBlock), 8192));
+  if (be) hipLaunchKernelGGL(k_blend<true>, g, dim3(kBlock), 0, h->stream, t, (const unsigned long long*)d, L, a, b);
+  else hipLaunchKernelGGL(k_blend<false>, g, dim3(kBlock), 0, h->stream, t, (const unsigned long long*)d, L, a, b);
+  HIP_TRY(h, hipGetLastError());
+  return IPLS_OK;
+}
+
+int ipls_agg_scale(ipls_agg* h, int p, int dst_target, int src_target, double c) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, dst_target) < 0 || target_off(h, p, src_target) < 0) return fail(h, IPLS_E_INVAL, "bad target");
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (int rc = materialize(h, p, src_target)) return rc;
+  if (uint8_t* f = zero_flag(h, p, dst_target)) *f = 0;
+  const int64_t L = h->len[p];
+  hipLaunchKernelGGL(k_scale, dim3(std::min<unsigned>(blocks_for(L, kBlock), 8192)), dim3(kBlock), 0, h->stream,
+                     h->arena + target_off(h, p, dst_target), (const double*)(h->arena + target_off(h, p, src_target)), L, c);
+  HIP_TRY(h, hipGetLastError());
+  return IPLS_OK;
+}
+
+int ipls_encode_secure(const void* src, void* dst, int64_t n, int src_kind, int dst_kind, void* stream) {
+  if (!src || !dst || n < 0) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  if ((src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE) || (dst_kind != IPLS_DEV_F64 && dst_kind != IPLS_DEV_BE))
+    return fail(nullptr, IPLS_E_INVAL, "device operands only (DEV_F64 / DEV_BE)");
+  if (n == 0) return IPLS_OK;
+  const dim3 g(std::min<unsigned>(blocks_for(n, kBlock), 8192));
+  hipStream_t st = (hipStream_t)stream;
+  auto s = (const unsigned long long*)src;
+  auto d = (unsigned long long*)dst;
+  const bool bi = src_kind == IPLS_DEV_BE, bo = dst_kind == IPLS_DEV_BE;
+  if (bi && bo) hipLaunchKernelGGL((k_encode_secure<true, true>), g, dim3(kBlock), 0, st, s, d, n);
+  else if (bi) hipLaunchKernelGGL((k_encode_secure<true, false>), g, dim3(kBlock), 0, st, s, d, n);
+  else if (bo) hipLaunchKernelGGL((k_encode_secure<false, true>), g, dim3(kBlock), 0, st, s, d, n);
+  else hipLaunchKernelGGL((k_encode_secure<false, false>), g, dim3(kBlock), 0, st, s, d, n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(nullptr, IPLS_E_DEVICE, "k_encode_secure: %s", hipGetErrorString(e));
+  return IPLS_OK;
+}
+
 int ipls_host_alloc(size_t bytes, void** ptr) {
   if (!ptr) return fail(nullptr, IPLS_E_INVAL, "null ptr");
   *ptr = nullptr;

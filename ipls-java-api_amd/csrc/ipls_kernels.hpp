@@ -532,4 +532,44 @@ __global__ __launch_bounds__(kBlock) void k_b64url_decode(const unsigned char* _
   if (bad) atomicOr(err + m, 1);
 }
 
+// ---------------------------------------------------------------------------
+// Variants, each product rounded, then the sum rounded
+// (Java evaluates a*W + b*g left to right, no FMA; -ffp-contract=off here):
+//   k_blend : t[i] = a*t[i] + b*g[i]
+//             async replica fold  a=0.75, b=1      (Updater.java:57-59)
+//             leaving-peer blend  a=0.6,  b=1-0.6  (Updater.java:65-69)
+//   k_scale : d[i] = c*s[i]        async publish 0.25*W (Updater.java:197-199)
+//   k_encode_secure : Middleware.Encode (Middleware.java:196-210):
+//             x > 10 -> 10*1e12, x < -10 -> -10*1e12, else x*1e12
+// ---------------------------------------------------------------------------
+template <bool BE_IN>
+__global__ __launch_bounds__(kBlock) void k_blend(double* __restrict__ t, const unsigned long long* __restrict__ g,
+                                                  int64_t L, double a, double b) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < L; i += (int64_t)gridDim.x * kBlock) {
+    const double x = decode1<BE_IN>(ld8(g + i));
+    const double aw = a * t[i];
+    const double bg = b * x;
+    t[i] = aw + bg;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scale(double* __restrict__ d, const double* __restrict__ s, int64_t L,
+                                                  double c) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < L; i += (int64_t)gridDim.x * kBlock)
+    d[i] = c * s[i];
+}
+
+template <bool BE_IN, bool BE_OUT>
+__global__ __launch_bounds__(kBlock) void k_encode_secure(const unsigned long long* __restrict__ src,
+                                                          unsigned long long* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double x = decode1<BE_IN>(ld8(src + i));
+    double y;
+    if (x > 10.0) y = 10 * 1e12;
+    else if (x < -10.0) y = -10 * 1e12;
+    else y = x * 1e12;
+    st8(dst + i, BE_OUT ? f64_to_be(y) : __builtin_bit_cast(unsigned long long, y));
+  }
+}
+
 }  // namespace ipls

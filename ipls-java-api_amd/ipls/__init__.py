@@ -11,7 +11,7 @@ from ._native import (  # noqa: F401
     IplsError, lib,
 )
 from .aggregator import (  # noqa: F401
-    Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, frame_encode, frame_parse, synth_fill,
+    Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, encode_secure, frame_encode, frame_parse, synth_fill,
 )
 
 SEED = 0x1B5_2026  # synthetic workload seed

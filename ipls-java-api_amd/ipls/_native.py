@@ -76,6 +76,8 @@ SIGNATURES = {
     "ipls_agg_reduce_batch": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _i]),
     "ipls_agg_reduce_batch_out": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _P(_vp), _i]),
     "ipls_agg_ingest_pubsub": (_i, [_vp, _i, _P(_vp), _P(_i64), _i, _i, _P(_i32), _P(_i32)]),
+    "ipls_agg_blend": (_i, [_vp, _i, _i, _vp, _i64, _i, ctypes.c_double, ctypes.c_double]),
+    "ipls_agg_scale": (_i, [_vp, _i, _i, _i, ctypes.c_double]),
     "ipls_agg_finalize": (_i, [_vp, _i, _vp, _i, _P(ctypes.c_double)]),
     "ipls_agg_set_weights": (_i, [_vp, _i, _vp, _i64, _i]),
     "ipls_agg_get_partitions": (_i, [_vp, _vp, _i64, _i]),
@@ -89,6 +91,7 @@ SIGNATURES = {
     "ipls_host_free": (_i, [_vp]),
     "ipls_synth_fill": (_i, [_vp, _i64, _u64, _i, _i, _i, _vp]),
     "ipls_checksum_dev": (_i, [_vp, _i64, _i, _P(_u64), _vp]),
+    "ipls_encode_secure": (_i, [_vp, _vp, _i64, _i, _i, _vp]),
     "ipls_frame_parse": (_i64, [_vp, _i64, _P(_i16), _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
     "ipls_frame_encode": (_i64, [_vp, _i64, _i, _i32, _i32, _i16, _vp, _i32, _vp, _i64]),
 }

@@ -209,6 +209,25 @@ class Aggregator:
         k = self._chk(self._lib.ipls_agg_ingest_pubsub(self._h, target, ptrs, lens, n, layers, parts, st))
         return k, list(st)[:n]
 
+    # ---- -async true variants (Updater.java:57-69, 197-199) ----
+    ASYNC_DECAY = 0.75      # Updater.java:58
+    LEAVING_A = 0.6         # Updater.java:17 (field a)
+
+    def UpdateAsyncReplica(self, gradient, partition: int):
+        """Async replica fold: W = 0.75*W + g (Updater.java:57-59)."""
+        ptr, n, kind, keep = _operand(gradient)
+        self._chk(self._lib.ipls_agg_blend(self._h, partition, N.TGT_WEIGHTS, ptr, n, kind, 0.75, 1.0))
+
+    def UpdateLeavingPeer(self, weights, partition: int):
+        """Leaving peer's weights: W = a*W + (1-a)*w, a = 0.6 (Updater.java:65-69)."""
+        a = self.LEAVING_A
+        ptr, n, kind, keep = _operand(weights)
+        self._chk(self._lib.ipls_agg_blend(self._h, partition, N.TGT_WEIGHTS, ptr, n, kind, a, 1 - a))
+
+    def AsyncPublishScale(self, partition: int):
+        """Aggregated = 0.25*Weights before the async publish (Updater.java:197-199)."""
+        self._chk(self._lib.ipls_agg_scale(self._h, partition, N.TGT_AGG, N.TGT_WEIGHTS, 0.25))
+
     def Collect_Replicas(self, partition: int, buckets):
         """IPLS.java:1217-1241: fold locally downloaded replica buckets into REP."""
         for b in buckets:
@@ -370,6 +389,11 @@ def checksum_dev(buf: DeviceBuffer, n: int | None = None, stream: int = 0) -> in
     N.check(N.lib().ipls_checksum_dev(buf.ptr, buf.n if n is None else n, buf.kind,
                                       ctypes.byref(v), stream or None))
     return int(v.value)
+
+
+def encode_secure(src: DeviceBuffer, dst: DeviceBuffer, stream: int = 0):
+    """Middleware.Encode (Middleware.java:196-210) on the device."""
+    N.check(N.lib().ipls_encode_secure(src.ptr, dst.ptr, min(src.n, dst.n), src.kind, dst.kind, stream or None))
 
 
 def frame_parse(frame: bytes):

@@ -136,6 +136,18 @@ def encode_secure(x) -> np.ndarray:
     return out
 
 
+def blend(w, g, a: float, b: float) -> np.ndarray:
+    """W[i] = a*W[i] + b*G[i]: Updater.java:58 (a=0.75, b=1) and 67 (a=0.6, b=1-a)."""
+    w = np.asarray(w, dtype=np.float64)
+    g = np.asarray(g[:len(w)], dtype=np.float64)
+    return (a * w) + (b * g)
+
+
+def scale(w, c: float) -> np.ndarray:
+    """Updater.java:198: Aggregated[i] = 0.25*Weights[i]."""
+    return c * np.asarray(w, dtype=np.float64)
+
+
 # --------------------------------------------------------------------------
 # byte codecs
 # --------------------------------------------------------------------------

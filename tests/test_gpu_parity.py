@@ -589,3 +589,29 @@ def test_ingest_pubsub_single_layer_large(ipls, O):
     assert n == 3
     assert_bits_equal(agg.read(1, ipls.TGT_REP), O.reduce(bufs, L), "replica frames")
     agg.close()
+
+
+def test_async_variants(ipls, O):
+    """-async true branches: W = 0.75*W + g, leaving-peer W = 0.6*W + (1-0.6)*w,
+    and the 0.25*W publish scale -- each product rounded, then the sum."""
+    L = 20011
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    w0 = O.synth_bucket(L, 3, 0) * 37.0
+    agg.cache_partition(0, w0)
+    g1, g2 = O.synth_bucket(L, 3, 1), O.synth_bucket(L, 3, 2)
+    agg.UpdateAsyncReplica(g1, 0)
+    agg.UpdateLeavingPeer(O.be_encode(g2), 0)
+    w = O.blend(O.blend(w0, g1, 0.75, 1.0), g2, 0.6, 1 - 0.6)
+    assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), w, "blends")
+    agg.AsyncPublishScale(0)
+    assert_bits_equal(agg.read(0, ipls.TGT_AGG), O.scale(w, 0.25), "scale")
+    agg.close()
+
+
+def test_encode_secure_device(ipls, O, golden):
+    x = golden["enc_in"]
+    t, d = dev(x)
+    o = torch.empty(8 * len(x), dtype=torch.uint8, device="cuda")
+    ipls.encode_secure(d, ipls.DeviceBuffer(int(o.data_ptr()), len(x), big_endian=True))
+    torch.cuda.synchronize()
+    assert bytes(o.cpu().numpy()) == O.be_encode(golden["enc_out"])
