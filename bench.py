@@ -241,6 +241,32 @@ def main():
             got = agg.checksum(0)
         verified = got == O.c_synth_sum_checksum(L, p0, K)
 
+    # the rest of an aggregation round on the same handle, one launch each:
+    # AggregatePartition for all partitions (k_finalize: read AGG, write W ->
+    # 16 B/element) and GetPartitions into a device buffer (k_divide: read W,
+    # write the flat model -> 16 B/element)
+    round_info = None
+    if not args.be:
+        flat = torch.empty(P * (L - 1), dtype=torch.float64, device="cuda")
+        fb = ipls.DeviceBuffer.from_tensor(flat)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+        e[0].record(stream)
+        agg.AggregatePartition(ipls.ALL_PARTITIONS)
+        e[1].record(stream)
+        agg.GetPartitions(out=fb)
+        e[2].record(stream)
+        agg.sync()
+        fin_ms, div_ms = e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2])
+        n_el = P * L
+        round_info = {
+            "finalize_ms": round(fin_ms, 4), "finalize_GBps": round(16 * n_el / fin_ms / 1e6, 1),
+            "divide_ms": round(div_ms, 4), "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
+            "round_ms": round(kern_ms + fin_ms + div_ms, 4),
+            "note": "one aggregation round on device: reduce (K buckets) + AggregatePartition(all) + GetPartitions",
+        }
+        del flat
+
     out = None
     if rank == 0:
         achieved = bytes_step / (kern_ms / 1e3) / 1e9
@@ -278,6 +304,8 @@ def main():
             },
             "verified_checksum_p0": verified,
         }
+        if round_info:
+            out["round"] = round_info
         if world == 1 and not args.no_e2e:
             out["host_inclusive"] = host_inclusive(ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_cpu_baseline:

@@ -726,7 +726,7 @@ int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* a
   }
   void* dtab = nullptr;
   if (int rc = upload_table(h, fd.data(), fd.size() * sizeof(FinDesc), &dtab)) return rc;
-  const int64_t tile = (int64_t)kBlock * 8;
+  const int64_t tile = (int64_t)kBlock * 8;  // == k_finalize / k_divide tile (256 lanes x 2 x 4)
   const int tpp = (int)((maxL + tile - 1) / tile);
   // AGG/REP are left in place and flagged logically zero (IPLS.java:1268-1269
   // zeroes them; the next fold starts from +0.0 without reading them).

@@ -263,7 +263,9 @@ template <bool REP_ZERO, bool ZERO_ACC>
 __global__ __launch_bounds__(kBlock) void k_finalize(const FinDesc* __restrict__ parts,
                                                      double* __restrict__ arena,
                                                      int tiles_per_part) {
-  constexpr int64_t kTile = (int64_t)kBlock * 8;
+  // 16 B per lane per step (arena arrays are 256-B aligned), 4 steps per lane.
+  constexpr int kV = 4;
+  constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
   const int q = blockIdx.x / tiles_per_part;
   const int t = blockIdx.x - q * tiles_per_part;
   const FinDesc d = parts[q];
@@ -273,6 +275,30 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const FinDesc* __restrict__
   double* agg = arena + d.agg_off;
   double* rep = arena + d.rep_off;
   double* w = arena + d.w_off;
+  if (end - base == kTile) {
+    u2 a[kV], r[kV];
+#pragma unroll
+    for (int v = 0; v < kV; ++v) {
+      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      a[v] = __builtin_nontemporal_load((gcu2)(agg + i));
+      if constexpr (!REP_ZERO) r[v] = __builtin_nontemporal_load((gcu2)(rep + i));
+    }
+#pragma unroll
+    for (int v = 0; v < kV; ++v) {
+      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      const d2 x = __builtin_bit_cast(d2, a[v]);
+      const d2 y = REP_ZERO ? d2{0.0, 0.0} : __builtin_bit_cast(d2, r[v]);
+      d2 o;
+      o.x = x.x + y.x;
+      o.y = x.y + y.y;
+      *(gu2)(w + i) = __builtin_bit_cast(u2, o);
+      if constexpr (ZERO_ACC) {
+        *(gu2)(agg + i) = u2{0, 0};
+        if constexpr (!REP_ZERO) *(gu2)(rep + i) = u2{0, 0};
+      }
+    }
+    return;
+  }
   for (int64_t i = base + threadIdx.x; i < end; i += kBlock) {
     const double a = agg[i];
     const double r = REP_ZERO ? 0.0 : rep[i];
@@ -301,28 +327,51 @@ __global__ __launch_bounds__(kBlock) void k_divide(const DivDesc* __restrict__ p
                                                    const double* __restrict__ arena,
                                                    unsigned long long* __restrict__ out,
                                                    int tiles_per_part) {
-  constexpr int64_t kTile = (int64_t)kBlock * 8;
+  // W reads are 16-B aligned; the flat output offset p*chunk is arbitrary, so
+  // each lane stores the element pair that is aligned in the OUTPUT and reads
+  // its two W values with 8-B loads.
+  constexpr int kV = 4;
+  constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
   const int q = blockIdx.x / tiles_per_part;
   const int t = blockIdx.x - q * tiles_per_part;
   const DivDesc d = parts[q];
   const int64_t n = d.len - 1;
-  const int64_t base = (int64_t)t * kTile;
-  if (base >= n) return;
-  const int64_t end = (base + kTile < n) ? base + kTile : n;
   const double* w = arena + d.w_off;
   const double cnt = w[d.len - 1];
   // Math.pow(10,12) * W[last] (IPLS.java:1167): 1e12 is exact, product rounded once.
   const double den = SECURE ? 1e12 * cnt : cnt;
-  for (int64_t i = base + threadIdx.x; i < end; i += kBlock) {
-    const double x = w[i];
+  auto f = [&](double x) -> unsigned long long {
     const double y = (cnt == 0.0) ? x : x / den;
     unsigned long long bits = __builtin_bit_cast(unsigned long long, y);
     if constexpr (OUT_BE) {
       if (y != y) bits = 0x7ff8000000000000ULL;
       bits = __builtin_bswap64(bits);
     }
-    out[d.out_off + i] = bits;
+    return bits;
+  };
+  const int64_t shift = (d.out_off & 1);         // first element whose output index is even
+  const int64_t base = (int64_t)t * kTile + shift;
+  if (t == 0 && shift && threadIdx.x == 0 && n > 0) out[d.out_off] = f(w[0]);
+  if (base >= n) return;
+  if (base + kTile <= n) {
+    double x[kV][2];
+#pragma unroll
+    for (int v = 0; v < kV; ++v) {
+      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      x[v][0] = w[i];
+      x[v][1] = w[i + 1];
+    }
+#pragma unroll
+    for (int v = 0; v < kV; ++v) {
+      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      u2 o;
+      o.x = f(x[v][0]);
+      o.y = f(x[v][1]);
+      *(gu2)(out + d.out_off + i) = o;
+    }
+    return;
   }
+  for (int64_t i = base + threadIdx.x; i < n; i += kBlock) out[d.out_off + i] = f(w[i]);
 }
 
 // ---------------------------------------------------------------------------

@@ -95,14 +95,18 @@ int main(int argc, char** argv) {
   int64_t off = 0;
   for (int p = 0; p < P; ++p) {
     pd[p].len = L;
-    pd[p].dst_off = off;
+    pd[p].dst = nullptr;  // set below, once dst is allocated
     off += (L + 31) / 32 * 32;
+  }
+  unsigned long long* dst;
+  CK(hipMalloc(&dst, (size_t)off * 8));
+  for (int p = 0, o = 0; p < P; ++p) {
+    pd[p].dst = dst + o;
+    o += (int)((L + 31) / 32 * 32);
   }
   PartDesc* d_pd;
   CK(hipMalloc(&d_pd, P * sizeof(PartDesc)));
   CK(hipMemcpy(d_pd, pd.data(), P * sizeof(PartDesc), hipMemcpyHostToDevice));
-  unsigned long long* dst;
-  CK(hipMalloc(&dst, (size_t)off * 8));
   unsigned long long* sink;
   CK(hipMalloc(&sink, 64));
   unsigned long long* copy_out;
@@ -113,25 +117,27 @@ int main(int argc, char** argv) {
 
   const double alg = (double)P * (K + 1) * L * 8;
   std::vector<Var> vars;
-#define ADD(G, R, NT, MAP)                                                                     \
-  vars.push_back(Var{"reduce G=" #G " R=" #R " NT=" #NT " MAP=" #MAP,                           \
+#define ADDL(G, R, MAP, LDS)                                                                   \
+  vars.push_back(Var{"reduce G=" #G " R=" #R " MAP=" #MAP " lds=" #LDS,                          \
                      [=](hipStream_t s) {                                                       \
                        const int64_t tile = (int64_t)kBlock * 2 * R;                            \
                        const int tpp = (int)((L + tile - 1) / tile);                            \
-                       hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, NT, MAP>),       \
-                                          dim3((unsigned)grid_blocks(MAP, (int64_t)tpp * P)), dim3(kBlock), 0, s, \
-                                          (const unsigned long long* const*)d_ptrs, d_pd, dst, K, tpp, P); \
+                       hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, true, MAP>),     \
+                                          dim3((unsigned)grid_blocks(MAP, (int64_t)tpp * P)), dim3(kBlock), LDS, s, \
+                                          (const unsigned long long* const*)d_ptrs, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
-  ADD(8, 1, true, 0);
-  ADD(8, 1, true, 2);
-  ADD(2, 8, true, 2);
-  ADD(1, 16, true, 0);
-  ADD(1, 16, true, 2);
-  ADD(2, 16, true, 0);
-  ADD(2, 16, true, 2);
-  ADD(1, 32, true, 2);
-#undef ADD
+  ADDL(1, 16, 2, 0);
+  ADDL(1, 16, 2, 50000);    // <= 3 blocks / CU
+  ADDL(1, 16, 2, 70000);    // <= 2 blocks / CU
+  ADDL(1, 16, 2, 100000);   // 1 block / CU
+  ADDL(2, 8, 2, 0);
+  ADDL(2, 8, 2, 40000);     // <= 4 blocks / CU
+  ADDL(2, 8, 2, 70000);     // <= 2 blocks / CU
+  ADDL(8, 1, 2, 0);
+  ADDL(8, 1, 2, 20000);     // <= 8 blocks / CU
+  ADDL(8, 1, 2, 40000);     // <= 4 blocks / CU
+#undef ADDL
 #define RA(G, R)                                                                                   \
   vars.push_back(Var{"readall G=" #G " R=" #R " (read ceiling)",                                     \
                      [=](hipStream_t s) {                                                            \
