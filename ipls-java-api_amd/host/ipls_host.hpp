@@ -1,0 +1,304 @@
+// ipls_host.hpp -- C++17 host-side mirror of the reference's aggregation path
+// over the C-ABI (include/ipls_agg.h).  Header-only.
+//
+// The reference is Java (no JDK in this image), so the host layer above the
+// C-ABI mirrors its classes in C++ under the same names, with the same
+// argument meaning and the same exceptions:
+//
+//   IPLS                 IPLS.java:880-2305  (aggregation methods only)
+//   Updater              Updater.java:14-218 (_Update)
+//   Light_IPLS_Daemon    Light_IPLS_Daemon.java:9-114 (UpdateModel / Get_Partitions)
+//   MyIPFSClass          MyIPFSClass.java codecs used on the path
+//   Middleware           Middleware.java:26-210 (flags, wire stream, Encode)
+//
+// Every arithmetic loop runs in the HIP library; nothing here computes on
+// doubles.  Negative C-ABI codes become the Java exception the reference
+// throws at the same spot (ArrayIndexOutOfBoundsException, ...).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ipls_agg.h"
+
+namespace ipls_host {
+
+// ---- Java exceptions -------------------------------------------------------
+struct JavaException : std::runtime_error {
+  int code;
+  JavaException(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+  virtual const char* java_name() const { return "java.lang.RuntimeException"; }
+};
+#define IPLS_HOST_EXC(NAME, JNAME)                                           \
+  struct NAME : JavaException {                                              \
+    using JavaException::JavaException;                                      \
+    const char* java_name() const override { return JNAME; }                 \
+  };
+IPLS_HOST_EXC(ArrayIndexOutOfBoundsException, "java.lang.ArrayIndexOutOfBoundsException")
+IPLS_HOST_EXC(NegativeArraySizeException, "java.lang.NegativeArraySizeException")
+IPLS_HOST_EXC(BufferUnderflowException, "java.nio.BufferUnderflowException")
+IPLS_HOST_EXC(IllegalArgumentException, "java.lang.IllegalArgumentException")
+IPLS_HOST_EXC(OutOfMemoryError, "java.lang.OutOfMemoryError")
+IPLS_HOST_EXC(DeviceError, "ipls.DeviceError")
+#undef IPLS_HOST_EXC
+
+[[noreturn]] inline void raise(int rc, const ipls_agg* h) {
+  const std::string msg = ipls_agg_last_error(h);
+  switch (rc) {
+    case IPLS_E_RANGE: throw ArrayIndexOutOfBoundsException(rc, msg);
+    case IPLS_E_NEGSIZE: throw NegativeArraySizeException(rc, msg);
+    case IPLS_E_FORMAT: throw BufferUnderflowException(rc, msg);
+    case IPLS_E_INVAL: throw IllegalArgumentException(rc, msg);
+    case IPLS_E_NOMEM: throw OutOfMemoryError(rc, msg);
+    default: throw DeviceError(rc, msg);
+  }
+}
+inline int64_t check(int64_t rc, const ipls_agg* h) {
+  if (rc < 0) raise((int)rc, h);
+  return rc;
+}
+
+// ---- PeerData: the configuration the path reads (PeerData.java) -------------
+struct PeerData {
+  int64_t _MODEL_SIZE = 0;          // IPLS(..., long model_size)
+  int _PARTITIONS = 1;              // -pa
+  int _MIN_PARTITIONS = 1;          // -mp
+  int Min_Members = 1;              // -n
+  bool Indirect_Communication = false;  // -i
+  bool Partial_Aggregation = false;     // -aggr
+  bool IPNS_Enable = false;             // -IPNS
+  bool isSynchronous = true;            // -async
+  int Training_time = 0;                // -training
+  int port = 0;                         // -p
+  bool secure_ipls = false;             // PeerData.java:62 (hard-coded false)
+  int device = 0;                       // HIP device ordinal
+};
+
+// ---- Middleware (Middleware.java) ------------------------------------------
+struct Middleware {
+  // parse_arguments (Middleware.java:26-110): required -p -pa -mp -n -i
+  // -training -aggr; optional -IPNS -async.  Missing/invalid -> throws
+  // IllegalArgumentException (Middleware prints help and exits 1).
+  static PeerData parse_arguments(const std::vector<std::string>& args) {
+    struct Flag { const char* s; const char* l; bool req; };
+    static const Flag flags[] = {{"p", "port_number", true}, {"pa", "partitions", true},
+                                 {"mp", "minimum_partitions", true}, {"n", "min_peers", true},
+                                 {"i", "indirect_communication", true}, {"training", "training", true},
+                                 {"aggr", "partial_aggregation", true}, {"IPNS", "IPNS", false},
+                                 {"async", "Async", false}};
+    std::map<std::string, std::string> v;
+    for (size_t i = 0; i < args.size(); ++i) {
+      std::string a = args[i];
+      if (a.empty() || a[0] != '-') continue;
+      a = a.substr(a.find_first_not_of('-'));
+      const Flag* f = nullptr;
+      for (const auto& fl : flags)
+        if (a == fl.s || a == fl.l) f = &fl;
+      if (!f || i + 1 >= args.size()) throw IllegalArgumentException(IPLS_E_INVAL, "Unrecognized option: " + args[i]);
+      v[f->s] = args[++i];
+    }
+    for (const auto& fl : flags)
+      if (fl.req && !v.count(fl.s)) throw IllegalArgumentException(IPLS_E_INVAL, std::string("Missing required option: ") + fl.s);
+    auto num = [&](const char* k) {
+      try {
+        size_t pos = 0;
+        const int x = std::stoi(v[k], &pos);
+        if (pos != v[k].size()) throw std::invalid_argument(k);
+        return x;
+      } catch (const std::exception&) {
+        throw IllegalArgumentException(IPLS_E_INVAL, std::string("NumberFormatException for -") + k);
+      }
+    };
+    PeerData d;
+    d.port = num("p");
+    d._PARTITIONS = num("pa");
+    d._MIN_PARTITIONS = num("mp");
+    d.Min_Members = num("n");
+    d.Indirect_Communication = num("i") > 0;
+    d.Training_time = num("training");
+    d.Partial_Aggregation = num("aggr") > 0;
+    d.IPNS_Enable = v.count("IPNS") && v["IPNS"] == "true";
+    d.isSynchronous = !(v.count("async") && v["async"] == "true");
+    return d;
+  }
+
+  // Serialize (Middleware.java:164-170): the task-3 writeDouble stream.
+  static std::vector<uint8_t> Serialize_wire_from(ipls_agg* h, int64_t model_size) {
+    std::vector<uint8_t> out(8 * (size_t)model_size);
+    check(ipls_agg_get_partitions(h, out.data(), model_size, IPLS_HOST_BE_CANON), h);
+    return out;
+  }
+};
+
+// ---- MyIPFSClass codecs on the path ---------------------------------------------
+struct MyIPFSClass {
+  // Marshall_Packet(double[], origin, partition, iteration, pid) before base64
+  // (MyIPFSClass.java:990-1017).
+  static std::vector<uint8_t> Marshall_Packet(const std::vector<double>& g, const std::string& origin,
+                                              int partition, int iteration, int16_t pid) {
+    std::vector<uint8_t> out(14 + 8 * g.size() + origin.size());
+    check(ipls_frame_encode(g.data(), (int64_t)g.size(), IPLS_HOST_F64, partition, iteration, pid,
+                            (const uint8_t*)origin.data(), (int32_t)origin.size(), out.data(), (int64_t)out.size()),
+          nullptr);
+    return out;
+  }
+  struct Frame { int16_t pid; int64_t n; int32_t partition, iteration; int64_t payload_off, origin_off; };
+  // GET_GRADIENTS header (MyIPFSClass.java:1437-1446) -- the payload is
+  // folded on the device, never decoded here.
+  static Frame GET_GRADIENTS(const std::vector<uint8_t>& frame) {
+    Frame f{};
+    f.n = check(ipls_frame_parse(frame.data(), (int64_t)frame.size(), &f.pid, &f.partition, &f.iteration,
+                                 &f.payload_off, &f.origin_off),
+                nullptr);
+    return f;
+  }
+};
+
+// ---- IPLS: the aggregation methods of IPLS.java ----------------------------------
+class IPLS {
+ public:
+  explicit IPLS(const PeerData& pd, std::vector<int> auth_list = {}) : cfg_(pd), Auth_List(std::move(auth_list)) {
+    ipls_agg_cfg c{};
+    c.model_size = pd._MODEL_SIZE;
+    c.n_partitions = pd._PARTITIONS;
+    c.max_peers = pd.Min_Members;
+    c.partial_aggregation = pd.Partial_Aggregation;
+    c.secure = pd.secure_ipls;
+    c.device = pd.device;
+    ipls_agg* h = nullptr;
+    const int rc = ipls_agg_open(&c, &h);   // init() -> InitializeWeights() (IPLS.java:1860)
+    if (rc < 0) raise(rc, nullptr);
+    h_.reset(h);
+  }
+  ipls_agg* handle() const { return h_.get(); }
+  int64_t partition_length(int p) const {
+    int64_t L = 0;
+    check(ipls_agg_partition_len(h_.get(), p, &L), h_.get());
+    return L;
+  }
+
+  // InitializeWeights(List<Double> Model) -- IPLS.java:1880-1901
+  void InitializeWeights(const std::vector<double>& Model) {
+    check(ipls_agg_load_model(h_.get(), Model.data(), (int64_t)Model.size(), IPLS_HOST_F64), h_.get());
+  }
+
+  // OrganizeGradients -- IPLS.java:1018-1040
+  std::map<int, std::vector<double>> OrganizeGradients(const std::vector<double>& Gradients) const {
+    std::map<int, std::vector<double>> out;
+    for (int p = 0; p < cfg_._PARTITIONS; ++p) {
+      std::vector<double> part((size_t)partition_length(p));
+      check(ipls_agg_split(h_.get(), Gradients.data(), (int64_t)Gradients.size(), IPLS_HOST_F64, p, part.data(),
+                           IPLS_HOST_F64),
+            h_.get());
+      out.emplace(p, std::move(part));
+    }
+    return out;
+  }
+
+  // UpdateGradient (IPLS.java:1703): the own-partition accumulate of
+  // 1737-1743.  nullptr = "did not train in time" (Gradients == null).
+  void UpdateGradient(const std::vector<double>* Gradients) {
+    if (!Gradients) return;
+    check(ipls_agg_update_gradient(h_.get(), Gradients->data(), (int64_t)Gradients->size(), IPLS_HOST_F64,
+                                   Auth_List.data(), (int)Auth_List.size()),
+          h_.get());
+  }
+
+  // Collect_Replicas (IPLS.java:1217-1241): fold a missing replica's
+  // downloaded buckets into Replicas_Gradients.
+  void Collect_Replicas(int Partition, const std::vector<double>& Other_Replica_Gradient) {
+    check(ipls_agg_accumulate(h_.get(), Partition, IPLS_TGT_REP, Other_Replica_Gradient.data(),
+                              (int64_t)Other_Replica_Gradient.size(), IPLS_HOST_F64),
+          h_.get());
+  }
+
+  // AggregatePartition (IPLS.java:1248-1274); returns the update_file bytes
+  // commit_update publishes (IPLS_Comm.java:27-37).
+  std::vector<uint8_t> AggregatePartition(int Partition) {
+    std::vector<uint8_t> file(8 * (size_t)partition_length(Partition));
+    check(ipls_agg_finalize(h_.get(), Partition, file.data(), IPLS_HOST_BE, nullptr), h_.get());
+    return file;
+  }
+
+  // Download_Scheduler.cache_partition (:752-754): Weight_Address[p] = GetParameters(hash)
+  void cache_partition(int Partition, const std::vector<uint8_t>& file_bytes) {
+    check(ipls_agg_set_weights(h_.get(), Partition, file_bytes.data(), (int64_t)file_bytes.size() / 8, IPLS_HOST_BE),
+          h_.get());
+  }
+
+  // GetPartitions (IPLS.java:1080-1178), the synchronous steady-state branch.
+  std::vector<double> GetPartitions() const {
+    std::vector<double> out((size_t)cfg_._MODEL_SIZE);
+    check(ipls_agg_get_partitions(h_.get(), out.data(), (int64_t)out.size(), IPLS_HOST_F64), h_.get());
+    return out;
+  }
+
+  const PeerData& peer_data() const { return cfg_; }
+
+ private:
+  struct Closer {
+    void operator()(ipls_agg* h) const { ipls_agg_close(h); }
+  };
+  PeerData cfg_;
+  std::unique_ptr<ipls_agg, Closer> h_;
+
+ public:
+  std::vector<int32_t> Auth_List;   // PeerData.Auth_List: partitions this peer aggregates
+};
+
+// ---- Updater (Updater.java) -----------------------------------------------------
+class Updater {
+ public:
+  explicit Updater(IPLS& ipls) : ipls_(ipls) {}
+  // _Update(double[] Gradient, int Partition, List<String> Origin, int
+  // iteration, boolean from_clients) -- the synchronous folds
+  // (Updater.java:40-44 replicas, 115-117 clients).
+  void _Update(const std::vector<double>* Gradient, int Partiton, bool from_clients) {
+    if (!Gradient) return;   // `&& Gradient != null` in every loop
+    check(ipls_agg_accumulate(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
+                              Gradient->data(), (int64_t)Gradient->size(), IPLS_HOST_F64),
+          ipls_.handle());
+  }
+  // run(): a queue item with a hash and no payload -- GetParameters(hash,
+  // Gradient_Buff) then _Update (Updater.java:176-187).  The BE decode is
+  // fused into the device fold.
+  void _Update_from_file(const std::vector<uint8_t>& ipfs_cat_bytes, int Partiton, bool from_clients) {
+    check(ipls_agg_accumulate(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
+                              ipfs_cat_bytes.data(), (int64_t)ipfs_cat_bytes.size() / 8, IPLS_HOST_BE),
+          ipls_.handle());
+  }
+  // ThreadReceiver pid 3 -> queue -> _Update (IPLS.java:453-465): a decoded frame.
+  void _Update_from_frame(const std::vector<uint8_t>& frame, int Partiton, bool from_clients) {
+    check(ipls_agg_accumulate(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP, frame.data(),
+                              (int64_t)frame.size(), IPLS_HOST_FRAME),
+          ipls_.handle());
+  }
+
+ private:
+  IPLS& ipls_;
+};
+
+// ---- Light_IPLS_Daemon (Light_IPLS_Daemon.java) -----------------------------------
+// The blocking API pair the Middleware calls.  One round here = the daemon
+// loop's UpdateGradient for this peer's own partitions, the arrivals the
+// Updater folded, then AggregatePartition for Auth_List and GetPartitions.
+class Light_IPLS_Daemon {
+ public:
+  explicit Light_IPLS_Daemon(IPLS& ipls) : ipls_(ipls) {}
+  void UpdateModel(const std::vector<double>& Gradients) { ipls_.UpdateGradient(&Gradients); }
+  std::vector<double> Get_Partitions() {
+    for (int p : ipls_.Auth_List) ipls_.AggregatePartition(p);
+    return ipls_.GetPartitions();
+  }
+
+ private:
+  IPLS& ipls_;
+};
+
+}  // namespace ipls_host

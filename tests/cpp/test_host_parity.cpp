@@ -1,0 +1,222 @@
+// test_host_parity.cpp -- parity of the C++ host mirror (ipls_host.hpp) over
+// the HIP C-ABI, against the C oracle (oracle/ipls_oracle.c, linked as the
+// checker only).  Each TEST reads like the Java flow it mirrors.
+//
+//   test_host_parity            -> all tests (needs a GPU)
+//   test_host_parity --no-gpu   -> the host-only tests (flags, frame codec)
+//
+// ETHModel (config A) is read from tests/golden/ethmodel.f64be.gz via zlib.
+#include <zlib.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "ipls_host.hpp"
+#include "ipls_oracle.h"
+
+using namespace ipls_host;
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(cond, what)                                                        \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      std::fprintf(stderr, "  FAIL %s:%d %s\n", __FILE__, __LINE__, what);       \
+      throw std::runtime_error(what);                                            \
+    }                                                                            \
+  } while (0)
+
+static void run(const char* name, const std::function<void()>& f) {
+  try {
+    f();
+    ++g_pass;
+    std::printf("PASS %s\n", name);
+  } catch (const std::exception& e) {
+    ++g_fail;
+    std::printf("FAIL %s: %s\n", name, e.what());
+  }
+}
+
+static bool bits_equal(const double* a, const double* b, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t x, y;
+    std::memcpy(&x, &a[i], 8);
+    std::memcpy(&y, &b[i], 8);
+    if (x != y && !(a[i] != a[i] && b[i] != b[i])) {
+      std::fprintf(stderr, "  element %zu: %.17g != %.17g\n", i, a[i], b[i]);
+      return false;
+    }
+  }
+  return true;
+}
+
+static std::vector<double> synth(int64_t L, int p, int k) {
+  std::vector<double> v((size_t)L);
+  ipls_oracle_synth_fill(v.data(), L, 0x1B52026ULL, p, k);
+  return v;
+}
+
+// oracle: OrganizeGradients partition p of flat
+static std::vector<double> organize(const std::vector<double>& flat, int64_t M, int P, int p) {
+  std::vector<double> out((size_t)ipls_oracle_partition_len(M, P, p));
+  if (ipls_oracle_organize(flat.data(), (int64_t)flat.size(), M, P, p, out.data()) != 0)
+    throw std::runtime_error("oracle organize");
+  return out;
+}
+
+static std::vector<double> read_ethmodel(const std::string& path) {
+  gzFile f = gzopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot open " + path);
+  std::vector<unsigned char> raw;
+  unsigned char buf[1 << 16];
+  int n;
+  while ((n = gzread(f, buf, sizeof buf)) > 0) raw.insert(raw.end(), buf, buf + n);
+  gzclose(f);
+  std::vector<double> m(raw.size() / 8);
+  ipls_oracle_be_decode(raw.data(), (int64_t)m.size(), m.data());
+  return m;
+}
+
+int main(int argc, char** argv) {
+  const bool gpu = !(argc > 1 && std::string(argv[1]) == "--no-gpu");
+  const std::string golden = argc > 2 ? argv[2] : "tests/golden";
+
+  // ---------------- host-only ----------------
+  run("Middleware.parse_arguments", [] {
+    auto d = Middleware::parse_arguments({"-p", "5000", "-pa", "3", "-mp", "1", "-n", "3", "-i", "0", "-training",
+                                          "60", "-aggr", "1", "-async", "true"});
+    CHECK(d.port == 5000 && d._PARTITIONS == 3 && d.Min_Members == 3 && d.Partial_Aggregation && !d.isSynchronous,
+          "flag values");
+    bool threw = false;
+    try {
+      Middleware::parse_arguments({"-p", "5000", "-pa", "3"});
+    } catch (const IllegalArgumentException&) {
+      threw = true;
+    }
+    CHECK(threw, "missing required flags must throw");
+  });
+  run("MyIPFSClass.Marshall_Packet/GET_GRADIENTS", [] {
+    std::vector<double> g = {1.5, -0.0, 1e300, 5e-324};
+    auto fr = MyIPFSClass::Marshall_Packet(g, "QmOrigin", 7, 42, 3);
+    std::vector<uint8_t> ref(14 + 8 * g.size() + 8);
+    const int64_t nb = ipls_oracle_frame_encode(g.data(), (int32_t)g.size(), 7, 42, 3, (const uint8_t*)"QmOrigin", 8,
+                                                ref.data());
+    CHECK(nb == (int64_t)fr.size() && std::memcmp(fr.data(), ref.data(), fr.size()) == 0, "frame bytes");
+    auto h = MyIPFSClass::GET_GRADIENTS(fr);
+    CHECK(h.pid == 3 && h.n == 4 && h.partition == 7 && h.iteration == 42 && h.payload_off == 14, "header");
+    bool threw = false;
+    try {
+      MyIPFSClass::GET_GRADIENTS(std::vector<uint8_t>(fr.begin(), fr.begin() + 20));
+    } catch (const BufferUnderflowException&) {
+      threw = true;
+    }
+    CHECK(threw, "truncated frame must throw BufferUnderflowException");
+  });
+
+  if (gpu) {
+    // ---------------- device path ----------------
+    run("IPLS config A (ETHModel, -pa 3 -n 3)", [&] {
+      const auto model = read_ethmodel(golden + "/ethmodel.f64be.gz");
+      const int64_t M = (int64_t)model.size();
+      PeerData pd;
+      pd._MODEL_SIZE = M;
+      pd._PARTITIONS = 3;
+      pd.Min_Members = 3;
+      IPLS ipls(pd, {0, 1, 2});
+      Updater updater(ipls);
+      Light_IPLS_Daemon daemon(ipls);
+      ipls.InitializeWeights(model);
+      auto first = ipls.GetPartitions();   // count slot 0.0: model passes through
+      CHECK(bits_equal(first.data(), model.data(), model.size()), "initial GetPartitions");
+      std::vector<std::vector<double>> peers(3, model);
+      for (int k = 0; k < 3; ++k) {
+        auto noise = synth(M + 1, 0, k);
+        for (int64_t i = 0; i < M; ++i) peers[k][i] = model[i] + noise[i];
+      }
+      daemon.UpdateModel(peers[0]);                              // own partitions
+      for (int k = 1; k < 3; ++k) {
+        auto parts = ipls.OrganizeGradients(peers[k]);
+        for (int p = 0; p < 3; ++p) updater._Update(&parts[p], p, true);   // arrivals
+      }
+      auto avg = daemon.Get_Partitions();
+      // oracle
+      std::vector<double> expect;
+      for (int p = 0; p < 3; ++p) {
+        const int64_t L = ipls_oracle_partition_len(M, 3, p);
+        std::vector<double> s((size_t)L);
+        std::vector<std::vector<double>> b;
+        for (int k = 0; k < 3; ++k) b.push_back(organize(peers[k], M, 3, p));
+        const double* bp[3] = {b[0].data(), b[1].data(), b[2].data()};
+        ipls_oracle_reduce(s.data(), bp, 3, L, 1);
+        std::vector<double> d((size_t)L - 1);
+        ipls_oracle_divide(s.data(), L, 0, d.data());
+        expect.insert(expect.end(), d.begin(), d.end());
+      }
+      CHECK(avg.size() == expect.size() && bits_equal(avg.data(), expect.data(), avg.size()), "averaged model");
+    });
+
+    run("Updater file + frame arrivals, replicas, commit bytes", [&] {
+      const int64_t L = 70001;
+      PeerData pd;
+      pd._MODEL_SIZE = 0;
+      pd._PARTITIONS = 1;
+      // synthetic geometry goes through the C-ABI's bucket_len
+      ipls_agg_cfg c{};
+      c.n_partitions = 1;
+      c.bucket_len = L;
+      ipls_agg* h = nullptr;
+      check(ipls_agg_open(&c, &h), nullptr);
+      std::vector<std::vector<double>> b;
+      for (int k = 0; k < 4; ++k) b.push_back(synth(L, 3, k));
+      std::vector<uint8_t> be(8 * (size_t)L);
+      ipls_oracle_be_encode(b[1].data(), L, be.data());
+      auto frame = MyIPFSClass::Marshall_Packet(b[2], "QmPeer2", 0, 1, 3);
+      check(ipls_agg_accumulate(h, 0, IPLS_TGT_AGG, b[0].data(), L, IPLS_HOST_F64), h);
+      check(ipls_agg_accumulate(h, 0, IPLS_TGT_AGG, be.data(), L, IPLS_HOST_BE), h);
+      check(ipls_agg_accumulate(h, 0, IPLS_TGT_AGG, frame.data(), (int64_t)frame.size(), IPLS_HOST_FRAME), h);
+      check(ipls_agg_accumulate(h, 0, IPLS_TGT_REP, b[3].data(), L, IPLS_HOST_F64), h);
+      std::vector<uint8_t> file(8 * (size_t)L);
+      check(ipls_agg_finalize(h, 0, file.data(), IPLS_HOST_BE, nullptr), h);
+      ipls_agg_close(h);
+      std::vector<double> s((size_t)L), r((size_t)L), w((size_t)L), wa((size_t)L);
+      const double* bp[3] = {b[0].data(), b[1].data(), b[2].data()};
+      ipls_oracle_reduce(s.data(), bp, 3, L, 1);
+      const double* rp[1] = {b[3].data()};
+      ipls_oracle_reduce(r.data(), rp, 1, L, 1);
+      ipls_oracle_aggregate_partition(s.data(), r.data(), w.data(), wa.data(), L);
+      std::vector<uint8_t> ref(8 * (size_t)L);
+      ipls_oracle_be_encode(w.data(), L, ref.data());
+      CHECK(file == ref, "update_file bytes of AGG + REP");
+    });
+
+    run("exceptions", [] {
+      PeerData pd;
+      pd._MODEL_SIZE = 10;
+      pd._PARTITIONS = 7;
+      bool neg = false;
+      try {
+        IPLS bad(pd);
+      } catch (const NegativeArraySizeException&) {
+        neg = true;
+      }
+      CHECK(neg, "M=10, -pa 7 -> NegativeArraySizeException");
+      pd._PARTITIONS = 2;
+      IPLS ok(pd, {0, 1});
+      Updater u(ok);
+      std::vector<double> shortg(3, 1.0);
+      bool aioobe = false;
+      try {
+        u._Update(&shortg, 0, true);
+      } catch (const ArrayIndexOutOfBoundsException&) {
+        aioobe = true;
+      }
+      CHECK(aioobe, "short bucket -> ArrayIndexOutOfBoundsException");
+      u._Update(nullptr, 0, true);   // Gradient == null: no-op
+    });
+  }
+  std::printf("%d passed, %d failed\n", g_pass, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,30 @@
+"""The C++ host mirror (ipls-java-api_amd/host/ipls_host.hpp: IPLS, Updater,
+Light_IPLS_Daemon, MyIPFSClass, Middleware with Java names and exceptions)
+driven by tests/cpp/test_host_parity.cpp against the C oracle."""
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+BIN = ROOT / "tests" / "cpp" / "build" / "test_host_parity"
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "ipls-java-api_amd"), "host_test"], check=True)
+    assert BIN.exists()
+
+
+def test_host_mirror_host_only():
+    _build()
+    r = subprocess.run([str(BIN), "--no-gpu", str(GOLDEN)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "2 passed, 0 failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_host_mirror_on_gpu():
+    _build()
+    r = subprocess.run([str(BIN), "--gpu", str(GOLDEN)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "5 passed, 0 failed" in r.stdout
