@@ -247,55 +247,51 @@ unsigned blocks_for(int64_t n, int64_t per_block) { return (unsigned)((n + per_b
 
 // ---- kernel dispatch: k_reduce ----
 // Two shapes (tools/reduce_sweep.hip, profiles/r01/sweep*.txt):
-//  * big batches: 1 peer in flight x 16 x 16 B per lane (64 KiB contiguous per
-//    bucket per block), XCD-chunked block order -- 80-83 % of 8 TB/s on config
-//    C over every bucket layout tried, within ~3 % of a pure streaming read;
-//  * small batches (< kBigMinBlocks tiles of the big shape): 8 peers in flight
-//    x 16 B per lane, partition-major -- more blocks to fill 256 CUs.
-constexpr int kBigG = 1, kBigR = 16, kBigMap = 2;
+//  * big batches: 1024-lane workgroups, 1 peer in flight x 16 x 16 B per lane,
+//    i.e. each CU streams one 256 KiB contiguous chunk of one bucket at a time
+//    (fewer, longer DRAM streams): 85-89 % of 8 TB/s on config C over every
+//    bucket layout tried, vs 80-86 % for 256-lane / 64 KiB blocks;
+//  * small batches (< kBigMinBlocks big tiles): 256 lanes, 8 peers in flight
+//    x 16 B per lane, partition-major -- enough blocks to fill 256 CUs.
+constexpr int kBigG = 1, kBigMap = 0, kBigBS = 1024;
 constexpr int kSmallG = 8, kSmallR = 1, kSmallMap = 0;
-constexpr int64_t kBigMinBlocks = 2048;
+constexpr int64_t kBigMinBlocks = 512;
+// 16 x 16 B per lane fits the 128-VGPR budget of a 1024-lane workgroup only
+// for native-double input without an ACCUM read of the target; the BE-input
+// and ACCUM variants use 8 (16 spilled to scratch -- checked in the ISA).
+template <bool BE_IN, int START>
+constexpr int big_r() { return (!BE_IN && START != kAccum) ? 16 : 8; }
 
-template <bool BE_IN, bool BE_OUT, int START, bool BIG>
-void launch_reduce_t(dim3 grid, hipStream_t st, const unsigned long long* const* bufs,
-                     const PartDesc* parts, int k, int tpp, int n_parts) {
-  if constexpr (BIG)
-    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kBigR, true, kBigMap>), grid, dim3(kBlock), 0, st,
-                       bufs, parts, k, tpp, n_parts);
-  else
+template <bool BE_IN, bool BE_OUT, int START>
+void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,
+                     const PartDesc* parts, int k) {
+  constexpr int R = big_r<BE_IN, START>();
+  const int64_t big_tile = (int64_t)kBigBS * 2 * R;
+  const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
+  if (big_tpp * n_parts >= kBigMinBlocks) {
+    const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
+    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS>), grid, dim3(kBigBS), 0, st,
+                       bufs, parts, k, (int)big_tpp, n_parts);
+  } else {
+    const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
+    const int64_t tpp = (maxL + tile - 1) / tile;
+    const dim3 grid((unsigned)grid_blocks(kSmallMap, tpp * n_parts));
     hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
-                       st, bufs, parts, k, tpp, n_parts);
-}
-
-template <bool BE_IN, bool BE_OUT>
-void launch_reduce_io(bool big, int start, dim3 grid, hipStream_t st, const unsigned long long* const* bufs,
-                      const PartDesc* parts, int k, int tpp, int n_parts) {
-#define LR(ST)                                                                                  \
-  do {                                                                                          \
-    if (big) launch_reduce_t<BE_IN, BE_OUT, ST, true>(grid, st, bufs, parts, k, tpp, n_parts);  \
-    else launch_reduce_t<BE_IN, BE_OUT, ST, false>(grid, st, bufs, parts, k, tpp, n_parts);     \
-  } while (0)
-  if (start == kZero) LR(kZero);
-  else if (start == kFirst) LR(kFirst);
-  else LR(kAccum);
-#undef LR
+                       st, bufs, parts, k, (int)tpp, n_parts);
+  }
 }
 
 void launch_reduce(bool be_in, bool be_out, int start, int64_t maxL, int n_parts, hipStream_t st,
                    const unsigned long long* const* bufs, const PartDesc* parts, int k) {
-  const int64_t big_tile = (int64_t)kBlock * 2 * kBigR;
-  const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
-  const bool big = big_tpp * n_parts >= kBigMinBlocks;
-  const int64_t tile = big ? big_tile : (int64_t)kBlock * 2 * kSmallR;
-  const int tpp = (int)((maxL + tile - 1) / tile);
-  const dim3 grid((unsigned)grid_blocks(big ? kBigMap : kSmallMap, (int64_t)tpp * n_parts));
-  if (be_in) {
-    if (be_out) launch_reduce_io<true, true>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
-    else launch_reduce_io<true, false>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
-  } else {
-    if (be_out) launch_reduce_io<false, true>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
-    else launch_reduce_io<false, false>(big, start, grid, st, bufs, parts, k, tpp, n_parts);
-  }
+#define LV(BI, BO)                                                                                  \
+  do {                                                                                              \
+    if (start == kZero) launch_reduce_v<BI, BO, kZero>(maxL, n_parts, st, bufs, parts, k);          \
+    else if (start == kFirst) launch_reduce_v<BI, BO, kFirst>(maxL, n_parts, st, bufs, parts, k);   \
+    else launch_reduce_v<BI, BO, kAccum>(maxL, n_parts, st, bufs, parts, k);                        \
+  } while (0)
+  if (be_in) { if (be_out) LV(true, true); else LV(true, false); }
+  else { if (be_out) LV(false, true); else LV(false, false); }
+#undef LV
 }
 
 void launch_reduce_scalar(bool be_in, bool be_out, int start, dim3 grid, hipStream_t st,

@@ -86,7 +86,8 @@ int main(int argc, char** argv) {
       else b = base + (int64_t)(p * K + k) * stride;
       ptrs[p * K + k] = b;
       const unsigned long long key = 0x1B52026ULL ^ ((unsigned long long)p << 40) ^ ((unsigned long long)k << 32);
-      hipLaunchKernelGGL(k_synth<false>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
+      if (getenv("SWEEP_BE")) hipLaunchKernelGGL(k_synth<true>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
+      else hipLaunchKernelGGL(k_synth<false>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
     }
   const unsigned long long** d_ptrs;
   CK(hipMalloc(&d_ptrs, ptrs.size() * 8));
@@ -117,27 +118,27 @@ int main(int argc, char** argv) {
 
   const double alg = (double)P * (K + 1) * L * 8;
   std::vector<Var> vars;
-#define ADDL(G, R, MAP, LDS)                                                                   \
-  vars.push_back(Var{"reduce G=" #G " R=" #R " MAP=" #MAP " lds=" #LDS,                          \
+  const bool be = getenv("SWEEP_BE") != nullptr;
+#define ADDC(G, R, MAP, BS, RC)                                                                \
+  vars.push_back(Var{"reduce G=" #G " R=" #R " MAP=" #MAP " BS=" #BS " RC=" #RC,                \
                      [=](hipStream_t s) {                                                       \
-                       const int64_t tile = (int64_t)kBlock * 2 * R;                            \
+                       const int64_t tile = (int64_t)BS * 2 * R;                                \
                        const int tpp = (int)((L + tile - 1) / tile);                            \
-                       hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, true, MAP>),     \
-                                          dim3((unsigned)grid_blocks(MAP, (int64_t)tpp * P)), dim3(kBlock), LDS, s, \
-                                          (const unsigned long long* const*)d_ptrs, d_pd, K, tpp, P); \
+                       const dim3 grid((unsigned)grid_blocks(MAP, (int64_t)tpp * P));           \
+                       auto bp = (const unsigned long long* const*)d_ptrs;                      \
+                       if (be)                                                                  \
+                         hipLaunchKernelGGL((k_reduce<true, false, kZero, G, R, true, MAP, BS, RC>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                       else                                                                     \
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, true, MAP, BS, RC>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
-  ADDL(1, 16, 2, 0);
-  ADDL(1, 16, 2, 50000);    // <= 3 blocks / CU
-  ADDL(1, 16, 2, 70000);    // <= 2 blocks / CU
-  ADDL(1, 16, 2, 100000);   // 1 block / CU
-  ADDL(2, 8, 2, 0);
-  ADDL(2, 8, 2, 40000);     // <= 4 blocks / CU
-  ADDL(2, 8, 2, 70000);     // <= 2 blocks / CU
-  ADDL(8, 1, 2, 0);
-  ADDL(8, 1, 2, 20000);     // <= 8 blocks / CU
-  ADDL(8, 1, 2, 40000);     // <= 4 blocks / CU
-#undef ADDL
+  ADDC(1, 8, 0, 1024, 8);
+  ADDC(1, 16, 0, 1024, 16);
+  ADDC(1, 16, 0, 1024, 8);
+  ADDC(1, 16, 0, 1024, 4);
+  ADDC(1, 16, 0, 256, 16);
+  ADDC(8, 1, 0, 256, 1);
+#undef ADDC
 #define RA(G, R)                                                                                   \
   vars.push_back(Var{"readall G=" #G " R=" #R " (read ceiling)",                                     \
                      [=](hipStream_t s) {                                                            \
