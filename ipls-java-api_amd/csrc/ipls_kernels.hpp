@@ -129,10 +129,7 @@ __device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_pa
 }
 
 //   BS     : lanes per workgroup
-//   RC     : loads issued per batch (RC < R: batches of RC vectors separated by
-//            a scheduling fence, so the in-flight registers stay RC x 4 VGPRs
-//            while each CU still streams BS x 16 B x R contiguous per bucket)
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock, int RC = R>
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock>
 __global__ __launch_bounds__(BS) void k_reduce(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
     int k, int tiles_per_part, int n_parts) {
@@ -151,10 +148,13 @@ __global__ __launch_bounds__(BS) void k_reduce(
 
   if (base + kTile <= L) {
     // ---------------- vector path: R x 16 B per lane ----------------
-    // element offset of vector r for this lane = lane0 + r * 2 * BS; only the
-    // lane base is kept live (per-r 64-bit offsets would pin 2R VGPRs).
-    const int64_t lane0 = base + 2 * (int64_t)tid;
-    constexpr int64_t kStep = 2 * (int64_t)kBlock;
+    // (This form -- per-r offsets, loads of a peer group written before its
+    // adds -- is the one hipcc schedules as "all G x R loads, then counted
+    // vmcnt waits" within 128 VGPRs at R = 16; a single lane-base pointer
+    // made it interleave 2 loads at a time with vmcnt(0).  Checked in the ISA.)
+    int64_t off[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * kBlock + tid);
 
     d2 acc[R];
 #pragma unroll
@@ -162,54 +162,44 @@ __global__ __launch_bounds__(BS) void k_reduce(
       if constexpr (START == kZero) {
         acc[r] = d2{0.0, 0.0};
       } else if constexpr (START == kFirst) {
-        acc[r] = decode2<BE_IN>(ld16<NT>(pb[0] + lane0 + r * kStep));
+        acc[r] = decode2<BE_IN>(ld16<NT>(pb[0] + off[r]));
       } else {  // kAccum: the target holds native doubles (or BE if BE_OUT)
-        acc[r] = decode2<BE_OUT>(ld16<false>(dst + lane0 + r * kStep));
+        acc[r] = decode2<BE_OUT>(ld16<false>(dst + off[r]));
       }
     }
-    static_assert(R % RC == 0, "RC must divide R");
     int j = j0;
     for (; j + G <= k; j += G) {
+      u2 v[G][R];
 #pragma unroll
-      for (int c = 0; c < R; c += RC) {
-        u2 v[G][RC];
+      for (int g = 0; g < G; ++g) {
+        const unsigned long long* __restrict__ src = pb[j + g];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const unsigned long long* __restrict__ src = pb[j + g] + lane0;
+        for (int r = 0; r < R; ++r) v[g][r] = ld16<NT>(src + off[r]);
+      }
 #pragma unroll
-          for (int r = 0; r < RC; ++r) v[g][r] = ld16<NT>(src + (c + r) * kStep);
+      for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          d2 x = decode2<BE_IN>(v[g][r]);
+          acc[r].x = acc[r].x + x.x;
+          acc[r].y = acc[r].y + x.y;
         }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-#pragma unroll
-          for (int r = 0; r < RC; ++r) {
-            d2 x = decode2<BE_IN>(v[g][r]);
-            acc[c + r].x = acc[c + r].x + x.x;
-            acc[c + r].y = acc[c + r].y + x.y;
-          }
-        }
-        if constexpr (RC < R) __builtin_amdgcn_sched_barrier(0);
       }
     }
     for (; j < k; ++j) {
-      const unsigned long long* __restrict__ src = pb[j] + lane0;
+      const unsigned long long* __restrict__ src = pb[j];
+      u2 v[R];
 #pragma unroll
-      for (int c = 0; c < R; c += RC) {
-        u2 v[RC];
+      for (int r = 0; r < R; ++r) v[r] = ld16<NT>(src + off[r]);
 #pragma unroll
-        for (int r = 0; r < RC; ++r) v[r] = ld16<NT>(src + (c + r) * kStep);
-#pragma unroll
-        for (int r = 0; r < RC; ++r) {
-          d2 x = decode2<BE_IN>(v[r]);
-          acc[c + r].x = acc[c + r].x + x.x;
-          acc[c + r].y = acc[c + r].y + x.y;
-        }
-        if constexpr (RC < R) __builtin_amdgcn_sched_barrier(0);
+      for (int r = 0; r < R; ++r) {
+        d2 x = decode2<BE_IN>(v[r]);
+        acc[r].x = acc[r].x + x.x;
+        acc[r].y = acc[r].y + x.y;
       }
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + lane0 + r * kStep));
+    for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
   } else {
     // ------- partial last tile: 512-element vector steps, scalar remainder -------
     for (int64_t sb = base; sb < L; sb += 2 * kBlock) {

@@ -119,25 +119,25 @@ int main(int argc, char** argv) {
   const double alg = (double)P * (K + 1) * L * 8;
   std::vector<Var> vars;
   const bool be = getenv("SWEEP_BE") != nullptr;
-#define ADDC(G, R, MAP, BS, RC)                                                                \
-  vars.push_back(Var{"reduce G=" #G " R=" #R " MAP=" #MAP " BS=" #BS " RC=" #RC,                \
+#define ADDC(G, R, MAP, BS)                                                                    \
+  vars.push_back(Var{"reduce G=" #G " R=" #R " MAP=" #MAP " BS=" #BS,                            \
                      [=](hipStream_t s) {                                                       \
                        const int64_t tile = (int64_t)BS * 2 * R;                                \
                        const int tpp = (int)((L + tile - 1) / tile);                            \
                        const dim3 grid((unsigned)grid_blocks(MAP, (int64_t)tpp * P));           \
                        auto bp = (const unsigned long long* const*)d_ptrs;                      \
                        if (be)                                                                  \
-                         hipLaunchKernelGGL((k_reduce<true, false, kZero, G, R, true, MAP, BS, RC>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                         hipLaunchKernelGGL((k_reduce<true, false, kZero, G, R, true, MAP, BS>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
                        else                                                                     \
-                         hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, true, MAP, BS, RC>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, true, MAP, BS>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
-  ADDC(1, 8, 0, 1024, 8);
-  ADDC(1, 16, 0, 1024, 16);
-  ADDC(1, 16, 0, 1024, 8);
-  ADDC(1, 16, 0, 1024, 4);
-  ADDC(1, 16, 0, 256, 16);
-  ADDC(8, 1, 0, 256, 1);
+  ADDC(1, 8, 0, 1024);
+  ADDC(1, 16, 0, 1024);
+  ADDC(1, 16, 2, 1024);
+  ADDC(1, 16, 0, 256);
+  ADDC(1, 16, 2, 256);
+  ADDC(8, 1, 0, 256);
 #undef ADDC
 #define RA(G, R)                                                                                   \
   vars.push_back(Var{"readall G=" #G " R=" #R " (read ceiling)",                                     \
