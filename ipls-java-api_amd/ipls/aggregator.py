@@ -313,15 +313,26 @@ class Aggregator:
 
     # ---- replica exchange hooks (ipls.distributed) ----
     def export_partial(self, partition: int, tensor):
-        """Copy this aggregator's partial sum AGG[p] into a device tensor (the
-        published partial of IPLS.java:1423-1431) and wait for it."""
-        d = DeviceBuffer.from_tensor(tensor)
-        self._chk(self._lib.ipls_agg_read(self._h, partition, N.TGT_AGG, d.ptr, d.n, N.DEV_F64))
-        self.sync()
+        """Copy this aggregator's partial sum AGG[p] into a transport tensor
+        (the published partial of IPLS.java:1423-1431) and wait for it.  A
+        device tensor (RCCL) gets a device-to-device copy, a host tensor
+        (gloo) a device-to-host copy."""
+        if getattr(tensor, "is_cuda", False):
+            d = DeviceBuffer.from_tensor(tensor)
+            self._chk(self._lib.ipls_agg_read(self._h, partition, N.TGT_AGG, d.ptr, d.n, N.DEV_F64))
+            self.sync()
+        else:
+            self._chk(self._lib.ipls_agg_read(self._h, partition, N.TGT_AGG, int(tensor.data_ptr()),
+                                              tensor.numel(), N.HOST_F64))
 
     def import_partial(self, partition: int, tensor, *, replace_agg: bool = False):
-        """Fold a replica's partial (a device tensor that has landed) into
+        """Fold a replica's partial (a transport tensor that has landed) into
         REP[p] (Updater.java:40-44); replace_agg stores it as AGG[p] instead."""
+        if not getattr(tensor, "is_cuda", False):
+            if not replace_agg:
+                self.Update(tensor.numpy(), partition, from_clients=False)
+                return
+            tensor = tensor.to(f"cuda:{self.device}")   # exact FIRST-start copy needs a device operand
         d = DeviceBuffer.from_tensor(tensor)
         if replace_agg:
             self.reduce_batch(partition, [[d]], start_mode=N.START_FIRST, target=N.TGT_AGG)

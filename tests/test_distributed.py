@@ -147,3 +147,54 @@ def test_replica_exchange_rccl_reduce_mode_two_ranks():
     exp = expected(P, L, K, world, replicas)
     for p in exp:
         assert np.array_equal(got[p], exp[p]) or np.allclose(got[p], exp[p], rtol=0, atol=4e-16 * np.abs(exp[p]).max())
+
+
+def gpu_worker(rank, world, port, P, L, K, replicas, q):
+    """Two processes on one GPU: real HIP aggregators, gloo transport with
+    host tensors (RCCL needs one GPU per rank)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ipls
+    from ipls.distributed import ReplicaPlan, combine_replicas
+    plan = ReplicaPlan.build(P, world, replicas)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=0)
+    for p, hs in plan.holders.items():
+        if rank in hs:
+            idx = hs.index(rank)
+            for k in range(K):
+                if k % len(hs) == idx:
+                    agg.Update(bucket(p, k, L), p)
+    filled = combine_replicas(agg, plan, rank, device="cpu")
+    res = {}
+    for p in filled:
+        s, _ = agg.AggregatePartition(p, with_sum=True, sum_big_endian=False)
+        res[p] = s
+    agg.close()
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_replica_exchange_hip_aggregators_two_processes():
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    P, L, K, world = 4, 20011, 5, 2
+    replicas = {0: [1], 3: [0]}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=gpu_worker, args=(r, world, port, P, L, K, replicas, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = {}
+    for _ in range(world):
+        rank, res = q.get(timeout=300)
+        got.update(res)
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    exp = expected(P, L, K, world, replicas)
+    assert sorted(got) == sorted(exp)
+    for p in exp:
+        assert_bits_equal(got[p], exp[p], f"partition {p}")
