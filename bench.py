@@ -259,13 +259,29 @@ def main():
         agg.sync()
         fin_ms, div_ms = e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2])
         n_el = P * L
+        ref_flat = flat.clone()
+        # the same round as ONE launch (ipls_agg_aggregate_round): folds + W + averages
+        reps = 5
+        fe = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        for i in range(reps):
+            fe[i].record(stream)
+            agg.aggregate_round(0, rows, out=fb)
+        fe[reps].record(stream)
+        agg.sync()
+        fused_ms = fe[0].elapsed_time(fe[reps]) / reps
+        fused_same = bool(torch.equal(flat.view(torch.int64), ref_flat.view(torch.int64)))
+        fused_bytes = P * (K + 1) * L * 8 + 8 * (n_el - P)   # K buckets in, W out, averages out
         round_info = {
             "finalize_ms": round(fin_ms, 4), "finalize_GBps": round(16 * n_el / fin_ms / 1e6, 1),
             "divide_ms": round(div_ms, 4), "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
             "round_ms": round(kern_ms + fin_ms + div_ms, 4),
-            "note": "one aggregation round on device: reduce (K buckets) + AggregatePartition(all) + GetPartitions",
+            "fused_round_ms": round(fused_ms, 4),
+            "fused_round_GBps": round(fused_bytes / fused_ms / 1e6, 1),
+            "fused_round_bit_identical": fused_same,
+            "note": "one aggregation round on device: reduce (K buckets) + AggregatePartition(all) + GetPartitions "
+                    "as three launches (round_ms), and fused into one (fused_round_ms)",
         }
-        del flat
+        del flat, ref_flat
 
     out = None
     if rank == 0:

@@ -187,6 +187,21 @@ int ipls_agg_scale(ipls_agg *h, int p, int dst_target, int src_target, double c)
  * (L_p - 1 averaged values, the GetPartitions divide).  Either may be NULL. */
 int ipls_agg_finalize(ipls_agg *h, int p, void *sum_out, int sum_kind, double *avg_out);
 
+/* A whole aggregation round for partitions [p_first, p_first+n_parts) in ONE
+ * kernel launch (one pass over the buckets):
+ *   AGG[p]   = AGG[p] + b_0 + ... + b_{k-1}     Updater._Update folds (Updater.java:115-117)
+ *   W[p]     = AGG[p] + REP[p]; AGG = REP = 0   AggregatePartition (IPLS.java:1248-1274)
+ *   avg_out  = W[p][j] / W[p][L_p-1]            GetPartitions divide (IPLS.java:1159-1174)
+ * AGG is never stored: its final value only feeds W.  Results are bit-identical
+ * to reduce_batch(ACCUM) + finalize + get_partitions.  bufs: n_parts*k device
+ * buckets (DEV_F64/DEV_BE, k may be 0).  avg_out (or NULL) receives the
+ * averaged values of the partitions, partition p at flat offset
+ * partition_offset(p) - partition_offset(p_first) -- for all partitions the
+ * GetPartitions model; avg_kind DEV_F64 or HOST_F64. */
+int ipls_agg_aggregate_round(ipls_agg *h, int p_first, int n_parts,
+                             const void *const *bufs, int k, int src_kind,
+                             void *avg_out, int avg_kind);
+
 /* Download_Scheduler.cache_partition (Download_Scheduler.java:752-792):
  * Weight_Address[p] = GetParameters(hash) -- the downloaded updated partition. */
 int ipls_agg_set_weights(ipls_agg *h, int p, const void *src, int64_t n, int src_kind);

@@ -82,6 +82,7 @@ struct ipls_agg {
 
   // checksum result
   unsigned long long* d_sum = nullptr;
+  double* d_cnt = nullptr;   // per-partition count slots of a fused round (P doubles)
 };
 
 namespace {
@@ -259,25 +260,26 @@ constexpr int64_t kBigMinBlocks = 512;
 // 16 x 16 B per lane fits the 128-VGPR budget of a 1024-lane workgroup only
 // for native-double input without an ACCUM read of the target; the BE-input
 // and ACCUM variants use 8 (16 spilled to scratch -- checked in the ISA).
-template <bool BE_IN, int START>
+// The fused round (FIN) uses the same R: 128 VGPRs, no scratch (checked).
+template <bool BE_IN, int START, bool FIN = false>
 constexpr int big_r() { return (!BE_IN && START != kAccum) ? 16 : 8; }
 
-template <bool BE_IN, bool BE_OUT, int START>
+template <bool BE_IN, bool BE_OUT, int START, bool FIN = false>
 void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,
-                     const PartDesc* parts, int k) {
-  constexpr int R = big_r<BE_IN, START>();
+                     const PartDesc* parts, int k, int secure = 0, const double* cnts = nullptr) {
+  constexpr int R = big_r<BE_IN, START, FIN>();
   const int64_t big_tile = (int64_t)kBigBS * 2 * R;
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   if (big_tpp * n_parts >= kBigMinBlocks) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
-    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS>), grid, dim3(kBigBS), 0, st,
-                       bufs, parts, k, (int)big_tpp, n_parts);
+    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS, FIN>), grid, dim3(kBigBS), 0,
+                       st, bufs, parts, k, (int)big_tpp, n_parts, secure, cnts);
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
     const int64_t tpp = (maxL + tile - 1) / tile;
     const dim3 grid((unsigned)grid_blocks(kSmallMap, tpp * n_parts));
-    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
-                       st, bufs, parts, k, (int)tpp, n_parts);
+    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap, kBlock, FIN>), grid,
+                       dim3(kBlock), 0, st, bufs, parts, k, (int)tpp, n_parts, secure, cnts);
   }
 }
 
@@ -294,6 +296,23 @@ void launch_reduce(bool be_in, bool be_out, int start, int64_t maxL, int n_parts
 #undef LV
 }
 
+// fused round: native-double Weights out, ZERO or ACCUM start (AGG is never
+// FIRST-started).  A one-block pre-pass folds each partition's count slot
+// (k + 2 scalar loads per partition) so that the wide kernel reads one value
+// per block instead of a k-long chain of dependent loads.
+void launch_reduce_fin(bool be_in, int start, int secure, int64_t maxL, int n_parts, hipStream_t st,
+                       const unsigned long long* const* bufs, const PartDesc* parts, int k, double* cnts) {
+#define FIN(BI, ST)                                                                                   \
+  do {                                                                                                \
+    hipLaunchKernelGGL((k_round_counts<BI, ST>), dim3((n_parts + kBlock - 1) / kBlock), dim3(kBlock), 0, st, \
+                       bufs, parts, k, n_parts, cnts);                                                 \
+    launch_reduce_v<BI, false, ST, true>(maxL, n_parts, st, bufs, parts, k, secure, cnts);           \
+  } while (0)
+  if (be_in) { if (start == kZero) FIN(true, kZero); else FIN(true, kAccum); }
+  else { if (start == kZero) FIN(false, kZero); else FIN(false, kAccum); }
+#undef FIN
+}
+
 void launch_reduce_scalar(bool be_in, bool be_out, int start, dim3 grid, hipStream_t st,
                           const unsigned long long* const* bufs, const PartDesc* parts, int k, int tpp,
                           int64_t tile) {
@@ -308,13 +327,22 @@ void launch_reduce_scalar(bool be_in, bool be_out, int start, dim3 grid, hipStre
 // Core of accumulate / reduce_batch: all pointers device-resident.  The
 // destination is the handle's `target` accumulators, or -- when ext_dst is
 // given -- one caller buffer per partition (doubles or, be_out, BE bytes).
+// fused round (fin != nullptr): fold into AGG's values and write
+// W = fold + REP to Weights, plus the averages at fin->avg (if set); AGG and
+// REP end logically zero.  Callers guarantee 16-B aligned buckets.
+struct FinOut {
+  unsigned long long* avg;   // averages of p_first.. at flat_off[p] - flat_off[p_first], or null
+};
+
 int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, bool be_in,
-               int start_mode, int target, void* const* ext_dst = nullptr, bool be_out = false) {
+               int start_mode, int target, void* const* ext_dst = nullptr, bool be_out = false,
+               const FinOut* fin = nullptr) {
   auto dst_of = [&](int q) -> unsigned long long* {
+    if (fin) return (unsigned long long*)(h->arena + h->w_off[p_first + q]);
     return ext_dst ? (unsigned long long*)ext_dst[q]
                    : (unsigned long long*)(h->arena + target_off(h, p_first + q, target));
   };
-  if (k <= 0) {
+  if (k <= 0 && !fin) {
     if (start_mode == IPLS_START_ZERO) {
       for (int q = 0; q < n_parts; ++q) {
         uint8_t* f = ext_dst ? nullptr : zero_flag(h, p_first + q, target);
@@ -356,8 +384,17 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   std::vector<unsigned char> tbl(bytes);
   PartDesc* pd = (PartDesc*)tbl.data();
   for (int q = 0; q < n_parts; ++q) {
-    pd[q].len = h->len[p_first + q];
+    const int p = p_first + q;
+    pd[q].len = h->len[p];
     pd[q].dst = dst_of(q);
+    pd[q].init = pd[q].dst;
+    pd[q].rep = nullptr;
+    pd[q].avg = nullptr;
+    if (fin) {
+      pd[q].init = (const unsigned long long*)(h->arena + h->agg_off[p]);
+      if (!h->rep_zero[p]) pd[q].rep = (const unsigned long long*)(h->arena + h->rep_off[p]);
+      if (fin->avg) pd[q].avg = fin->avg + (h->flat_off[p] - h->flat_off[p_first]);
+    }
     if (!pd[q].dst) return fail(h, IPLS_E_INVAL, "destination %d is NULL", q);
     if ((uintptr_t)pd[q].dst & 7) return fail(h, IPLS_E_INVAL, "destination %d not 8-byte aligned", q);
     if ((uintptr_t)pd[q].dst & 15) aligned16 = false;
@@ -368,6 +405,13 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   if (rc) return rc;
   const PartDesc* dparts = (const PartDesc*)dtab;
   auto dbufs = (const unsigned long long* const*)((char*)dtab + desc_bytes);
+  if (fin) {
+    if (!aligned16) return fail(h, IPLS_E_INVAL, "fused round needs 16-B aligned buckets");
+    launch_reduce_fin(be_in, start, h->secure, maxL, n_parts, h->stream, dbufs, dparts, k, h->d_cnt);
+    HIP_TRY(h, hipGetLastError());
+    for (int q = p_first; q < p_first + n_parts; ++q) h->agg_zero[q] = h->rep_zero[q] = 1;
+    return IPLS_OK;
+  }
   if (aligned16) {
     launch_reduce(be_in, be_out, start, maxL, n_parts, h->stream, dbufs, dparts, k);
   } else {
@@ -493,6 +537,8 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
     return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc of %lld-byte arena failed", (long long)h->arena_elems * 8));
   }
   if (hipMalloc(&h->d_sum, 64) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc failed"));
+  if (hipMalloc(&h->d_cnt, sizeof(double) * h->P) != hipSuccess)
+    return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc failed"));
   // InitializeWeights(): new double[] -> all zero (IPLS.java:1860-1878).
   if (hipMemsetAsync(h->arena, 0, (size_t)h->arena_elems * 8, h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream) != hipSuccess)
@@ -514,6 +560,7 @@ int ipls_agg_close(ipls_agg* h) {
     if (d) hipFree(d);
   if (h->d_scratch) hipFree(h->d_scratch);
   if (h->d_sum) hipFree(h->d_sum);
+  if (h->d_cnt) hipFree(h->d_cnt);
   if (h->arena) hipFree(h->arena);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
@@ -693,18 +740,8 @@ int ipls_agg_checksum(ipls_agg* h, int p, int target, uint64_t* out) {
   return IPLS_OK;
 }
 
-int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* avg_out) {
-  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
-  int p0 = p, np = 1;
-  if (p == IPLS_ALL_PARTITIONS) {
-    p0 = 0;
-    np = h->P;
-    if (sum_out || avg_out) return fail(h, IPLS_E_INVAL, "host outputs need a single partition");
-  } else if (int rc = check_part(h, p)) {
-    return rc;
-  }
-  HIP_TRY(h, hipSetDevice(h->device));
+// AggregatePartition's W = AGG + REP for partitions [p0, p0+np) (IPLS.java:1256-1269).
+static int finalize_range(ipls_agg* h, int p0, int np) {
   // AGG logically zero but present as an operand -> make it physical.
   bool rep_zero_all = true;
   for (int q = p0; q < p0 + np; ++q) {
@@ -734,6 +771,46 @@ int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* a
                        (const FinDesc*)dtab, h->arena, tpp);
   HIP_TRY(h, hipGetLastError());
   for (int q = p0; q < p0 + np; ++q) h->agg_zero[q] = h->rep_zero[q] = 1;
+  return IPLS_OK;
+}
+
+// GetPartitions' divide (IPLS.java:1159-1174) of Weights[p0..p0+np) into d_out,
+// partition p at flat_off[p] - flat_off[p0].
+static int divide_range(ipls_agg* h, int p0, int np, unsigned long long* d_out, bool be) {
+  std::vector<DivDesc> dd(np);
+  int64_t maxn = 0;
+  for (int q = 0; q < np; ++q) {
+    const int p = p0 + q;
+    dd[q] = DivDesc{h->len[p], h->w_off[p], h->flat_off[p] - h->flat_off[p0]};
+    maxn = std::max(maxn, h->len[p] - 1);
+  }
+  if (maxn <= 0) return IPLS_OK;
+  void* dtab = nullptr;
+  if (int rc = upload_table(h, dd.data(), dd.size() * sizeof(DivDesc), &dtab)) return rc;
+  const int64_t tile = (int64_t)kBlock * 8;
+  const int tpp = (int)((maxn + tile - 1) / tile);
+  const dim3 g((unsigned)tpp * np);
+#define DIV(B, S) hipLaunchKernelGGL((k_divide<B, S>), g, dim3(kBlock), 0, h->stream, (const DivDesc*)dtab, (const double*)h->arena, d_out, tpp)
+  if (be) { if (h->secure) DIV(true, true); else DIV(true, false); }
+  else { if (h->secure) DIV(false, true); else DIV(false, false); }
+#undef DIV
+  HIP_TRY(h, hipGetLastError());
+  return IPLS_OK;
+}
+
+int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* avg_out) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  int p0 = p, np = 1;
+  if (p == IPLS_ALL_PARTITIONS) {
+    p0 = 0;
+    np = h->P;
+    if (sum_out || avg_out) return fail(h, IPLS_E_INVAL, "host outputs need a single partition");
+  } else if (int rc = check_part(h, p)) {
+    return rc;
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (int rc = finalize_range(h, p0, np)) return rc;
 
   if (np == 1 && (sum_out || avg_out)) {
     const int64_t L = h->len[p0];
@@ -753,17 +830,7 @@ int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* a
     }
     if (avg_out && L > 1) {
       if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
-      DivDesc dd{L, h->w_off[p0], 0};
-      void* dt2 = nullptr;
-      if (int rc = upload_table(h, &dd, sizeof dd, &dt2)) return rc;
-      const int tp = (int)((L - 1 + tile - 1) / tile);
-      if (h->secure)
-        hipLaunchKernelGGL((k_divide<false, true>), dim3((unsigned)tp), dim3(kBlock), 0, h->stream,
-                           (const DivDesc*)dt2, (const double*)h->arena, (unsigned long long*)h->d_scratch, tp);
-      else
-        hipLaunchKernelGGL((k_divide<false, false>), dim3((unsigned)tp), dim3(kBlock), 0, h->stream,
-                           (const DivDesc*)dt2, (const double*)h->arena, (unsigned long long*)h->d_scratch, tp);
-      HIP_TRY(h, hipGetLastError());
+      if (int rc = divide_range(h, p0, 1, (unsigned long long*)h->d_scratch, false)) return rc;
       if (int rc = d2h(h, avg_out, h->d_scratch, (size_t)(L - 1) * 8)) return rc;
     }
   }
@@ -959,25 +1026,7 @@ int ipls_agg_get_partitions(ipls_agg* h, void* out, int64_t n, int out_kind) {
     if (int rc = ensure_scratch(h, (size_t)std::max<int64_t>(M, 1) * 8)) return rc;
     d_out = (unsigned long long*)h->d_scratch;
   }
-  std::vector<DivDesc> dd(h->P);
-  int64_t maxn = 0;
-  for (int p = 0; p < h->P; ++p) {
-    dd[p] = DivDesc{h->len[p], h->w_off[p], h->flat_off[p]};
-    maxn = std::max(maxn, h->len[p] - 1);
-  }
-  if (maxn > 0) {
-    void* dtab = nullptr;
-    if (int rc = upload_table(h, dd.data(), dd.size() * sizeof(DivDesc), &dtab)) return rc;
-    const int64_t tile = (int64_t)kBlock * 8;
-    const int tpp = (int)((maxn + tile - 1) / tile);
-    const dim3 g((unsigned)tpp * h->P);
-    const bool be = out_kind == IPLS_HOST_BE_CANON;
-#define DIV(B, S) hipLaunchKernelGGL((k_divide<B, S>), g, dim3(kBlock), 0, h->stream, (const DivDesc*)dtab, (const double*)h->arena, d_out, tpp)
-    if (be) { if (h->secure) DIV(true, true); else DIV(true, false); }
-    else { if (h->secure) DIV(false, true); else DIV(false, false); }
-#undef DIV
-    HIP_TRY(h, hipGetLastError());
-  }
+  if (int rc = divide_range(h, 0, h->P, d_out, out_kind == IPLS_HOST_BE_CANON)) return rc;
   if (out_kind == IPLS_DEV_F64) return IPLS_OK;
   return d2h(h, out, d_out, (size_t)M * 8);
 }
@@ -1039,6 +1088,48 @@ int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void*
   HIP_TRY(h, hipSetDevice(h->device));
   return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, IPLS_TGT_AGG, dst,
                     dst_kind == IPLS_DEV_BE);
+}
+
+int ipls_agg_aggregate_round(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+                             void* avg_out, int avg_kind) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_parts <= 0 || p_first < 0 || p_first + n_parts > h->P)
+    return fail(h, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, h->P);
+  if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE)
+    return fail(h, IPLS_E_INVAL, "aggregate_round takes device buckets (DEV_F64/DEV_BE)");
+  if (avg_out && avg_kind != IPLS_DEV_F64 && avg_kind != IPLS_HOST_F64)
+    return fail(h, IPLS_E_INVAL, "avg_kind must be DEV_F64 or HOST_F64");
+  if (k < 0 || (k > 0 && !bufs)) return fail(h, IPLS_E_INVAL, "bad bucket list");
+  HIP_TRY(h, hipSetDevice(h->device));
+  const int p_last = p_first + n_parts - 1;
+  const int64_t n_avg = h->flat_off[p_last] + h->len[p_last] - 1 - h->flat_off[p_first];
+  unsigned long long* d_avg = nullptr;
+  if (avg_out && n_avg > 0) {
+    if (avg_kind == IPLS_DEV_F64) {
+      d_avg = (unsigned long long*)avg_out;
+    } else {
+      if (int rc = ensure_scratch(h, (size_t)n_avg * 8)) return rc;
+      d_avg = (unsigned long long*)h->d_scratch;
+    }
+  }
+  bool aligned16 = true;
+  for (int64_t i = 0; i < (int64_t)n_parts * k; ++i) aligned16 = aligned16 && !((uintptr_t)bufs[i] & 15);
+  if (aligned16) {
+    FinOut fo{d_avg};
+    if (int rc = reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, IPLS_START_ACCUM, IPLS_TGT_AGG,
+                            nullptr, false, &fo))
+      return rc;
+  } else {
+    // 8-B aligned buckets (frames at odd offsets): the same three steps unfused
+    if (int rc = reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, IPLS_START_ACCUM, IPLS_TGT_AGG))
+      return rc;
+    if (int rc = finalize_range(h, p_first, n_parts)) return rc;
+    if (d_avg)
+      if (int rc = divide_range(h, p_first, n_parts, d_avg, false)) return rc;
+  }
+  if (d_avg && avg_kind == IPLS_HOST_F64) return d2h(h, avg_out, d_avg, (size_t)n_avg * 8);
+  return IPLS_OK;
 }
 
 // ---- pubsub ingest: base64url (x layers) -> frame -> fold, on the device ----

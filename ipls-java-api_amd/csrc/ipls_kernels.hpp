@@ -29,8 +29,12 @@ constexpr int kBlock = 256;
 enum Start : int { kAccum = 0, kZero = 1, kFirst = 2 };
 
 struct PartDesc {
-  int64_t len;               // L_p incl. count slot
-  unsigned long long* dst;   // target: an arena accumulator or a caller buffer
+  int64_t len;                      // L_p incl. count slot
+  unsigned long long* dst;          // target: an arena accumulator or a caller buffer
+  // fused-round fields (k_reduce<..., FIN=true> only):
+  const unsigned long long* init;   // START_ACCUM source (the AGG accumulator)
+  const unsigned long long* rep;    // REP accumulator, or null = logically +0.0
+  unsigned long long* avg;          // averaged values out (L-1 doubles), or null
 };
 
 // Global-address-space views.  Bucket pointers come from a device table, so
@@ -129,10 +133,14 @@ __device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_pa
 }
 
 //   BS     : lanes per workgroup
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock>
+//   FIN    : fused round -- dst is Weights[p] and receives fold + REP
+//            (AggregatePartition, IPLS.java:1256), and parts[q].avg (if set)
+//            the GetPartitions divide (IPLS.java:1159-1174), in the same pass
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock,
+          bool FIN = false>
 __global__ __launch_bounds__(BS) void k_reduce(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
-    int k, int tiles_per_part, int n_parts) {
+    int k, int tiles_per_part, int n_parts, int secure = 0, const double* __restrict__ cnts = nullptr) {
   constexpr int kBlock = BS;   // lanes per workgroup (shadows the namespace default)
   constexpr int64_t kTile = (int64_t)kBlock * 2 * R;
   int q, t;
@@ -145,6 +153,26 @@ __global__ __launch_bounds__(BS) void k_reduce(
   const unsigned long long* const* __restrict__ pb = bufs + (size_t)q * k;
   const int tid = threadIdx.x;
   const int j0 = (START == kFirst) ? 1 : 0;
+  static_assert(!(FIN && BE_OUT), "the fused round writes native Weights");
+  // ACCUM source: the target itself, or AGG when the round is fused
+  const unsigned long long* __restrict__ init = FIN ? parts[q].init : dst;
+  const unsigned long long* __restrict__ rep = FIN ? parts[q].rep : nullptr;
+  unsigned long long* __restrict__ avg = FIN ? parts[q].avg : nullptr;
+  // count slot W[L-1] (k_round_counts folded it exactly as element L-1 is)
+  double den = 0.0, cnt = 0.0;
+  if constexpr (FIN) {
+    if (avg) {
+      cnt = cnts[q];
+      den = secure ? 1e12 * cnt : cnt;   // Math.pow(10,12) * W[last] (IPLS.java:1167)
+    }
+  }
+  const bool avg_aligned = FIN && !((uintptr_t)avg & 15);
+  // fused epilogue for element e holding fold value a: W = a + REP; avg = W / count
+  auto fin1 = [&](int64_t e, double a) {
+    const double w = a + (rep ? __builtin_bit_cast(double, ld8(rep + e)) : 0.0);
+    st8(dst + e, __builtin_bit_cast(unsigned long long, w));
+    if (avg && e < L - 1) st8(avg + e, __builtin_bit_cast(unsigned long long, cnt == 0.0 ? w : w / den));
+  };
 
   if (base + kTile <= L) {
     // ---------------- vector path: R x 16 B per lane ----------------
@@ -164,7 +192,7 @@ __global__ __launch_bounds__(BS) void k_reduce(
       } else if constexpr (START == kFirst) {
         acc[r] = decode2<BE_IN>(ld16<NT>(pb[0] + off[r]));
       } else {  // kAccum: the target holds native doubles (or BE if BE_OUT)
-        acc[r] = decode2<BE_OUT>(ld16<false>(dst + off[r]));
+        acc[r] = decode2<BE_OUT>(ld16<false>(init + off[r]));
       }
     }
     int j = j0;
@@ -198,8 +226,42 @@ __global__ __launch_bounds__(BS) void k_reduce(
         acc[r].y = acc[r].y + x.y;
       }
     }
+    if constexpr (FIN) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
+      for (int r = 0; r < R; ++r) {
+        d2 w = acc[r];
+        if (rep) {
+          const d2 y = decode2<false>(ld16<true>(rep + off[r]));
+          w.x = w.x + y.x;
+          w.y = w.y + y.y;
+        } else {
+          w.x = w.x + 0.0;   // AGG + REP with REP == +0.0, as AggregatePartition computes it
+          w.y = w.y + 0.0;
+        }
+        __builtin_nontemporal_store(encode2<false>(w), (gu2)(dst + off[r]));
+        if (avg) {
+          // averages of elements e, e+1 (e + 1 may be the count slot L-1, which is not output)
+          const int64_t e = off[r];
+          const double ax = cnt == 0.0 ? w.x : w.x / den;
+          const double ay = cnt == 0.0 ? w.y : w.y / den;
+          if (avg_aligned) {
+            if (e + 1 < L - 1) __builtin_nontemporal_store(encode2<false>(d2{ax, ay}), (gu2)(avg + e));
+            else st8(avg + e, __builtin_bit_cast(unsigned long long, ax));
+          } else {
+            // avg + e is 8 mod 16: lane t writes the aligned pair (e+1, e+2) =
+            // (its y, lane t+1's x); the wave's first x and last y go alone.
+            const double nx = __shfl_down(ax, 1);
+            const int lane = tid & 63;
+            if (lane == 0) st8(avg + e, __builtin_bit_cast(unsigned long long, ax));
+            if (lane < 63) __builtin_nontemporal_store(encode2<false>(d2{ay, nx}), (gu2)(avg + e + 1));
+            else if (e + 1 < L - 1) st8(avg + e + 1, __builtin_bit_cast(unsigned long long, ay));
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
+    }
   } else {
     // ------- partial last tile: 512-element vector steps, scalar remainder -------
     for (int64_t sb = base; sb < L; sb += 2 * kBlock) {
@@ -208,25 +270,48 @@ __global__ __launch_bounds__(BS) void k_reduce(
         d2 acc;
         if constexpr (START == kZero) acc = d2{0.0, 0.0};
         else if constexpr (START == kFirst) acc = decode2<BE_IN>(ld16<NT>(pb[0] + i));
-        else acc = decode2<BE_OUT>(ld16<false>(dst + i));
+        else acc = decode2<BE_OUT>(ld16<false>(init + i));
         for (int jj = j0; jj < k; ++jj) {
           const d2 x = decode2<BE_IN>(ld16<NT>(pb[jj] + i));
           acc.x = acc.x + x.x;
           acc.y = acc.y + x.y;
         }
-        __builtin_nontemporal_store(encode2<BE_OUT>(acc), (gu2)(dst + i));
+        if constexpr (FIN) {
+          fin1(i, acc.x);
+          fin1(i + 1, acc.y);
+        } else {
+          __builtin_nontemporal_store(encode2<BE_OUT>(acc), (gu2)(dst + i));
+        }
       } else {
         for (int64_t e = sb + tid; e < L; e += kBlock) {
           double acc;
           if constexpr (START == kZero) acc = 0.0;
           else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + e));
-          else acc = decode1<BE_OUT>(ld8(dst + e));
+          else acc = decode1<BE_OUT>(ld8(init + e));
           for (int jj = j0; jj < k; ++jj) acc = acc + decode1<BE_IN>(ld8(pb[jj] + e));
-          st8(dst + e, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
+          if constexpr (FIN) fin1(e, acc);
+          else st8(dst + e, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
         }
       }
     }
   }
+}
+
+// Count slot of a fused round, per partition (one lane each): the same fold
+// k_reduce<..., FIN> applies to element L-1, i.e. W[L-1] =
+// (init[L-1] | +0.0) + b_0[L-1] + ... + b_{k-1}[L-1] + (REP[L-1] | +0.0).
+template <bool BE_IN, int START>
+__global__ __launch_bounds__(kBlock) void k_round_counts(const unsigned long long* const* __restrict__ bufs,
+                                                         const PartDesc* __restrict__ parts, int k, int n_parts,
+                                                         double* __restrict__ cnts) {
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= n_parts) return;
+  const PartDesc d = parts[q];
+  const int64_t e = d.len - 1;
+  const unsigned long long* const* pb = bufs + (size_t)q * k;
+  double c = (START == kZero) ? 0.0 : __builtin_bit_cast(double, ld8(d.init + e));
+  for (int jj = 0; jj < k; ++jj) c = c + decode1<BE_IN>(ld8(pb[jj] + e));
+  cnts[q] = c + (d.rep ? __builtin_bit_cast(double, ld8(d.rep + e)) : 0.0);
 }
 
 // Same fold for buckets that are only 8-byte aligned (e.g. a device view into

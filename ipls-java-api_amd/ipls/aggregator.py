@@ -265,6 +265,33 @@ class Aggregator:
             self._h, p_first, n_parts, arr, k, N.DEV_BE if big_endian_in else N.DEV_F64, start_mode,
             darr, N.DEV_BE if big_endian_out else N.DEV_F64))
 
+    def aggregate_round(self, p_first: int, buckets, *, big_endian: bool = False, with_average: bool = True,
+                        out=None):
+        """A whole round in one launch: the folds of ``buckets`` (buckets[q] =
+        device buckets of partition p_first+q, may be empty lists) into AGG,
+        AggregatePartition (IPLS.java:1248-1274) and the GetPartitions divide
+        (IPLS.java:1159-1174).  Returns the averaged values of the partitions
+        (host array, or ``out`` when a DeviceBuffer is given), or None."""
+        n_parts = len(buckets)
+        k = len(buckets[0]) if n_parts else 0
+        flat = []
+        for row in buckets:
+            if len(row) != k:
+                raise ValueError("every partition needs the same number of buckets")
+            flat.extend(b.ptr if isinstance(b, DeviceBuffer) else int(b) for b in row)
+        arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
+        kind = N.DEV_BE if big_endian else N.DEV_F64
+        ap, ak, res = None, N.HOST_F64, None
+        if isinstance(out, DeviceBuffer):
+            ap, ak, res = out.ptr, N.DEV_F64, out
+        elif with_average:
+            last = p_first + n_parts - 1
+            n = self.offsets[last] + self.lengths[last] - 1 - self.offsets[p_first]
+            res = np.empty(max(0, n))
+            ap = res.ctypes.data if res.size else None
+        self._chk(self._lib.ipls_agg_aggregate_round(self._h, p_first, n_parts, arr, k, kind, ap, ak))
+        return res
+
     def Merge(self, partition: int, buckets, *, big_endian: bool = True, target: int = N.TGT_REP):
         """Storage-node merge (Decentralized_Storage_Receiver.java:239-247):
         S = g0; S += g_i -- a FIRST-start fold (it overwrites ``target``, so call

@@ -615,3 +615,127 @@ def test_encode_secure_device(ipls, O, golden):
     ipls.encode_secure(d, ipls.DeviceBuffer(int(o.data_ptr()), len(x), big_endian=True))
     torch.cuda.synchronize()
     assert bytes(o.cpu().numpy()) == O.be_encode(golden["enc_out"])
+
+
+# ---------------------------------------------------------------------------
+# fused round: folds + AggregatePartition + GetPartitions divide in one launch
+# ---------------------------------------------------------------------------
+def _round_oracle(O, own_prev, rounds_buckets, reps, secure=False):
+    """AGG = fold(prev arrivals) then fold(batch); W = AGG + REP; avg = divide(W)."""
+    out_w, out_avg = [], []
+    for prev, batch, rep in zip(own_prev, rounds_buckets, reps):
+        L = len(batch[0]) if batch else len(prev[0]) if prev else len(rep[0])
+        a = O.reduce(prev, L) if prev else np.zeros(L)
+        a = O.reduce(batch, L, O.START_ACCUM, acc=a) if batch else a
+        r = O.reduce(rep, L) if rep else np.zeros(L)
+        w = a + r
+        out_w.append(w)
+        out_avg.append(O.divide(w, secure))
+    return out_w, np.concatenate(out_avg)
+
+
+@pytest.mark.parametrize("be", [False, True])
+@pytest.mark.parametrize("secure", [False, True])
+def test_aggregate_round_model_geometry(ipls, O, be, secure):
+    """Ragged -pa geometry; partition 0 has earlier arrivals in AGG (ACCUM
+    start), partition 1 has replicas in REP, partition 2 starts from zero."""
+    M, P, K = 300007, 3, 5
+    agg = ipls.Aggregator(M, P, max_peers=K, secure=secure)
+    Ls = agg.lengths
+    prev = [[O.synth_bucket(Ls[0], 0, 90 + j) for j in range(2)], [], []]
+    reps = [[], [O.synth_bucket(Ls[1], 1, 80 + j) for j in range(3)], []]
+    batch = [[O.synth_bucket(Ls[p], p, k) for k in range(K)] for p in range(P)]
+    for b in prev[0]:
+        agg.Update(b, 0, from_clients=True)
+    for r in reps[1]:
+        agg.Update(r, 1, from_clients=False)
+    keep, rows = [], []
+    for p in range(P):
+        row = []
+        for b in batch[p]:
+            t, d = dev_be(b) if be else dev(b)
+            keep.append(t)
+            row.append(d)
+        rows.append(row)
+    avg = agg.aggregate_round(0, rows, big_endian=be)
+    ref_w, ref_avg = _round_oracle(O, prev, batch, reps, secure)
+    assert_bits_equal(avg, ref_avg, "avg")
+    for p in range(P):
+        assert_bits_equal(agg.read(p, ipls.TGT_WEIGHTS), ref_w[p], f"W[{p}]")
+        assert not agg.read(p, ipls.TGT_AGG).any() and not agg.read(p, ipls.TGT_REP).any()
+    # the unfused sequence gives the same model
+    assert_bits_equal(agg.GetPartitions(), ref_avg, "GetPartitions after round")
+    # next round starts from +0.0
+    agg.aggregate_round(0, [rows[0][:1]], big_endian=be, with_average=False)
+    assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), O.reduce(batch[0][:1], Ls[0]) + 0.0, "next round")
+    agg.close()
+
+
+@pytest.mark.parametrize("shift", [0, 1])
+def test_aggregate_round_big_shape_device_out(ipls, O, shift):
+    """1024-lane shape with a partial tile; averages into a device buffer
+    that is 16-B aligned (shift 0) or 8 mod 16 (shift 1: lane-pair stores)."""
+    P, L, K = 4, 2100001, 3
+    arena = torch.empty(P * K * (L + 1), dtype=torch.float64, device="cuda")
+    base = int(arena.data_ptr())
+    rows = [[ipls.DeviceBuffer(base + 8 * (p * K + k) * (L + 1), L) for k in range(K)] for p in range(P)]
+    for p in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[p][k], p, k, O.SEED)
+    out = torch.full((P * (L - 1) + 2,), 7.0, dtype=torch.float64, device="cuda")
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.Update(O.synth_bucket(L, 3, 77), 3, from_clients=False)    # one partition with REP
+    agg.aggregate_round(0, rows, out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1)))
+    torch.cuda.synchronize()
+    full = out.cpu().numpy()
+    got = full[shift:shift + P * (L - 1)]
+    assert full[:shift].tolist() == [7.0] * shift and full[shift + P * (L - 1):].tolist() == [7.0] * (2 - shift)
+    for p in (0, 3):
+        S = O.reduce([O.synth_bucket(L, p, k) for k in range(K)], L)
+        S = S + (O.synth_bucket(L, 3, 77) if p == 3 else 0.0)
+        assert_bits_equal(agg.read(p, ipls.TGT_WEIGHTS), S, f"W[{p}]")
+        assert_bits_equal(got[p * (L - 1):(p + 1) * (L - 1)], O.divide(S), f"avg[{p}]")
+    assert [agg.checksum(p, ipls.TGT_WEIGHTS) for p in (1, 2)] == \
+        [O.c_synth_sum_checksum(L, p, K) for p in (1, 2)]
+    agg.close()
+    del arena, out
+    torch.cuda.empty_cache()
+
+
+def test_aggregate_round_edges(ipls, O, golden):
+    """k = 0 (W = AGG + REP), a zero count slot (values pass through),
+    special values, a sub-range of partitions, 8-B aligned buckets (unfused
+    fallback)."""
+    L = 1031
+    agg = ipls.Aggregator(n_partitions=4, bucket_len=L)
+    b = O.synth_bucket(L, 0, 0)
+    agg.Update(b, 1, from_clients=True)
+    avg = agg.aggregate_round(1, [[]])
+    assert_bits_equal(avg, O.divide(b + 0.0), "k=0")
+    assert_bits_equal(agg.read(1, ipls.TGT_WEIGHTS), b + 0.0, "k=0 W")
+    # count slot 0 -> pass through; specials from the golden edge cases
+    z = O.synth_bucket(L, 2, 0)
+    z[-1] = 0.0
+    t1, d1 = dev(z)
+    avg = agg.aggregate_round(2, [[d1]])
+    assert_bits_equal(avg, O.divide(z + 0.0), "cnt 0")
+    # 8-B aligned buckets -> unfused path, same results
+    raw = torch.empty(2 * L + 1, dtype=torch.float64, device="cuda")
+    x = [O.synth_bucket(L, 3, k) for k in range(2)]
+    raw[1:L + 1] = torch.from_numpy(x[0]).cuda()
+    raw[L + 1:] = torch.from_numpy(x[1]).cuda()
+    base = int(raw.data_ptr())
+    avg = agg.aggregate_round(3, [[ipls.DeviceBuffer(base + 8, L), ipls.DeviceBuffer(base + 8 * (L + 1), L)]])
+    S = O.reduce(x, L)
+    assert_bits_equal(avg, O.divide(S), "unaligned")
+    assert_bits_equal(agg.read(3, ipls.TGT_WEIGHTS), S, "unaligned W")
+    agg.close()
+    # NaN / inf / -0.0 / subnormal buckets (golden), the count slot among them
+    sb = golden["special_bufs"]
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=sb.shape[1])
+    keep = [dev(r) for r in sb]
+    avg = agg.aggregate_round(0, [[d for _, d in keep]])
+    W = golden["special_zero"] + 0.0
+    assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), W, "special W")
+    assert_bits_equal(avg, O.divide(W), "special avg")
+    agg.close()
