@@ -43,6 +43,7 @@ CONFIGS = {
     "B": (16, 1048576, 8),
     "C": (16, 4194304, 32),
     "D": (64, 4194304, 32),
+    "F": (16, 8388608, 64),     # per GPU; 69.8 GB of buckets resident in HBM
 }
 
 
@@ -52,6 +53,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
+    ap.add_argument("--strong", action="store_true",
+                    help="fixed total work: the config's partitions are split over the ranks "
+                         "(default: weak scaling, the config per GPU)")
     ap.add_argument("--be", action="store_true",
                     help="buckets are big-endian IPFS bytes and the sum is written as BE bytes "
                          "(fused unpack + pack, config D's timed pack/unpack)")
@@ -172,7 +176,11 @@ def main():
 
     import ipls
     P, L, K = CONFIGS[args.config]
-    p0 = rank * P                                  # this GPU's -pa segment
+    if args.strong:
+        if P % world:
+            sys.exit(f"--strong: {P} partitions do not split over {world} ranks")
+        P //= world
+    p0 = rank * P                                  # this GPU's -pa segment (contiguous block)
     elem = L + 32                                  # 256-B pad between buckets
     arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
     base = (int(arena.data_ptr()) + 255) // 256 * 256
@@ -297,12 +305,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (splitmix64 counter buckets generated on device, SURVEY.md 8(d))",
             "config": {
                 "workload": f"{args.config}: {P} partitions x {L} doubles x {K} peers per GPU"
+                            + (f" ({P * world} in total, split over {world} GPUs)" if args.strong else "")
                             + (" (BE IPFS bytes in, BE sum bytes out: fused unpack/pack)" if args.be else ""),
                 "partitions": P * world, "bucket_len": L, "peers": K,
                 "parallelism": f"partition-sharded x{world} (no data-path collective)",

@@ -399,7 +399,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
     if ((uintptr_t)pd[q].dst & 7) return fail(h, IPLS_E_INVAL, "destination %d not 8-byte aligned", q);
     if ((uintptr_t)pd[q].dst & 15) aligned16 = false;
   }
-  std::memcpy(tbl.data() + desc_bytes, bufs, sizeof(void*) * (size_t)n_parts * k);
+  if (k > 0) std::memcpy(tbl.data() + desc_bytes, bufs, sizeof(void*) * (size_t)n_parts * k);
   void* dtab = nullptr;
   int rc = upload_table(h, tbl.data(), bytes, &dtab);
   if (rc) return rc;

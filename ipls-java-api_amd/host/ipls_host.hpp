@@ -16,6 +16,7 @@
 // throws at the same spot (ArrayIndexOutOfBoundsException, ...).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -232,6 +233,16 @@ class IPLS {
           h_.get());
   }
 
+  // AggregatePartition for every partition + GetPartitions, fused
+  // (ipls_agg_aggregate_round with no further buckets).
+  std::vector<double> AggregateRound() {
+    std::vector<double> out((size_t)cfg_._MODEL_SIZE);
+    check(ipls_agg_aggregate_round(h_.get(), 0, cfg_._PARTITIONS, nullptr, 0, IPLS_DEV_F64, out.data(),
+                                   IPLS_HOST_F64),
+          h_.get());
+    return out;
+  }
+
   // GetPartitions (IPLS.java:1080-1178), the synchronous steady-state branch.
   std::vector<double> GetPartitions() const {
     std::vector<double> out((size_t)cfg_._MODEL_SIZE);
@@ -293,6 +304,13 @@ class Light_IPLS_Daemon {
   explicit Light_IPLS_Daemon(IPLS& ipls) : ipls_(ipls) {}
   void UpdateModel(const std::vector<double>& Gradients) { ipls_.UpdateGradient(&Gradients); }
   std::vector<double> Get_Partitions() {
+    // Responsible for every partition: AggregatePartition for all of them and
+    // the divide are one fused launch (the update_file bytes are not needed here).
+    std::vector<int> sorted = ipls_.Auth_List;
+    std::sort(sorted.begin(), sorted.end());
+    bool all = (int)sorted.size() == ipls_.peer_data()._PARTITIONS;
+    for (int i = 0; all && i < (int)sorted.size(); ++i) all = sorted[i] == i;
+    if (all) return ipls_.AggregateRound();
     for (int p : ipls_.Auth_List) ipls_.AggregatePartition(p);
     return ipls_.GetPartitions();
   }

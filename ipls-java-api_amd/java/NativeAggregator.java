@@ -77,6 +77,14 @@ public final class NativeAggregator implements AutoCloseable {
         return out;
     }
 
+    /** AggregatePartition for partitions [pFirst, pFirst+nParts) and their
+     *  GetPartitions averages in one fused launch (ipls_agg_aggregate_round). */
+    public double[] aggregateRound(int pFirst, int nParts, int nValues) {
+        double[] out = new double[nValues];
+        aggregateRound(handle, pFirst, nParts, out);
+        return out;
+    }
+
     /** Middleware task 3: the writeDouble stream in one bulk write. */
     public void getPartitionsWire(ByteBuffer direct) { getPartitionsWire(handle, direct); }
 
@@ -97,6 +105,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void finalizePartition(long h, int p, byte[] sumOut);
     private static native void setWeightsDirect(long h, int p, ByteBuffer buf, long n);
     private static native void getPartitions(long h, double[] out);
+    private static native void aggregateRound(long h, int pFirst, int nParts, double[] avgOut);
     private static native void getPartitionsWire(long h, ByteBuffer direct);
     private static native ByteBuffer hostAllocDirect(int bytes);
 }

@@ -137,6 +137,15 @@ JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c
     CHECK(rc, H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_aggregateRound(JNIEnv *env, jclass c, jlong h, jint p0, jint np,
+                                                              jdoubleArray out) {
+    (void)c;
+    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    int rc = ipls_agg_aggregate_round(H(h), p0, np, NULL, 0, IPLS_DEV_F64, dst, IPLS_HOST_F64);
+    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    CHECK(rc, H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf) {
     (void)c;
     jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
