@@ -57,6 +57,9 @@ extern "C" {
 #define IPLS_TGT_REP      1  /* PeerData.Replicas_Gradients[p]    */
 #define IPLS_TGT_WEIGHTS  2  /* PeerData.Weights[p]               */
 #define IPLS_TGT_WADDR    3  /* PeerData.Weight_Address[p]        */
+#define IPLS_TGT_FUTURE   4  /* PeerData.Aggregated_Gradients_from_future[p]
+                                (Updater.java:99-101: a client's bucket for a
+                                later iteration) */
 
 /* ---- operand kinds ---- */
 #define IPLS_HOST_F64     0  /* host double[] (native byte order)                          */
@@ -215,6 +218,12 @@ int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
 /* Copy an accumulator out (tests, replica publish IPLS.java:1423-1431).
  * dst_kind HOST_F64, HOST_BE, DEV_F64, DEV_BE; n >= L_p. */
 int ipls_agg_read(ipls_agg *h, int p, int target, void *dst, int64_t n, int dst_kind);
+
+/* End of IPLS.Update_Client_WaitAck_List (IPLS.java:1556-1562): for every p
+ * in parts[0..n_parts): AGG[p] = FUTURE[p]; FUTURE[p] = 0.  O(1) per partition
+ * (the two accumulators swap storage), so an address from ipls_agg_device_ptr
+ * for AGG or FUTURE of such a p is stale afterwards. */
+int ipls_agg_promote_future(ipls_agg *h, const int32_t *parts, int n_parts);
 
 /* Zero AGG[p] and REP[p] (IPLS.java:1268-1269); p may be IPLS_ALL_PARTITIONS. */
 int ipls_agg_reset(ipls_agg *h, int p);

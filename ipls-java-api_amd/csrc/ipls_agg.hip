@@ -64,8 +64,8 @@ struct ipls_agg {
   // arena
   double* arena = nullptr;
   int64_t arena_elems = 0;
-  std::vector<int64_t> agg_off, rep_off, w_off;
-  std::vector<uint8_t> agg_zero, rep_zero;  // "logically +0.0" flags
+  std::vector<int64_t> agg_off, rep_off, w_off, fut_off;
+  std::vector<uint8_t> agg_zero, rep_zero, fut_zero;  // "logically +0.0" flags
 
   // table upload ring (pinned host slots -> device slots)
   PinnedSlot ring[kRingSlots];
@@ -120,6 +120,7 @@ int64_t target_off(ipls_agg* h, int p, int target) {
     case IPLS_TGT_REP: return h->rep_off[p];
     case IPLS_TGT_WEIGHTS:
     case IPLS_TGT_WADDR: return h->w_off[p];
+    case IPLS_TGT_FUTURE: return h->fut_off[p];
     default: return -1;
   }
 }
@@ -127,6 +128,7 @@ int64_t target_off(ipls_agg* h, int p, int target) {
 uint8_t* zero_flag(ipls_agg* h, int p, int target) {
   if (target == IPLS_TGT_AGG) return &h->agg_zero[p];
   if (target == IPLS_TGT_REP) return &h->rep_zero[p];
+  if (target == IPLS_TGT_FUTURE) return &h->fut_zero[p];
   return nullptr;
 }
 
@@ -514,8 +516,10 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
   h->agg_off.resize(h->P);
   h->rep_off.resize(h->P);
   h->w_off.resize(h->P);
+  h->fut_off.resize(h->P);
   h->agg_zero.assign(h->P, 1);
   h->rep_zero.assign(h->P, 1);
+  h->fut_zero.assign(h->P, 1);
   int64_t cur = 0;
   for (int p = 0; p < h->P; ++p) {
     h->max_len = std::max(h->max_len, h->len[p]);
@@ -523,6 +527,7 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
     h->agg_off[p] = cur; cur = align_up(cur + h->len[p], kAlignElems);
     h->rep_off[p] = cur; cur = align_up(cur + h->len[p], kAlignElems);
     h->w_off[p] = cur;   cur = align_up(cur + h->len[p], kAlignElems);
+    h->fut_off[p] = cur; cur = align_up(cur + h->len[p], kAlignElems);
   }
   h->arena_elems = cur;
   auto cleanup = [&](int code) {
@@ -674,6 +679,22 @@ int ipls_agg_reset(ipls_agg* h, int p) {
   }
   if (int rc = check_part(h, p)) return rc;
   h->agg_zero[p] = h->rep_zero[p] = 1;
+  return IPLS_OK;
+}
+
+int ipls_agg_promote_future(ipls_agg* h, const int32_t* parts, int n_parts) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (n_parts < 0 || (n_parts > 0 && !parts)) return fail(h, IPLS_E_INVAL, "bad partition list");
+  for (int i = 0; i < n_parts; ++i)
+    if (int rc = check_part(h, parts[i])) return rc;
+  for (int i = 0; i < n_parts; ++i) {
+    const int p = parts[i];
+    // AGG[p][j] = FUTURE[p].get(j); FUTURE[p].set(j, 0.0)   (IPLS.java:1558-1561)
+    std::swap(h->agg_off[p], h->fut_off[p]);
+    h->agg_zero[p] = h->fut_zero[p];
+    h->fut_zero[p] = 1;
+  }
   return IPLS_OK;
 }
 
@@ -914,7 +935,7 @@ int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {
       hipLaunchKernelGGL(k_load_model<false>, dim3(blocks_for(L, kBlock)), dim3(kBlock), 0, h->stream, d,
                          h->flat_off[p], L - 1, L, h->arena + h->w_off[p]);
     HIP_TRY(h, hipGetLastError());
-    h->agg_zero[p] = h->rep_zero[p] = 1;
+    h->agg_zero[p] = h->rep_zero[p] = h->fut_zero[p] = 1;   // IPLS.java:1886-1898
   }
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return IPLS_OK;

@@ -227,6 +227,12 @@ class IPLS {
     return file;
   }
 
+  // Tail of Update_Client_WaitAck_List (IPLS.java:1556-1562): for p in
+  // Auth_List, Aggregated_Gradients[p] = from_future[p], from_future[p] = 0.
+  void Update_Client_WaitAck_List() {
+    check(ipls_agg_promote_future(h_.get(), Auth_List.data(), (int)Auth_List.size()), h_.get());
+  }
+
   // Download_Scheduler.cache_partition (:752-754): Weight_Address[p] = GetParameters(hash)
   void cache_partition(int Partition, const std::vector<uint8_t>& file_bytes) {
     check(ipls_agg_set_weights(h_.get(), Partition, file_bytes.data(), (int64_t)file_bytes.size() / 8, IPLS_HOST_BE),
@@ -282,6 +288,14 @@ class Updater {
   void _Update_from_file(const std::vector<uint8_t>& ipfs_cat_bytes, int Partiton, bool from_clients) {
     check(ipls_agg_accumulate(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
                               ipfs_cat_bytes.data(), (int64_t)ipfs_cat_bytes.size() / 8, IPLS_HOST_BE),
+          ipls_.handle());
+  }
+  // The "gradients from the future" branch (Updater.java:91-101): a client's
+  // bucket for a later iteration folds into Aggregated_Gradients_from_future.
+  void _Update_from_future(const std::vector<double>* Gradient, int Partiton) {
+    if (!Gradient) return;
+    check(ipls_agg_accumulate(ipls_.handle(), Partiton, IPLS_TGT_FUTURE, Gradient->data(),
+                              (int64_t)Gradient->size(), IPLS_HOST_F64),
           ipls_.handle());
   }
   // ThreadReceiver pid 3 -> queue -> _Update (IPLS.java:453-465): a decoded frame.

@@ -7,7 +7,7 @@ binding plus the Middleware wire codec.
 """
 from ._native import (  # noqa: F401
     ALL_PARTITIONS, DEV_BE, DEV_F64, HOST_BE, HOST_BE_CANON, HOST_F64, HOST_FRAME,
-    START_ACCUM, START_FIRST, START_ZERO, TGT_AGG, TGT_REP, TGT_WADDR, TGT_WEIGHTS,
+    START_ACCUM, START_FIRST, START_ZERO, TGT_AGG, TGT_FUTURE, TGT_REP, TGT_WADDR, TGT_WEIGHTS,
     IplsError, lib,
 )
 from .aggregator import (  # noqa: F401

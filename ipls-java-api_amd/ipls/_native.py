@@ -20,7 +20,7 @@ IPLS_OK = 0
 IPLS_E_INVAL, IPLS_E_RANGE, IPLS_E_NEGSIZE, IPLS_E_NOMEM = -1, -2, -3, -4
 IPLS_E_DEVICE, IPLS_E_FORMAT, IPLS_E_NODEV = -5, -6, -7
 
-TGT_AGG, TGT_REP, TGT_WEIGHTS, TGT_WADDR = 0, 1, 2, 3
+TGT_AGG, TGT_REP, TGT_WEIGHTS, TGT_WADDR, TGT_FUTURE = 0, 1, 2, 3, 4
 HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON = 0, 1, 2, 3, 4, 5
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1
@@ -76,6 +76,7 @@ SIGNATURES = {
     "ipls_agg_reduce_batch": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _i]),
     "ipls_agg_reduce_batch_out": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _i, _P(_vp), _i]),
     "ipls_agg_aggregate_round": (_i, [_vp, _i, _i, _P(_vp), _i, _i, _vp, _i]),
+    "ipls_agg_promote_future": (_i, [_vp, _P(ctypes.c_int32), _i]),
     "ipls_agg_ingest_pubsub": (_i, [_vp, _i, _P(_vp), _P(_i64), _i, _i, _P(_i32), _P(_i32)]),
     "ipls_agg_blend": (_i, [_vp, _i, _i, _vp, _i64, _i, ctypes.c_double, ctypes.c_double]),
     "ipls_agg_scale": (_i, [_vp, _i, _i, _i, ctypes.c_double]),

@@ -176,15 +176,18 @@ class Aggregator:
         self._chk(self._lib.ipls_agg_update_gradient(
             self._h, ptr, n, kind, owned.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(owned)))
 
-    def Update(self, gradient, partition: int, from_clients: bool = True, *, frame: bool = False):
+    def Update(self, gradient, partition: int, from_clients: bool = True, *, frame: bool = False,
+               from_future: bool = False):
         """Updater._Update: client buckets fold into Aggregated_Gradients
         (Updater.java:115-117), replica partial sums into Replicas_Gradients
-        (Updater.java:40-44).  ``gradient`` may be doubles, big-endian file
+        (Updater.java:40-44), and a client's bucket for a later iteration
+        (``from_future=True``) into Aggregated_Gradients_from_future
+        (Updater.java:99-101).  ``gradient`` may be doubles, big-endian file
         bytes (GetParameters input), a pubsub frame (``frame=True``) or a
         DeviceBuffer.  ``None`` is a no-op, as in the reference."""
         if gradient is None:
             return
-        target = N.TGT_AGG if from_clients else N.TGT_REP
+        target = N.TGT_FUTURE if from_future else (N.TGT_AGG if from_clients else N.TGT_REP)
         if frame:
             a = np.frombuffer(bytes(gradient), dtype=np.uint8)
             self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, a.ctypes.data,
@@ -192,6 +195,14 @@ class Aggregator:
             return
         ptr, n, kind, keep = _operand(gradient)
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
+
+    def PromoteFuture(self, partitions):
+        """End of Update_Client_WaitAck_List (IPLS.java:1556-1562): for p in
+        ``partitions`` (the Auth_List), Aggregated_Gradients[p] =
+        Aggregated_Gradients_from_future[p], and the latter is zeroed."""
+        parts = np.ascontiguousarray(list(partitions), dtype=np.int32)
+        self._chk(self._lib.ipls_agg_promote_future(
+            self._h, parts.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), parts.size))
 
     def ingest_pubsub(self, messages, *, from_clients: bool = True, layers: int = 2, partitions=None):
         """ThreadReceiver (IPLS.java:851-866, 453-465): a batch of pubsub

@@ -14,7 +14,7 @@ public final class NativeAggregator implements AutoCloseable {
     static { System.loadLibrary("ipls_jni"); }   // links libipls_agg.so
 
     // include/ipls_agg.h constants
-    public static final int TGT_AGG = 0, TGT_REP = 1, TGT_WEIGHTS = 2, TGT_WADDR = 3;
+    public static final int TGT_AGG = 0, TGT_REP = 1, TGT_WEIGHTS = 2, TGT_WADDR = 3, TGT_FUTURE = 4;
     public static final int START_ACCUM = 0, START_ZERO = 1, START_FIRST = 2;
     public static final int ALL_PARTITIONS = -1;
 
@@ -52,6 +52,14 @@ public final class NativeAggregator implements AutoCloseable {
     public void updateFromFile(ByteBuffer beDoubles, int p, boolean fromClients) {
         accumulateDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
     }
+
+    /** Updater.java:99-101: a client's bucket for a later iteration. */
+    public void updateFromFuture(double[] gradient, int p) {
+        if (gradient != null) accumulate(handle, p, TGT_FUTURE, gradient);
+    }
+
+    /** Tail of Update_Client_WaitAck_List (IPLS.java:1556-1562). */
+    public void promoteFuture(int[] authList) { promoteFuture(handle, authList); }
 
     /** ThreadReceiver pid 3: a decoded (base64) pubsub frame. */
     public void updateFromFrame(byte[] frame, int p, boolean fromClients) {
@@ -106,6 +114,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void setWeightsDirect(long h, int p, ByteBuffer buf, long n);
     private static native void getPartitions(long h, double[] out);
     private static native void aggregateRound(long h, int pFirst, int nParts, double[] avgOut);
+    private static native void promoteFuture(long h, int[] parts);
     private static native void getPartitionsWire(long h, ByteBuffer direct);
     private static native ByteBuffer hostAllocDirect(int bytes);
 }

@@ -146,6 +146,15 @@ JNIEXPORT void JNICALL Java_NativeAggregator_aggregateRound(JNIEnv *env, jclass 
     CHECK(rc, H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c, jlong h, jintArray parts) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, parts);
+    jint *ps = (*env)->GetIntArrayElements(env, parts, NULL);
+    int rc = ipls_agg_promote_future(H(h), (const int32_t *)ps, n);
+    (*env)->ReleaseIntArrayElements(env, parts, ps, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf) {
     (void)c;
     jlong cap = (*env)->GetDirectBufferCapacity(env, buf);

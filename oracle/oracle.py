@@ -110,6 +110,13 @@ def aggregate_partition(agg, rep, w, wa):
     rep[:] = 0.0
 
 
+def promote_future(agg: np.ndarray, fut: np.ndarray) -> None:
+    """IPLS.java:1557-1562 (Update_Client_WaitAck_List): for j < L,
+    Aggregated_Gradients[p][j] = from_future[p].get(j); from_future[p].set(j, 0.0)."""
+    agg[:] = fut
+    fut[:] = 0.0
+
+
 def divide(w: np.ndarray, secure: bool = False) -> np.ndarray:
     """GetPartitions, IPLS.java:1159-1174, one partition -> len(w)-1 values."""
     w = np.asarray(w, dtype=np.float64)

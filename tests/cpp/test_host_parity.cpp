@@ -192,6 +192,26 @@ int main(int argc, char** argv) {
       CHECK(file == ref, "update_file bytes of AGG + REP");
     });
 
+    run("gradients from the future -> Update_Client_WaitAck_List", [&] {
+      PeerData pd;
+      pd._MODEL_SIZE = 50001;
+      pd._PARTITIONS = 2;
+      IPLS ipls(pd, {0, 1});
+      Updater u(ipls);
+      const int64_t L0 = ipls_oracle_partition_len(50001, 2, 0);
+      auto now = synth(L0, 0, 1), later = synth(L0, 0, 2);
+      u._Update(&now, 0, true);
+      u._Update_from_future(&later, 0);
+      auto first = ipls.AggregatePartition(0);          // this round: `now` only
+      std::vector<uint8_t> ref(8 * (size_t)L0);
+      ipls_oracle_be_encode(now.data(), L0, ref.data());
+      CHECK(first == ref, "round before promotion");
+      ipls.Update_Client_WaitAck_List();
+      auto second = ipls.AggregatePartition(0);         // next round starts from `later`
+      ipls_oracle_be_encode(later.data(), L0, ref.data());
+      CHECK(second == ref, "promoted future gradients");
+    });
+
     run("exceptions", [] {
       PeerData pd;
       pd._MODEL_SIZE = 10;

@@ -739,3 +739,43 @@ def test_aggregate_round_edges(ipls, O, golden):
     assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), W, "special W")
     assert_bits_equal(avg, O.divide(W), "special avg")
     agg.close()
+
+
+def test_future_accumulator_and_promotion(ipls, O):
+    """Updater.java:99-101 folds a bucket for a later iteration into
+    Aggregated_Gradients_from_future; Update_Client_WaitAck_List
+    (IPLS.java:1556-1562) then makes it the new AGG and zeroes it."""
+    M, P = 200003, 4
+    agg = ipls.Aggregator(M, P, max_peers=4)
+    Ls = agg.lengths
+    now = [[O.synth_bucket(Ls[p], p, k) for k in range(2)] for p in range(P)]
+    fut = [[O.synth_bucket(Ls[p], p, 10 + k) for k in range(3)] for p in range(P)]
+    for p in range(P):
+        for b in now[p]:
+            agg.Update(b, p)
+        for b in fut[p]:
+            agg.Update(O.be_encode(b), p, from_future=True)       # BE file bytes
+    # this round sees only the current-iteration buckets
+    for p in range(P):
+        assert_bits_equal(agg.read(p), O.reduce(now[p], Ls[p]), f"AGG[{p}]")
+        assert_bits_equal(agg.read(p, ipls.TGT_FUTURE), O.reduce(fut[p], Ls[p]), f"FUT[{p}]")
+    avg = agg.aggregate_round(0, [[] for _ in range(P)])
+    assert_bits_equal(avg, O.get_partitions([O.reduce(now[p], Ls[p]) for p in range(P)]), "round 1")
+    # promotion for the Auth_List {1, 3}; 0 and 2 keep an empty AGG and their FUT
+    agg.PromoteFuture([1, 3])
+    ref_agg = [np.zeros(L) for L in Ls]
+    ref_fut = [O.reduce(fut[p], Ls[p]) for p in range(P)]
+    for p in (1, 3):
+        O.promote_future(ref_agg[p], ref_fut[p])
+    for p in range(P):
+        assert_bits_equal(agg.read(p), ref_agg[p], f"AGG after promote [{p}]")
+        assert_bits_equal(agg.read(p, ipls.TGT_FUTURE), ref_fut[p], f"FUT after promote [{p}]")
+    # the next iteration's arrivals fold on top of the promoted sums
+    extra = O.synth_bucket(Ls[1], 1, 99)
+    agg.Update(extra, 1)
+    assert_bits_equal(agg.read(1), O.reduce([extra], Ls[1], O.START_ACCUM, acc=ref_agg[1].copy()), "fold after")
+    agg.Update(extra, 1, from_future=True)
+    assert_bits_equal(agg.read(1, ipls.TGT_FUTURE), O.reduce([extra], Ls[1]), "FUT refills from +0.0")
+    with pytest.raises(ipls.IplsError):
+        agg.PromoteFuture([P])
+    agg.close()

@@ -171,3 +171,14 @@ def test_updater_loop_baseline_matches_reduce():
     bufs = [O.synth_bucket(L, 1, k) for k in range(K)]
     be = [np.frombuffer(O.be_encode(b), dtype=np.uint8).copy() for b in bufs]
     assert_bits_equal(O.c_updater_loop(be, L), O.reduce(bufs, L), "updater loop")
+
+
+def test_promote_future_oracle():
+    """IPLS.java:1557-1562: AGG takes FUTURE's values (bits, incl. -0.0/NaN), FUTURE -> +0.0."""
+    from oracle import oracle as O
+    fut = np.array([1.5, -0.0, np.nan, 5e-324])
+    agg = np.array([9.0, 9.0, 9.0, 9.0])
+    ref = fut.copy()
+    O.promote_future(agg, fut)
+    assert agg.view(np.uint64).tolist() == ref.view(np.uint64).tolist()
+    assert fut.view(np.uint64).tolist() == [0, 0, 0, 0]
