@@ -138,6 +138,17 @@ int ipls_agg_update_gradient(ipls_agg *h, const void *flat, int64_t n, int src_k
 int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t n,
                         int src_kind);
 
+/* Updater.run's indirect request (Updater.java:176-187): the queue item holds
+ * only a hash, so the bucket is `ipfs cat` bytes read into the Updater's one
+ * reusable Gradient_Buff of (int)M/P + 2 doubles (Updater.java:162, zeroed
+ * once) by GetParameters(hash, Gradient_Buff) (MyIPFSClass.java:444-455), and
+ * _Update folds Gradient_Buff[0..L_p) into target[p].  Exactly as in Java, a
+ * file shorter than L_p leaves the tail of the previous request in the buffer
+ * and that tail is folded; a file longer than the buffer overwrites the
+ * buffer, folds nothing and returns IPLS_E_RANGE (the AIOOBE).  The handle
+ * owns the buffer (one per handle, like one Updater thread per peer). */
+int ipls_agg_update_indirect(ipls_agg *h, int p, int target, const void *bytes, int64_t n_bytes);
+
 /* Batched fixed-order fold, ONE kernel launch for n_parts partitions:
  *   for q in [0,n_parts): target[p_first+q] = fold(start_mode; bufs[q*k + 0..k-1])
  * bufs are device pointers (DEV_F64 or DEV_BE), each at least L_p long.

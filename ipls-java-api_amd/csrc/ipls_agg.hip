@@ -83,6 +83,8 @@ struct ipls_agg {
   // checksum result
   unsigned long long* d_sum = nullptr;
   double* d_cnt = nullptr;   // per-partition count slots of a fused round (P doubles)
+  unsigned long long* d_gbuf = nullptr;   // Updater.run's Gradient_Buff (Updater.java:162), lazily
+  int64_t gbuf_len = 0;
 };
 
 namespace {
@@ -530,6 +532,8 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
     h->fut_off[p] = cur; cur = align_up(cur + h->len[p], kAlignElems);
   }
   h->arena_elems = cur;
+  // new double[(int)_MODEL_SIZE/_PARTITIONS + 2] (Updater.java:162)
+  h->gbuf_len = h->model_size > 0 ? (int64_t)((int32_t)h->model_size / h->P) + 2 : cfg->bucket_len;
   auto cleanup = [&](int code) {
     ipls_agg_close(h);
     return code;
@@ -566,6 +570,7 @@ int ipls_agg_close(ipls_agg* h) {
   if (h->d_scratch) hipFree(h->d_scratch);
   if (h->d_sum) hipFree(h->d_sum);
   if (h->d_cnt) hipFree(h->d_cnt);
+  if (h->d_gbuf) hipFree(h->d_gbuf);
   if (h->arena) hipFree(h->arena);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
@@ -668,6 +673,54 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
   }
   const void* bl[1] = {dptr};
   return reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target);
+}
+
+int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, int64_t n_bytes) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
+  HIP_TRY(h, hipSetDevice(h->device));
+  const int64_t G = h->gbuf_len;
+  if (!h->d_gbuf) {   // the Java loop fills it with 0.0 before the first request (Updater.java:165-167)
+    HIP_TRY(h, hipMalloc(&h->d_gbuf, (size_t)std::max<int64_t>(G, 1) * 8));
+    HIP_TRY(h, hipMemsetAsync(h->d_gbuf, 0, (size_t)std::max<int64_t>(G, 1) * 8, h->stream));
+  }
+  // GetParameters(hash, Gradient_Buff) (MyIPFSClass.java:444-455): arr[i] =
+  // getDouble() for i < data.length/8; past arr.length it throws after the
+  // in-range stores.  Entries beyond the file keep the previous request's values.
+  const int64_t nd = n_bytes / 8;
+  const int64_t nw = std::min(nd, G);
+  bool zero_copy = false;
+  if (nw > 0) {
+    const void* dsrc = nullptr;
+    void* alias = nullptr;
+    if (((uintptr_t)bytes & 7) == 0 && (size_t)nw * 8 >= (1u << 16) && is_pinned_host(bytes, &alias) && alias) {
+      dsrc = alias;
+      zero_copy = true;
+    } else {
+      if (int rc = ensure_scratch(h, (size_t)nw * 8)) return rc;
+      if (int rc = stage_h2d(h, h->d_scratch, bytes, (size_t)nw * 8)) return rc;
+      dsrc = h->d_scratch;
+    }
+    hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(nw, kBlock), 4096)), dim3(kBlock), 0,
+                       h->stream, (const unsigned long long*)dsrc, h->d_gbuf, nw);
+    HIP_TRY(h, hipGetLastError());
+  }
+  if (nd > G) {
+    if (zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return fail(h, IPLS_E_RANGE, "GetParameters: %lld doubles > Gradient_Buff length %lld "
+                "(ArrayIndexOutOfBoundsException, MyIPFSClass.java:451)", (long long)nd, (long long)G);
+  }
+  // _Update(Gradient_Buff, ...): target[p][i] += Gradient_Buff[i], i < L_p
+  if (h->len[p] > G)
+    return fail(h, IPLS_E_RANGE, "partition length %lld > Gradient_Buff length %lld", (long long)h->len[p],
+                (long long)G);
+  const void* bl[1] = {h->d_gbuf};
+  if (int rc = reduce_dev(h, p, 1, bl, 1, false, IPLS_START_ACCUM, target)) return rc;
+  if (zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
 }
 
 int ipls_agg_reset(ipls_agg* h, int p) {

@@ -285,9 +285,10 @@ class Updater {
   // run(): a queue item with a hash and no payload -- GetParameters(hash,
   // Gradient_Buff) then _Update (Updater.java:176-187).  The BE decode is
   // fused into the device fold.
+  // Like Java, the bytes go through the one reusable Gradient_Buff.
   void _Update_from_file(const std::vector<uint8_t>& ipfs_cat_bytes, int Partiton, bool from_clients) {
-    check(ipls_agg_accumulate(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
-                              ipfs_cat_bytes.data(), (int64_t)ipfs_cat_bytes.size() / 8, IPLS_HOST_BE),
+    check(ipls_agg_update_indirect(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
+                                   ipfs_cat_bytes.data(), (int64_t)ipfs_cat_bytes.size()),
           ipls_.handle());
   }
   // The "gradients from the future" branch (Updater.java:91-101): a client's

@@ -196,6 +196,21 @@ class Aggregator:
         ptr, n, kind, keep = _operand(gradient)
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
 
+    def UpdateIndirect(self, file_bytes, partition: int, from_clients: bool = True, *,
+                       from_future: bool = False):
+        """Updater.run for a queue item with only a hash (Updater.java:176-187):
+        GetParameters(hash, Gradient_Buff) then _Update(Gradient_Buff, ...),
+        with the reference's reusable Gradient_Buff (a short file folds the
+        previous request's tail; a file longer than the buffer raises the
+        AIOOBE after overwriting it).  ``file_bytes``: the `ipfs cat` bytes."""
+        target = N.TGT_FUTURE if from_future else (N.TGT_AGG if from_clients else N.TGT_REP)
+        if isinstance(file_bytes, PinnedBuffer):
+            ptr, nb = file_bytes.ptr, file_bytes.nbytes
+        else:
+            a = np.frombuffer(bytes(file_bytes), dtype=np.uint8)
+            ptr, nb = (a.ctypes.data if a.size else None), a.size
+        self._chk(self._lib.ipls_agg_update_indirect(self._h, partition, target, ptr, nb))
+
     def PromoteFuture(self, partitions):
         """End of Update_Client_WaitAck_List (IPLS.java:1556-1562): for p in
         ``partitions`` (the Auth_List), Aggregated_Gradients[p] =

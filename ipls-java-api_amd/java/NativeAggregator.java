@@ -48,8 +48,15 @@ public final class NativeAggregator implements AutoCloseable {
         if (gradient != null) accumulate(handle, p, fromClients ? TGT_AGG : TGT_REP, gradient);
     }
 
-    /** Updater indirect mode: the bytes of an IPFS gradient file (GetParameters input). */
-    public void updateFromFile(ByteBuffer beDoubles, int p, boolean fromClients) {
+    /** Updater indirect mode (Updater.java:176-187): the `ipfs cat` bytes of a
+     *  gradient file go through the handle's Gradient_Buff, as GetParameters(hash,
+     *  Gradient_Buff) + _Update do (short files fold the previous file's tail). */
+    public void updateFromFile(ByteBuffer catBytes, int p, boolean fromClients) {
+        updateIndirect(handle, p, fromClients ? TGT_AGG : TGT_REP, catBytes, catBytes.remaining());
+    }
+
+    /** A bucket already decoded to exactly L_p big-endian doubles (no Gradient_Buff). */
+    public void updateFromBytes(ByteBuffer beDoubles, int p, boolean fromClients) {
         accumulateDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
     }
 
@@ -110,6 +117,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void accumulate(long h, int p, int target, double[] g);
     private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
     private static native void accumulateFrame(long h, int p, int target, byte[] frame);
+    private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, long nBytes);
     private static native void finalizePartition(long h, int p, byte[] sumOut);
     private static native void setWeightsDirect(long h, int p, ByteBuffer buf, long n);
     private static native void getPartitions(long h, double[] out);

@@ -103,6 +103,13 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclas
     CHECK(ipls_agg_accumulate(H(h), p, tgt, src, n, kind), H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
+                                                              jobject buf, jlong nBytes) {
+    (void)c;
+    void *src = (*env)->GetDirectBufferAddress(env, buf);
+    CHECK(ipls_agg_update_indirect(H(h), p, tgt, src, nBytes), H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateFrame(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                                jbyteArray frame) {
     (void)c;

@@ -110,6 +110,22 @@ def aggregate_partition(agg, rep, w, wa):
     rep[:] = 0.0
 
 
+def get_parameters_into(arr: np.ndarray, data: bytes) -> None:
+    """MyIPFSClass.GetParameters(hash, double[] arr), MyIPFSClass.java:444-455:
+    arr[i] = getDouble() for i < data.length/8; at i == arr.length Java throws
+    ArrayIndexOutOfBoundsException after the in-range stores (IndexError here)."""
+    n = len(data) // 8
+    m = min(n, len(arr))
+    arr[:m] = np.frombuffer(bytes(data[:8 * m]), dtype=">f8").astype(np.float64)
+    if n > len(arr):
+        raise IndexError("ArrayIndexOutOfBoundsException (MyIPFSClass.java:451)")
+
+
+def gradient_buff_len(model_size: int, n_partitions: int) -> int:
+    """new double[(int)_MODEL_SIZE/_PARTITIONS + 2], Updater.java:162."""
+    return int(np.int32(np.int64(model_size).astype(np.int32) // np.int32(n_partitions))) + 2
+
+
 def promote_future(agg: np.ndarray, fut: np.ndarray) -> None:
     """IPLS.java:1557-1562 (Update_Client_WaitAck_List): for j < L,
     Aggregated_Gradients[p][j] = from_future[p].get(j); from_future[p].set(j, 0.0)."""

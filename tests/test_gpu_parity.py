@@ -779,3 +779,45 @@ def test_future_accumulator_and_promotion(ipls, O):
     with pytest.raises(ipls.IplsError):
         agg.PromoteFuture([P])
     agg.close()
+
+
+def test_update_indirect_gradient_buff(ipls, O):
+    """Updater.run indirect requests (Updater.java:162-187): every file goes
+    through the one reusable Gradient_Buff, so a short file folds the previous
+    file's tail and an over-long one raises after overwriting the buffer."""
+    M, P = 100003, 3
+    agg = ipls.Aggregator(M, P, max_peers=3)
+    Ls = agg.lengths
+    G = O.gradient_buff_len(M, P)
+    assert G >= max(Ls)
+    buff = np.zeros(G)
+    acc = [np.zeros(L) for L in Ls]
+
+    def step(p, vals, pinned=False, fut=False):
+        data = O.be_encode(vals)
+        if pinned:
+            pb = ipls.PinnedBuffer(len(data))
+            pb.view()[:] = np.frombuffer(data, dtype=np.uint8)
+            src = pb
+        else:
+            src = data
+        try:
+            O.get_parameters_into(buff, data)
+        except IndexError:
+            with pytest.raises(ipls.IplsError):
+                agg.UpdateIndirect(src, p)
+            return
+        agg.UpdateIndirect(src, p, from_future=fut)
+        if not fut:
+            acc[p][:] = O.reduce([buff[:Ls[p]]], Ls[p], O.START_ACCUM, acc=acc[p])
+
+    step(0, O.synth_bucket(Ls[0], 0, 1), pinned=True)     # whole partition, zero-copy source
+    step(1, O.synth_bucket(Ls[1] - 100, 1, 1))             # short: 100 stale values from the last file
+    step(2, O.synth_bucket(Ls[2], 2, 1))                   # last partition (2 shorter than G)
+    step(0, O.synth_bucket(G + 5, 0, 2))                   # too long: AIOOBE, buffer overwritten
+    step(0, O.synth_bucket(10, 0, 3))                      # 10 new values + the long file's tail
+    step(1, O.synth_bucket(Ls[1], 1, 4), pinned=True)
+    step(2, np.zeros(0))                                   # empty file: all stale
+    for p in range(P):
+        assert_bits_equal(agg.read(p), acc[p], f"AGG[{p}]")
+    agg.close()
