@@ -149,6 +149,22 @@ int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t
  * owns the buffer (one per handle, like one Updater thread per peer). */
 int ipls_agg_update_indirect(ipls_agg *h, int p, int target, const void *bytes, int64_t n_bytes);
 
+/* Download_Scheduler.download_gradients, a bucket of ANOTHER aggregator of
+ * partition p (Download_Scheduler.java:245-268): kept per (p, aggregator) in
+ * Other_Replica_Gradients -- the first download becomes the stored array
+ * (its own length n, -0.0 kept), later ones fold into it for j < n.  A later
+ * download longer than the stored array returns IPLS_E_RANGE, nothing folded. */
+int ipls_agg_other_replica(ipls_agg *h, int p, int32_t aggregator, const void *src, int64_t n,
+                           int src_kind);
+
+/* Collect_Replicas (IPLS.java:1217-1241): REP[p][j] = REP[p][j] + Other[(p,a)][j]
+ * for every stored (p, a), in ascending (p, a) order (the reference iterates a
+ * HashMap; this is the canonical order), then clears the store.
+ * participants (nullable, P ints) receives the per-partition download counts
+ * (PeerData.Participants).  Returns the number of stored arrays folded, or
+ * IPLS_E_RANGE (nothing folded) if one is longer than its partition. */
+int ipls_agg_collect_replicas(ipls_agg *h, int32_t *participants);
+
 /* Batched fixed-order fold, ONE kernel launch for n_parts partitions:
  *   for q in [0,n_parts): target[p_first+q] = fold(start_mode; bufs[q*k + 0..k-1])
  * bufs are device pointers (DEV_F64 or DEV_BE), each at least L_p long.

@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -84,6 +85,14 @@ struct ipls_agg {
   unsigned long long* d_sum = nullptr;
   double* d_cnt = nullptr;   // per-partition count slots of a fused round (P doubles)
   unsigned long long* d_gbuf = nullptr;   // Updater.run's Gradient_Buff (Updater.java:162), lazily
+  // PeerData.Other_Replica_Gradients / _Received, keyed (partition, aggregator);
+  // std::map order = the canonical (ascending) Collect_Replicas order
+  struct OtherRep {
+    unsigned long long* d = nullptr;
+    int64_t n = 0;
+    int32_t received = 0;
+  };
+  std::map<std::pair<int, int32_t>, OtherRep> other;
   int64_t gbuf_len = 0;
 };
 
@@ -571,6 +580,8 @@ int ipls_agg_close(ipls_agg* h) {
   if (h->d_sum) hipFree(h->d_sum);
   if (h->d_cnt) hipFree(h->d_cnt);
   if (h->d_gbuf) hipFree(h->d_gbuf);
+  for (auto& kv : h->other)
+    if (kv.second.d) hipFree(kv.second.d);
   if (h->arena) hipFree(h->arena);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
@@ -967,6 +978,79 @@ static int flat_to_device(ipls_agg* h, const void* flat, int64_t n, int kind, co
     default:
       return fail(h, IPLS_E_INVAL, "bad flat kind %d", kind);
   }
+}
+
+int ipls_agg_other_replica(ipls_agg* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (n < 0 || (n > 0 && !src)) return fail(h, IPLS_E_INVAL, "bad bucket");
+  if ((src_kind == IPLS_DEV_F64 || src_kind == IPLS_DEV_BE) && ((uintptr_t)src & 7))
+    return fail(h, IPLS_E_INVAL, "device bucket not 8-byte aligned");
+  HIP_TRY(h, hipSetDevice(h->device));
+  auto key = std::make_pair(p, aggregator);
+  auto it = h->other.find(key);
+  const bool first = it == h->other.end();
+  // Download_Scheduler.java:254-260: `for j < gradients.length: Other[j] += g[j]`
+  // -- a longer download overruns the stored array (rejected before folding).
+  if (!first && n > it->second.n)
+    return fail(h, IPLS_E_RANGE, "replica download of %lld doubles > stored %lld "
+                "(ArrayIndexOutOfBoundsException, Download_Scheduler.java:257)", (long long)n,
+                (long long)it->second.n);
+  const unsigned long long* d;
+  bool be;
+  if (int rc = flat_to_device(h, src, n, src_kind, &d, &be)) return rc;
+  unsigned long long* dst;
+  if (first) {   // Other.put(key, GetParameters(Hash)): a new array of the file's length (:263)
+    HIP_TRY(h, hipMalloc(&dst, (size_t)std::max<int64_t>(n, 1) * 8));
+    h->other[key] = ipls_agg::OtherRep{dst, n, 1};
+  } else {
+    dst = it->second.d;
+    it->second.received += 1;   // Other_Replica_Gradients_Received + 1 (:260)
+  }
+  if (n > 0) {
+    const dim3 g(std::min<unsigned>(blocks_for(n, kBlock), 4096));
+#define FN(B, F) hipLaunchKernelGGL((k_fold_n<B, F>), g, dim3(kBlock), 0, h->stream, dst, d, n)
+    if (be) { if (first) FN(true, true); else FN(true, false); }
+    else { if (first) FN(false, true); else FN(false, false); }
+#undef FN
+    HIP_TRY(h, hipGetLastError());
+  }
+  if (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE) HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
+}
+
+int ipls_agg_collect_replicas(ipls_agg* h, int32_t* participants) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  HIP_TRY(h, hipSetDevice(h->device));
+  // REP[p] is a double[L_p]: a longer stored array overruns it (IPLS.java:1225).
+  for (auto& kv : h->other)
+    if (kv.second.n > h->len[kv.first.first])
+      return fail(h, IPLS_E_RANGE, "stored replica of %lld doubles > partition %d length %lld "
+                  "(ArrayIndexOutOfBoundsException, IPLS.java:1225)", (long long)kv.second.n, kv.first.first,
+                  (long long)h->len[kv.first.first]);
+  if (participants)
+    for (int q = 0; q < h->P; ++q) participants[q] = 0;
+  int folded = 0;
+  for (auto& kv : h->other) {   // IPLS.java:1222-1234: REP[p][j] = REP[p][j] + Other[j], j < Other.length
+    const int p = kv.first.first;
+    const int64_t n = kv.second.n;
+    if (participants) participants[p] += kv.second.received;   // PeerData.Participants (:1228-1233)
+    if (n > 0) {
+      if (int rc = materialize(h, p, IPLS_TGT_REP)) return rc;
+      hipLaunchKernelGGL((k_fold_n<false, false>), dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)),
+                         dim3(kBlock), 0, h->stream, (unsigned long long*)(h->arena + h->rep_off[p]),
+                         kv.second.d, n);
+      HIP_TRY(h, hipGetLastError());
+    }
+    ++folded;
+  }
+  // Other_Replica_Gradients = new HashMap<>() (:1237-1238)
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  for (auto& kv : h->other) hipFree(kv.second.d);
+  h->other.clear();
+  return folded;
 }
 
 int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {

@@ -297,6 +297,20 @@ __global__ __launch_bounds__(BS) void k_reduce(
   }
 }
 
+// Elementwise fold of one bucket of n doubles into dst (off the hot path:
+// Download_Scheduler's Other_Replica_Gradients and their Collect_Replicas fold).
+//   FIRST: dst[i] = decode(src[i])          (GetParameters(Hash): a new array)
+//   else : dst[i] = dst[i] + decode(src[i])
+template <bool BE_IN, bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_fold_n(unsigned long long* __restrict__ dst,
+                                                   const unsigned long long* __restrict__ src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double x = decode1<BE_IN>(ld8(src + i));
+    const double y = FIRST ? x : __builtin_bit_cast(double, ld8(dst + i)) + x;
+    st8(dst + i, __builtin_bit_cast(unsigned long long, y));
+  }
+}
+
 // Count slot of a fused round, per partition (one lane each): the same fold
 // k_reduce<..., FIN> applies to element L-1, i.e. W[L-1] =
 // (init[L-1] | +0.0) + b_0[L-1] + ... + b_{k-1}[L-1] + (REP[L-1] | +0.0).

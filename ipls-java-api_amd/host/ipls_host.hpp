@@ -211,12 +211,20 @@ class IPLS {
           h_.get());
   }
 
-  // Collect_Replicas (IPLS.java:1217-1241): fold a missing replica's
-  // downloaded buckets into Replicas_Gradients.
-  void Collect_Replicas(int Partition, const std::vector<double>& Other_Replica_Gradient) {
-    check(ipls_agg_accumulate(h_.get(), Partition, IPLS_TGT_REP, Other_Replica_Gradient.data(),
-                              (int64_t)Other_Replica_Gradient.size(), IPLS_HOST_F64),
+  // Download_Scheduler.download_gradients (:245-268): a bucket another
+  // aggregator of Partition will fold, kept in Other_Replica_Gradients.
+  void Other_Replica_Gradients(int Partition, int32_t Aggregator, const std::vector<double>& gradients) {
+    check(ipls_agg_other_replica(h_.get(), Partition, Aggregator, gradients.data(), (int64_t)gradients.size(),
+                                 IPLS_HOST_F64),
           h_.get());
+  }
+
+  // Collect_Replicas (IPLS.java:1217-1241): fold every stored array into
+  // Replicas_Gradients and clear the store; returns PeerData.Participants.
+  std::vector<int32_t> Collect_Replicas() {
+    std::vector<int32_t> participants((size_t)cfg_._PARTITIONS);
+    check(ipls_agg_collect_replicas(h_.get(), participants.data()), h_.get());
+    return participants;
   }
 
   // AggregatePartition (IPLS.java:1248-1274); returns the update_file bytes

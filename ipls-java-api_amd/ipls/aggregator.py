@@ -12,7 +12,10 @@ IPLS.InitializeWeights(List) 1880      ``InitializeWeights(model)``
 IPLS.OrganizeGradients 1018            ``OrganizeGradients(gradients)``
 IPLS.UpdateGradient 1703 (1737-1743)   ``UpdateGradient(gradients, auth_list)``
 Updater._Update 31 (from_clients)      ``Update(gradient, partition, from_clients)``
-IPLS.Collect_Replicas 1217             ``Collect_Replicas(partition, buckets)``
+Download_Scheduler 245-268             ``OtherReplicaGradients(p, aggregator, g)``
+IPLS.Collect_Replicas 1217             ``Collect_Replicas()``
+IPLS.Update_Client_WaitAck_List 1556   ``PromoteFuture(auth_list)``
+Updater.run indirect 176-187           ``UpdateIndirect(file_bytes, partition)``
 Decentralized_Storage_Receiver 239     ``Merge(partition, buckets)``
 IPLS.AggregatePartition 1248           ``AggregatePartition(partition)``
 Download_Scheduler.cache_partition 752 ``cache_partition(partition, data)``
@@ -254,10 +257,21 @@ class Aggregator:
         """Aggregated = 0.25*Weights before the async publish (Updater.java:197-199)."""
         self._chk(self._lib.ipls_agg_scale(self._h, partition, N.TGT_AGG, N.TGT_WEIGHTS, 0.25))
 
-    def Collect_Replicas(self, partition: int, buckets):
-        """IPLS.java:1217-1241: fold locally downloaded replica buckets into REP."""
-        for b in buckets:
-            self.Update(b, partition, from_clients=False)
+    def OtherReplicaGradients(self, partition: int, aggregator: int, gradients):
+        """Download_Scheduler.download_gradients (Download_Scheduler.java:245-268):
+        a bucket that another aggregator of ``partition`` (an integer id) will
+        also fold.  The first one becomes Other_Replica_Gradients[(p, a)], later
+        ones fold into it."""
+        ptr, n, kind, keep = _operand(gradients)
+        self._chk(self._lib.ipls_agg_other_replica(self._h, partition, aggregator, ptr, n, kind))
+
+    def Collect_Replicas(self):
+        """IPLS.java:1217-1241: fold every stored Other_Replica_Gradients array
+        into REP (ascending (partition, aggregator) order) and clear the store.
+        Returns (arrays folded, per-partition download counts = Participants)."""
+        part = (ctypes.c_int32 * max(1, self.n_partitions))()
+        k = self._chk(self._lib.ipls_agg_collect_replicas(self._h, part))
+        return k, list(part)[:self.n_partitions]
 
     def reduce_batch(self, p_first: int, buckets, *, start_mode: int = N.START_ZERO,
                      target: int = N.TGT_AGG, big_endian: bool = False):

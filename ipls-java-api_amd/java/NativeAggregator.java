@@ -65,6 +65,19 @@ public final class NativeAggregator implements AutoCloseable {
         if (gradient != null) accumulate(handle, p, TGT_FUTURE, gradient);
     }
 
+    /** Download_Scheduler.download_gradients (:254-266): another aggregator's
+     *  bucket for partition p, kept per (p, aggregator) until collectReplicas(). */
+    public void otherReplica(int p, int aggregator, ByteBuffer catBytes) {
+        otherReplicaDirect(handle, p, aggregator, catBytes, catBytes.remaining() / 8);
+    }
+
+    /** IPLS.Collect_Replicas (IPLS.java:1217-1241); returns Participants per partition. */
+    public int[] collectReplicas(int partitions) {
+        int[] participants = new int[partitions];
+        collectReplicas(handle, participants);
+        return participants;
+    }
+
     /** Tail of Update_Client_WaitAck_List (IPLS.java:1556-1562). */
     public void promoteFuture(int[] authList) { promoteFuture(handle, authList); }
 
@@ -123,6 +136,8 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void getPartitions(long h, double[] out);
     private static native void aggregateRound(long h, int pFirst, int nParts, double[] avgOut);
     private static native void promoteFuture(long h, int[] parts);
+    private static native void otherReplicaDirect(long h, int p, int aggregator, ByteBuffer buf, long n);
+    private static native void collectReplicas(long h, int[] participants);
     private static native void getPartitionsWire(long h, ByteBuffer direct);
     private static native ByteBuffer hostAllocDirect(int bytes);
 }

@@ -162,6 +162,20 @@ JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c
     CHECK(rc, H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_otherReplicaDirect(JNIEnv *env, jclass c, jlong h, jint p, jint a,
+                                                                  jobject buf, jlong n) {
+    (void)c;
+    CHECK(ipls_agg_other_replica(H(h), p, a, (*env)->GetDirectBufferAddress(env, buf), n, IPLS_HOST_BE), H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass c, jlong h, jintArray out) {
+    (void)c;
+    jint *ps = (*env)->GetIntArrayElements(env, out, NULL);
+    int rc = ipls_agg_collect_replicas(H(h), (int32_t *)ps);
+    (*env)->ReleaseIntArrayElements(env, out, ps, 0);
+    CHECK(rc, H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf) {
     (void)c;
     jlong cap = (*env)->GetDirectBufferCapacity(env, buf);

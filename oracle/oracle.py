@@ -126,6 +126,36 @@ def gradient_buff_len(model_size: int, n_partitions: int) -> int:
     return int(np.int32(np.int64(model_size).astype(np.int32) // np.int32(n_partitions))) + 2
 
 
+def other_replica_add(store: dict, partition: int, aggregator, g: np.ndarray) -> None:
+    """Download_Scheduler.java:254-266: the first download of (p, a) becomes the
+    stored array (GetParameters(Hash) -> new double[n]); later ones fold into it
+    for j < len(g) (IndexError where Java overruns the stored array)."""
+    key = (partition, aggregator)
+    if key not in store:
+        store[key] = [np.array(g, dtype=np.float64, copy=True), 1]
+        return
+    arr = store[key][0]
+    if len(g) > len(arr):
+        raise IndexError("ArrayIndexOutOfBoundsException (Download_Scheduler.java:257)")
+    arr[:len(g)] = arr[:len(g)] + g
+    store[key][1] += 1
+
+
+def collect_replicas(rep: list, store: dict, participants: list | None = None) -> int:
+    """IPLS.Collect_Replicas, IPLS.java:1217-1241, in ascending (p, a) key order:
+    REP[p][j] = REP[p][j] + Other[(p, a)][j] for j < len(Other); store cleared."""
+    n = 0
+    for key in sorted(store):
+        p = key[0]
+        arr, received = store[key]
+        rep[p][:len(arr)] = rep[p][:len(arr)] + arr
+        if participants is not None:
+            participants[p] += received
+        n += 1
+    store.clear()
+    return n
+
+
 def promote_future(agg: np.ndarray, fut: np.ndarray) -> None:
     """IPLS.java:1557-1562 (Update_Client_WaitAck_List): for j < L,
     Aggregated_Gradients[p][j] = from_future[p].get(j); from_future[p].set(j, 0.0)."""

@@ -821,3 +821,34 @@ def test_update_indirect_gradient_buff(ipls, O):
     for p in range(P):
         assert_bits_equal(agg.read(p), acc[p], f"AGG[{p}]")
     agg.close()
+
+
+def test_other_replica_gradients_and_collect(ipls, O):
+    """Download_Scheduler.java:245-268 + IPLS.Collect_Replicas (:1217-1241):
+    per-(partition, aggregator) arrays, FIRST-started (so -0.0 survives), folded
+    into REP in ascending key order after what REP already holds."""
+    M, P = 80001, 2
+    agg = ipls.Aggregator(M, P, max_peers=4)
+    Ls = agg.lengths
+    rep = [np.zeros(L) for L in Ls]
+    store = {}
+    own_rep = O.synth_bucket(Ls[0], 0, 50)
+    agg.Update(own_rep, 0, from_clients=False)                 # a replica that did answer
+    rep[0] = O.reduce([own_rep], Ls[0])
+    negz = O.synth_bucket(Ls[0], 0, 60)
+    negz[::7] = -0.0
+    downloads = [(0, 7, negz), (0, 3, O.synth_bucket(Ls[0], 0, 61)), (0, 7, O.synth_bucket(Ls[0], 0, 62)),
+                 (1, 5, O.synth_bucket(Ls[1], 1, 63)), (1, 5, O.synth_bucket(Ls[1] - 1000, 1, 64))]
+    for i, (p, a, g) in enumerate(downloads):
+        O.other_replica_add(store, p, a, g)
+        agg.OtherReplicaGradients(p, a, O.be_encode(g) if i % 2 else g)   # BE file bytes or doubles
+    with pytest.raises(ipls.IplsError):                         # longer than the stored array
+        agg.OtherReplicaGradients(1, 5, O.synth_bucket(Ls[1] + 3, 1, 65))
+    parts_ref = [0] * P
+    n_ref = O.collect_replicas(rep, store, parts_ref)
+    n, parts = agg.Collect_Replicas()
+    assert (n, parts) == (n_ref, parts_ref) == (3, [3, 2])
+    for p in range(P):
+        assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}]")
+    assert agg.Collect_Replicas() == (0, [0, 0])               # the store was cleared
+    agg.close()
