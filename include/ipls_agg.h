@@ -233,7 +233,10 @@ int ipls_agg_aggregate_round(ipls_agg *h, int p_first, int n_parts,
                              void *avg_out, int avg_kind);
 
 /* Download_Scheduler.cache_partition (Download_Scheduler.java:752-792):
- * Weight_Address[p] = GetParameters(hash) -- the downloaded updated partition. */
+ * Weight_Address[p] = GetParameters(hash) -- the downloaded updated partition
+ * (n doubles, F64/BE host or device kinds).  src_kind HOST_FRAME (n = frame
+ * bytes) is the pid-4 ACK of ThreadReceiver (IPLS.java:491-498): the frame's
+ * first L_p payload doubles become Weight_Address[p]. */
 int ipls_agg_set_weights(ipls_agg *h, int p, const void *src, int64_t n, int src_kind);
 
 /* GetPartitions (IPLS.java:1140-1174): Weights = Weight_Address, then the

@@ -927,6 +927,27 @@ int ipls_agg_set_weights(ipls_agg* h, int p, const void* src, int64_t n, int src
   std::lock_guard<std::mutex> lk(h->mu);
   if (int rc = check_part(h, p)) return rc;
   const int64_t L = h->len[p];
+  if (src_kind == IPLS_HOST_FRAME) {
+    // ThreadReceiver pid 4 (IPLS.java:491-498): Weight_Address[p][i] =
+    // GET_GRADIENTS(frame) payload[i] for i < L_p.
+    int16_t pid;
+    int32_t a, b;
+    int64_t poff, ooff;
+    const int64_t nd = ipls_frame_parse((const uint8_t*)src, n, &pid, &a, &b, &poff, &ooff);
+    if (nd < 0) return fail(h, IPLS_E_FORMAT, "malformed frame (BufferUnderflowException)");
+    if (nd == 0) return fail(h, IPLS_E_INVAL, "frame without gradients (NullPointerException, IPLS.java:498)");
+    if (nd < L)
+      return fail(h, IPLS_E_RANGE, "frame payload of %lld doubles < length %lld (IPLS.java:498)", (long long)nd,
+                  (long long)L);
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+    if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
+    hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
+                       h->stream, (const unsigned long long*)h->d_scratch,
+                       (unsigned long long*)(h->arena + h->w_off[p]), L);
+    HIP_TRY(h, hipGetLastError());
+    return IPLS_OK;
+  }
   // GetParameters(hash, arr) writes data.length/8 values (MyIPFSClass.java:449-452);
   // more than arr.length -> ArrayIndexOutOfBoundsException.
   if (n > L) return fail(h, IPLS_E_RANGE, "downloaded partition of %lld doubles > length %lld", (long long)n, (long long)L);

@@ -358,8 +358,13 @@ class Aggregator:
         self._chk(self._lib.ipls_agg_finalize(self._h, partition, sp, sk, ap))
         return s, a
 
-    def cache_partition(self, partition: int, data):
-        """Download_Scheduler.cache_partition: Weight_Address[p] = GetParameters(hash)."""
+    def cache_partition(self, partition: int, data, *, frame: bool = False):
+        """Download_Scheduler.cache_partition: Weight_Address[p] = GetParameters(hash).
+        ``frame=True``: the pid-4 ACK frame of ThreadReceiver (IPLS.java:491-498)."""
+        if frame:
+            a = np.frombuffer(bytes(data), dtype=np.uint8)
+            self._chk(self._lib.ipls_agg_set_weights(self._h, partition, a.ctypes.data, a.size, N.HOST_FRAME))
+            return
         ptr, n, kind, keep = _operand(data)
         self._chk(self._lib.ipls_agg_set_weights(self._h, partition, ptr, n, kind))
 

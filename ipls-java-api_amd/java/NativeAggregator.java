@@ -98,6 +98,9 @@ public final class NativeAggregator implements AutoCloseable {
         setWeightsDirect(handle, p, beDoubles, beDoubles.remaining() / 8);
     }
 
+    /** ThreadReceiver pid 4 (IPLS.java:491-498): the ACK frame's payload becomes Weight_Address[p]. */
+    public void cachePartitionFrame(int p, byte[] frame) { setWeightsFrame(handle, p, frame); }
+
     /** GetPartitions (IPLS.java:1140-1174). */
     public double[] getPartitions(int modelSize) {
         double[] out = new double[modelSize];
@@ -133,6 +136,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, long nBytes);
     private static native void finalizePartition(long h, int p, byte[] sumOut);
     private static native void setWeightsDirect(long h, int p, ByteBuffer buf, long n);
+    private static native void setWeightsFrame(long h, int p, byte[] frame);
     private static native void getPartitions(long h, double[] out);
     private static native void aggregateRound(long h, int pFirst, int nParts, double[] avgOut);
     private static native void promoteFuture(long h, int[] parts);

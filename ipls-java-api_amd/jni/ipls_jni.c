@@ -135,6 +135,16 @@ JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclas
     CHECK(ipls_agg_set_weights(H(h), p, (*env)->GetDirectBufferAddress(env, buf), n, IPLS_HOST_BE), H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass c, jlong h, jint p,
+                                                               jbyteArray frame) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, frame);
+    void *src = (*env)->GetPrimitiveArrayCritical(env, frame, NULL);
+    int rc = ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_FRAME);
+    (*env)->ReleasePrimitiveArrayCritical(env, frame, src, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c, jlong h, jdoubleArray out) {
     (void)c;
     jsize n = (*env)->GetArrayLength(env, out);

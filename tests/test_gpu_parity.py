@@ -852,3 +852,20 @@ def test_other_replica_gradients_and_collect(ipls, O):
         assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}]")
     assert agg.Collect_Replicas() == (0, [0, 0])               # the store was cleared
     agg.close()
+
+
+def test_ack_frame_sets_weight_address(ipls, O):
+    """ThreadReceiver pid 4 (IPLS.java:491-498): the ACK frame's payload becomes
+    Weight_Address[p]; GetPartitions then divides it."""
+    M, P = 30001, 2
+    agg = ipls.Aggregator(M, P)
+    Ls = agg.lengths
+    ws = [O.synth_bucket(Ls[p], p, 3) for p in range(P)]
+    for p in range(P):
+        fr = O.frame_encode(np.concatenate([ws[p], [7.0, 8.0]]), p, 12, 4, b"QmServer")   # longer payload is fine
+        agg.cache_partition(p, fr, frame=True)
+        assert_bits_equal(agg.read(p, ipls.TGT_WADDR), ws[p], f"WADDR[{p}]")
+    assert_bits_equal(agg.GetPartitions(), O.get_partitions(ws), "model")
+    with pytest.raises(ipls.IplsError):
+        agg.cache_partition(0, O.frame_encode(ws[0][:-1], 0, 12, 4, b"Qm"), frame=True)    # short payload
+    agg.close()
