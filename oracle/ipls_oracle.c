@@ -209,6 +209,23 @@ uint64_t ipls_oracle_synth_sum_checksum(uint64_t seed, int32_t p, int32_t k, int
     return s;
 }
 
+/* Checksum of the averaged output of the same fold (GetPartitions divide,
+ * IPLS.java:1159-1174) over i < L-1, element index i: cnt = S[L-1] (the fold
+ * of k count slots), out = cnt == 0 ? S[i] : S[i] / (secure ? 1e12*cnt : cnt). */
+uint64_t ipls_oracle_synth_avg_checksum(uint64_t seed, int32_t p, int32_t k, int64_t L, int32_t secure) {
+    double cnt = 0.0;
+    for (int32_t j = 0; j < k; j++) cnt = cnt + 1.0;
+    const double den = secure ? 1e12 * cnt : cnt;
+    uint64_t s = 0;
+#pragma omp parallel for reduction(+ : s) schedule(static)
+    for (int64_t i = 0; i < L - 1; i++) {
+        double acc = 0.0;
+        for (int32_t j = 0; j < k; j++) acc = acc + ipls_oracle_synth_value(seed, p, j, i);
+        s += checksum_term(cnt == 0.0 ? acc : acc / den, i);
+    }
+    return s;
+}
+
 /* Updater.run + _Update for k indirect-mode buckets (Updater.java:162-187,
  * 115-117): decode into the reused buffer, then fold. */
 void ipls_oracle_updater_loop(double *agg, const uint8_t *const *be_bufs, int k,

@@ -104,6 +104,7 @@ uint64_t ipls_oracle_checksum(const double *x, int64_t n);
  * memory).  Multi-threaded over elements (OpenMP) -- the per-element fold
  * order is unchanged, so this is still the reference's arithmetic. */
 uint64_t ipls_oracle_synth_sum_checksum(uint64_t seed, int32_t p, int32_t k, int64_t L);
+uint64_t ipls_oracle_synth_avg_checksum(uint64_t seed, int32_t p, int32_t k, int64_t L, int32_t secure);
 
 /* CPU baseline: the reference's Updater loop over k BE byte buckets,
  * 1 thread: decode each bucket into a reused double[] (Updater.java:162,177

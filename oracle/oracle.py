@@ -370,6 +370,8 @@ def c_oracle():
         lib.ipls_oracle_checksum.argtypes = [D, i64]
         lib.ipls_oracle_synth_sum_checksum.restype = u64
         lib.ipls_oracle_synth_sum_checksum.argtypes = [u64, i32, i32, i64]
+        lib.ipls_oracle_synth_avg_checksum.restype = u64
+        lib.ipls_oracle_synth_avg_checksum.argtypes = [u64, i32, i32, i64, i32]
         lib.ipls_oracle_updater_loop.argtypes = [D, ctypes.POINTER(U8), ctypes.c_int, i64, D]
         lib.ipls_oracle_updater_loop_parts.restype = ctypes.c_int
         lib.ipls_oracle_updater_loop_parts.argtypes = [ctypes.c_int, ctypes.POINTER(U8), ctypes.c_int, i64, D]
@@ -398,6 +400,10 @@ def c_synth_bucket(L: int, p: int, k: int, seed: int = SEED) -> np.ndarray:
 
 def c_synth_sum_checksum(L: int, p: int, k: int, seed: int = SEED) -> int:
     return int(c_oracle().ipls_oracle_synth_sum_checksum(seed, p, k, L))
+
+
+def c_synth_avg_checksum(L: int, p: int, k: int, secure: bool = False, seed: int = SEED) -> int:
+    return int(c_oracle().ipls_oracle_synth_avg_checksum(seed, p, k, L, int(secure)))
 
 
 def c_checksum(x) -> int:

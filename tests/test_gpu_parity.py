@@ -869,3 +869,39 @@ def test_ack_frame_sets_weight_address(ipls, O):
     with pytest.raises(ipls.IplsError):
         agg.cache_partition(0, O.frame_encode(ws[0][:-1], 0, 12, 4, b"Qm"), frame=True)    # short payload
     agg.close()
+
+
+def _free_hbm():
+    free, _ = torch.cuda.mem_get_info()
+    return free
+
+
+@pytest.mark.parametrize("P,L,K", [(1, 2**31 - 3, 2), (3, 2**30 + 1, 2)])
+def test_maximum_sizes(ipls, O, P, L, K):
+    """Java's largest double[] (HotSpot: Integer.MAX_VALUE - 2) as one
+    partition, and flat model offsets past 2^31 elements: byte offsets past
+    2^34, through the fold, the fused round and the checksums."""
+    need = 8 * L * (P * K + 4 * P + P) + (1 << 30)      # buckets + AGG/REP/W/FUT + averages
+    if _free_hbm() < need:
+        pytest.skip(f"needs {need / 2**30:.0f} GiB of free HBM")
+    stride = L + (L & 1)                                  # keep every bucket 16-B aligned
+    arena = torch.empty(P * K * stride, dtype=torch.float64, device="cuda")
+    base = int(arena.data_ptr())
+    rows = [[ipls.DeviceBuffer(base + 8 * (p * K + k) * stride, L) for k in range(K)] for p in range(P)]
+    for p in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[p][k], p, k, O.SEED)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    ref = [O.c_synth_sum_checksum(L, p, K) for p in range(P)]
+    assert [agg.checksum(p) for p in range(P)] == ref
+    agg.reset(ipls.ALL_PARTITIONS)
+    avg = torch.empty(P * (L - 1), dtype=torch.float64, device="cuda")
+    agg.aggregate_round(0, rows, out=ipls.DeviceBuffer.from_tensor(avg))
+    assert [agg.checksum(p, ipls.TGT_WEIGHTS) for p in range(P)] == ref
+    for p in range(P):
+        part = ipls.DeviceBuffer(int(avg.data_ptr()) + 8 * p * (L - 1), L - 1)
+        assert ipls.checksum_dev(part) == O.c_synth_avg_checksum(L, p, K), f"avg[{p}]"
+    agg.close()
+    del arena, avg
+    torch.cuda.empty_cache()

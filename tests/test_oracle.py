@@ -182,3 +182,11 @@ def test_promote_future_oracle():
     O.promote_future(agg, fut)
     assert agg.view(np.uint64).tolist() == ref.view(np.uint64).tolist()
     assert fut.view(np.uint64).tolist() == [0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("secure", [False, True])
+def test_c_synth_avg_checksum_matches_numpy(secure):
+    """The large-size GPU tests check averages through this C checksum."""
+    L, p, k = 5003, 2, 3
+    S = O.reduce([O.synth_bucket(L, p, j) for j in range(k)], L)
+    assert O.c_synth_avg_checksum(L, p, k, secure) == O.checksum(O.divide(S, secure))
