@@ -133,12 +133,24 @@ def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dic
             s, _ = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True)
         dt = time.perf_counter() - t0
         out[name] = round(reps * (K + 1) * L * 8 / dt / 1e9, 2)
+    # per arrival, asynchronous: each fold is queued (ipls_agg_accumulate_async)
+    # and the round waits once, at AggregatePartition
+    for pb in pinned:                                    # warm
+        agg.UpdateAsync(pb, 0)
+    agg.AggregatePartition(0, with_sum=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for pb in pinned:
+            agg.UpdateAsync(pb, 0)
+        s, _ = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True)
+    out["pinned_async"] = round(reps * (K + 1) * L * 8 / (time.perf_counter() - t0) / 1e9, 2)
     agg.close()
     for pb in pinned:
         pb.close()
     return {"unit": "GB/s", **out,
             "sample": f"{reps} rounds x 1 partition x {K} peers x {L} doubles: each BE bucket from host memory "
-                      f"(pinned: per-arrival zero-copy fold; pinned_batched: one launch over all K; pageable: "
+                      f"(pinned: per-arrival zero-copy fold; pinned_async: the same, queued without waiting; "
+                      f"pinned_batched: one launch over all K; pageable: "
                       f"staged H2D) + finalize + D2H of the BE sum, algorithmic bytes (K+1)*L*8 per round",
             "pcie_ceiling": "~56 GB/s per direction measured (tools/h2d_bench.hip, profiles/r01/h2d_bench.txt)"}
 

@@ -138,6 +138,19 @@ int ipls_agg_update_gradient(ipls_agg *h, const void *flat, int64_t n, int src_k
 int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t n,
                         int src_kind);
 
+/* Asynchronous form of ipls_agg_accumulate for a bucket in pinned host memory
+ * (ipls_host_alloc, 16-B aligned, HOST_F64/HOST_BE): the fold is queued to
+ * read the bucket over PCIe and the call returns at once with *ticket.  The
+ * caller keeps the buffer untouched until ipls_agg_wait(h, ticket) -- or any
+ * synchronising call -- returns, so the next `ipfs cat` can fill another
+ * buffer meanwhile.  Other sources run synchronously (ticket already done).
+ * Folds still apply in call order. */
+int ipls_agg_accumulate_async(ipls_agg *h, int p, int target, const void *src, int64_t n,
+                              int src_kind, uint64_t *ticket);
+
+/* Wait until fold `ticket` (and every fold queued before it) has finished. */
+int ipls_agg_wait(ipls_agg *h, uint64_t ticket);
+
 /* Updater.run's indirect request (Updater.java:176-187): the queue item holds
  * only a hash, so the bucket is `ipfs cat` bytes read into the Updater's one
  * reusable Gradient_Buff of (int)M/P + 2 doubles (Updater.java:162, zeroed

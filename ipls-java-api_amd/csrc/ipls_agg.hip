@@ -80,6 +80,10 @@ struct ipls_agg {
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   hipEvent_t copy_ev = nullptr;
+  // asynchronous folds of pinned host buckets: ticket t completes at fold_ev[t % kTickets]
+  static constexpr int kTickets = 64;
+  hipEvent_t fold_ev[kTickets] = {};
+  uint64_t ticket_next = 1, ticket_done = 0;
 
   // checksum result
   unsigned long long* d_sum = nullptr;
@@ -574,6 +578,8 @@ int ipls_agg_close(ipls_agg* h) {
     if (s.ev) hipEventDestroy(s.ev);
   }
   if (h->copy_ev) hipEventDestroy(h->copy_ev);
+  for (auto& e : h->fold_ev)
+    if (e) hipEventDestroy(e);
   for (void* d : h->d_table)
     if (d) hipFree(d);
   if (h->d_scratch) hipFree(h->d_scratch);
@@ -610,6 +616,18 @@ int ipls_agg_sync(ipls_agg* h) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   std::lock_guard<std::mutex> lk(h->mu);
   HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
+}
+
+int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (ticket >= h->ticket_next) return fail(h, IPLS_E_INVAL, "ticket %llu was never issued", (unsigned long long)ticket);
+  // a slot is only reused after its previous ticket completed, so anything
+  // older than the ring is already <= ticket_done
+  if (ticket <= h->ticket_done) return IPLS_OK;
+  HIP_TRY(h, hipEventSynchronize(h->fold_ev[ticket % ipls_agg::kTickets]));
+  h->ticket_done = ticket;
   return IPLS_OK;
 }
 
@@ -684,6 +702,38 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
   }
   const void* bl[1] = {dptr};
   return reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target);
+}
+
+int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind,
+                              uint64_t* ticket) {
+  if (!h || !ticket) return fail(h, IPLS_E_INVAL, "null argument");
+  void* alias = nullptr;
+  const bool host = src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE;
+  if (!src || !host || ((uintptr_t)src & 15) || !is_pinned_host(src, &alias) || !alias) {
+    // not a pinned host bucket: the synchronous path, already complete on return
+    int rc = ipls_agg_accumulate(h, p, target, src, n, src_kind);
+    std::lock_guard<std::mutex> lk(h->mu);
+    *ticket = h->ticket_done;
+    return rc;
+  }
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (int rc = host_decode_count(src_kind, n, h->len[p], h)) return rc;
+  HIP_TRY(h, hipSetDevice(h->device));
+  const uint64_t t = h->ticket_next;
+  hipEvent_t& ev = h->fold_ev[t % ipls_agg::kTickets];
+  if (!ev) HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  if (t > (uint64_t)ipls_agg::kTickets && t - ipls_agg::kTickets > h->ticket_done) {
+    HIP_TRY(h, hipEventSynchronize(ev));   // the slot's previous fold (and all before it) is done
+    h->ticket_done = t - ipls_agg::kTickets;
+  }
+  const void* bl[1] = {alias};   // zero copy: the kernel reads the pinned bucket over PCIe
+  if (int rc = reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target)) return rc;
+  HIP_TRY(h, hipEventRecord(ev, h->stream));
+  h->ticket_next = t + 1;
+  *ticket = t;
+  return IPLS_OK;
 }
 
 int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, int64_t n_bytes) {

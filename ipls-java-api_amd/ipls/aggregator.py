@@ -199,6 +199,23 @@ class Aggregator:
         ptr, n, kind, keep = _operand(gradient)
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
 
+    def UpdateAsync(self, gradient, partition: int, from_clients: bool = True, *, big_endian: bool = True) -> int:
+        """Updater._Update without waiting: ``gradient`` is a PinnedBuffer (the
+        `ipfs cat` bytes, big-endian unless ``big_endian=False``) that the fold
+        reads over PCIe.  Returns a ticket; keep the buffer until Wait(ticket)."""
+        if not isinstance(gradient, PinnedBuffer):
+            raise TypeError("UpdateAsync takes a PinnedBuffer (ipls_host_alloc memory)")
+        target = N.TGT_AGG if from_clients else N.TGT_REP
+        t = ctypes.c_uint64()
+        self._chk(self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr,
+                                                      gradient.nbytes // 8,
+                                                      N.HOST_BE if big_endian else N.HOST_F64, ctypes.byref(t)))
+        return t.value
+
+    def Wait(self, ticket: int):
+        """Block until the UpdateAsync fold ``ticket`` (and all before it) is done."""
+        self._chk(self._lib.ipls_agg_wait(self._h, ticket))
+
     def UpdateIndirect(self, file_bytes, partition: int, from_clients: bool = True, *,
                        from_future: bool = False):
         """Updater.run for a queue item with only a hash (Updater.java:176-187):

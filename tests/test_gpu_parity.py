@@ -905,3 +905,33 @@ def test_maximum_sizes(ipls, O, P, L, K):
     agg.close()
     del arena, avg
     torch.cuda.empty_cache()
+
+
+def test_async_pinned_arrivals(ipls, O):
+    """ipls_agg_accumulate_async: queued zero-copy folds give the same bits as
+    synchronous Updates, in call order, across more folds than the ticket ring."""
+    L, K = 70001, 80
+    bufs = []
+    vals = [O.synth_bucket(L, 4, k) for k in range(8)]
+    for k in range(8):
+        pb = ipls.PinnedBuffer(8 * L)
+        pb.view()[:] = np.frombuffer(O.be_encode(vals[k]), dtype=np.uint8)
+        bufs.append(pb)
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    ref = np.zeros(L)
+    tickets = []
+    for j in range(K):                       # 80 folds > the 64-entry ring
+        tickets.append(agg.UpdateAsync(bufs[j % 8], 0))
+        ref = O.reduce([vals[j % 8]], L, O.START_ACCUM, acc=ref)
+    assert tickets == sorted(tickets) and len(set(tickets)) == K
+    agg.Wait(tickets[3])                     # an old ticket, long overwritten in the ring
+    agg.Wait(tickets[-1])
+    assert_bits_equal(agg.read(0), ref, "async folds")
+    t = agg.UpdateAsync(bufs[0], 1, from_clients=False)
+    agg.Wait(t)
+    assert_bits_equal(agg.read(1, ipls.TGT_REP), O.reduce([vals[0]], L), "REP")
+    with pytest.raises(ipls.IplsError):
+        agg.Wait(tickets[-1] + 100)          # never issued
+    agg.close()
+    for pb in bufs:
+        pb.close()
