@@ -386,6 +386,26 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
       }
     }
   }
+  // one bucket into one partition (every per-arrival fold): pointers go as
+  // kernel arguments, no table upload
+  if (!fin && n_parts == 1 && k == 1 && bufs[0]) {
+    unsigned long long* d0 = dst_of(0);
+    const int64_t L = h->len[p_first];
+    if (d0 && !((uintptr_t)bufs[0] & 15) && !((uintptr_t)d0 & 15) && L > 0) {
+      const auto* s0 = (const unsigned long long*)bufs[0];
+      const unsigned blocks = std::max(1u, std::min<unsigned>(blocks_for((L >> 1), kBlock * 4), 4096));
+#define F1(BI, BO, ST) hipLaunchKernelGGL((k_fold1<BI, BO, ST>), dim3(blocks), dim3(kBlock), 0, h->stream, d0, s0, L)
+#define F1S(BI, BO) do { if (start == kZero) F1(BI, BO, kZero); else if (start == kFirst) F1(BI, BO, kFirst); else F1(BI, BO, kAccum); } while (0)
+      if (be_in) { if (be_out) F1S(true, true); else F1S(true, false); }
+      else { if (be_out) F1S(false, true); else F1S(false, false); }
+#undef F1S
+#undef F1
+      HIP_TRY(h, hipGetLastError());
+      if (!ext_dst)
+        if (uint8_t* f = zero_flag(h, p_first, target)) *f = 0;
+      return IPLS_OK;
+    }
+  }
   bool aligned16 = true;
   int64_t maxL = 0;
   for (int q = 0; q < n_parts; ++q) maxL = std::max(maxL, h->len[p_first + q]);

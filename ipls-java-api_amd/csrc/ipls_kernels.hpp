@@ -354,6 +354,56 @@ __global__ __launch_bounds__(kBlock) void k_reduce_scalar(
 }
 
 // ---------------------------------------------------------------------------
+// k_fold1: the single-bucket fold of one arrival (Updater._Update,
+// Updater.java:115-117), pointers passed as kernel arguments -- no table
+// upload, so a per-arrival fold is one launch and nothing else on the stream.
+//   dst[i] = start(dst[i]) + decode(src[i]),  start: ZERO +0.0 | ACCUM dst | FIRST none
+// 16-B aligned src/dst; R pairs per lane in flight (zero-copy sources are
+// read over PCIe, where more outstanding requests per lane pay).
+// ---------------------------------------------------------------------------
+template <bool BE_IN, bool BE_OUT, int START, int R = 4>
+__global__ __launch_bounds__(kBlock) void k_fold1(unsigned long long* __restrict__ dst,
+                                                  const unsigned long long* __restrict__ src, int64_t L) {
+  const int64_t n2 = L >> 1;   // whole pairs
+  const int64_t stride = (int64_t)gridDim.x * kBlock * R;
+  auto fold = [&](const u2& v, const u2& t) -> u2 {
+    const d2 x = decode2<BE_IN>(v);
+    if constexpr (START == kFirst) return encode2<BE_OUT>(x);
+    d2 a = (START == kZero) ? d2{0.0, 0.0} : decode2<BE_OUT>(t);
+    a.x = a.x + x.x;
+    a.y = a.y + x.y;
+    return encode2<BE_OUT>(a);
+  };
+  int64_t b = (int64_t)blockIdx.x * kBlock * R + threadIdx.x;
+  for (; b + (int64_t)(R - 1) * kBlock < n2; b += stride) {   // all R pairs in range: loads first
+    u2 v[R], t[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = ld16<true>(src + 2 * (b + r * kBlock));
+    if constexpr (START == kAccum) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) t[r] = ld16<false>(dst + 2 * (b + r * kBlock));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) __builtin_nontemporal_store(fold(v[r], t[r]), (gu2)(dst + 2 * (b + r * kBlock)));
+  }
+  for (int r = 0; r < R; ++r) {   // this lane's last, partial group
+    const int64_t i2 = b + r * kBlock;
+    if (i2 < n2) {
+      const u2 t = (START == kAccum) ? ld16<false>(dst + 2 * i2) : u2{0, 0};
+      __builtin_nontemporal_store(fold(ld16<true>(src + 2 * i2), t), (gu2)(dst + 2 * i2));
+    }
+  }
+  if ((L & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd length: the last element
+    const int64_t e = L - 1;
+    const double x = decode1<BE_IN>(ld8(src + e));
+    double a;
+    if constexpr (START == kFirst) a = x;
+    else a = ((START == kZero) ? 0.0 : decode1<BE_OUT>(ld8(dst + e))) + x;
+    st8(dst + e, BE_OUT ? f64_to_be(a) : __builtin_bit_cast(unsigned long long, a));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_finalize: AggregatePartition (IPLS.java:1255-1270) over a batch.
 //   W[i] = AGG[i] + REP[i]  (REP_ZERO: AGG[i] + 0.0 without reading REP)
 //   Weight_Address is the same array as Weights (IPLS.java:1141 aliases them).
