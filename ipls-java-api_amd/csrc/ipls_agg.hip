@@ -289,14 +289,22 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   if (big_tpp * n_parts >= kBigMinBlocks) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
-    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS, FIN>), grid, dim3(kBigBS), 0,
-                       st, bufs, parts, k, (int)big_tpp, n_parts, secure, cnts);
+    if constexpr (FIN)
+      hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, kBigMap, kBigBS>), grid, dim3(kBigBS), 0, st, bufs, parts,
+                         k, (int)big_tpp, n_parts, secure, cnts);
+    else
+      hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS>), grid, dim3(kBigBS), 0,
+                         st, bufs, parts, k, (int)big_tpp, n_parts);
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
     const int64_t tpp = (maxL + tile - 1) / tile;
     const dim3 grid((unsigned)grid_blocks(kSmallMap, tpp * n_parts));
-    hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap, kBlock, FIN>), grid,
-                       dim3(kBlock), 0, st, bufs, parts, k, (int)tpp, n_parts, secure, cnts);
+    if constexpr (FIN)
+      hipLaunchKernelGGL((k_round<BE_IN, START, kSmallG, kSmallR, kSmallMap, kBlock>), grid, dim3(kBlock), 0, st,
+                         bufs, parts, k, (int)tpp, n_parts, secure, cnts);
+    else
+      hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
+                         st, bufs, parts, k, (int)tpp, n_parts);
   }
 }
 

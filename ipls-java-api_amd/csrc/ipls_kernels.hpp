@@ -31,7 +31,7 @@ enum Start : int { kAccum = 0, kZero = 1, kFirst = 2 };
 struct PartDesc {
   int64_t len;                      // L_p incl. count slot
   unsigned long long* dst;          // target: an arena accumulator or a caller buffer
-  // fused-round fields (k_reduce<..., FIN=true> only):
+  // fused-round fields (k_round only):
   const unsigned long long* init;   // START_ACCUM source (the AGG accumulator)
   const unsigned long long* rep;    // REP accumulator, or null = logically +0.0
   unsigned long long* avg;          // averaged values out (L-1 doubles), or null
@@ -136,11 +136,10 @@ __device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_pa
 //   FIN    : fused round -- dst is Weights[p] and receives fold + REP
 //            (AggregatePartition, IPLS.java:1256), and parts[q].avg (if set)
 //            the GetPartitions divide (IPLS.java:1159-1174), in the same pass
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock,
-          bool FIN = false>
-__global__ __launch_bounds__(BS) void k_reduce(
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP, int BS, bool FIN>
+__device__ __forceinline__ void reduce_tiles(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
-    int k, int tiles_per_part, int n_parts, int secure = 0, const double* __restrict__ cnts = nullptr) {
+    int k, int tiles_per_part, int n_parts, int secure, const double* __restrict__ cnts) {
   constexpr int kBlock = BS;   // lanes per workgroup (shadows the namespace default)
   constexpr int64_t kTile = (int64_t)kBlock * 2 * R;
   int q, t;
@@ -297,6 +296,23 @@ __global__ __launch_bounds__(BS) void k_reduce(
   }
 }
 
+// The batched fold (the benchmarked kernel) and the fused round are two
+// kernels over the same tile code, so profiles name them apart.
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_reduce(const unsigned long long* const* __restrict__ bufs,
+                                               const PartDesc* __restrict__ parts, int k, int tiles_per_part,
+                                               int n_parts) {
+  reduce_tiles<BE_IN, BE_OUT, START, G, R, NT, MAP, BS, false>(bufs, parts, k, tiles_per_part, n_parts, 0, nullptr);
+}
+
+template <bool BE_IN, int START, int G, int R, int MAP = 0, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_round(const unsigned long long* const* __restrict__ bufs,
+                                              const PartDesc* __restrict__ parts, int k, int tiles_per_part,
+                                              int n_parts, int secure, const double* __restrict__ cnts) {
+  reduce_tiles<BE_IN, false, START, G, R, true, MAP, BS, true>(bufs, parts, k, tiles_per_part, n_parts, secure,
+                                                               cnts);
+}
+
 // Elementwise fold of one bucket of n doubles into dst (off the hot path:
 // Download_Scheduler's Other_Replica_Gradients and their Collect_Replicas fold).
 //   FIRST: dst[i] = decode(src[i])          (GetParameters(Hash): a new array)
@@ -312,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_n(unsigned long long* __restric
 }
 
 // Count slot of a fused round, per partition (one lane each): the same fold
-// k_reduce<..., FIN> applies to element L-1, i.e. W[L-1] =
+// k_round applies to element L-1, i.e. W[L-1] =
 // (init[L-1] | +0.0) + b_0[L-1] + ... + b_{k-1}[L-1] + (REP[L-1] | +0.0).
 template <bool BE_IN, int START>
 __global__ __launch_bounds__(kBlock) void k_round_counts(const unsigned long long* const* __restrict__ bufs,
