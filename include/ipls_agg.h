@@ -71,6 +71,9 @@ extern "C" {
 #define IPLS_DEV_BE       4  /* device bytes, big-endian doubles, 8-byte aligned             */
 #define IPLS_HOST_BE_CANON 5 /* output only: BE with NaN canonicalised, DataOutputStream
                                 .writeDouble (Middleware.java:164-170)                      */
+#define IPLS_HOST_PAIR    6  /* host byte[] of a Java-serialised org.javatuples.Pair<Integer,
+                                double[]> partial update (MyIPFSClass.java:160-166, read by
+                                Download_Partial_Updates :326-338); n = byte length         */
 
 /* ---- fold start modes ---- */
 #define IPLS_START_ACCUM  0  /* fold into the target's current value (Updater arrival fold)     */
@@ -133,7 +136,7 @@ int ipls_agg_update_gradient(ipls_agg *h, const void *flat, int64_t n, int src_k
 /* Updater._Update for one arriving bucket (Updater.java:36-48 REP branch,
  * 74-137 AGG branches): target[p][i] = target[p][i] + g[i], i < L_p.
  * n = #doubles (F64/BE kinds) or frame byte length (FRAME kind; the frame's
- * n field must be >= L_p).  Returns IPLS_E_RANGE when the bucket is shorter
+ * n field must be >= L_p; PAIR kind: its double[] must be >= L_p).  Returns IPLS_E_RANGE when the bucket is shorter
  * than L_p.  Also Collect_Replicas (IPLS.java:1217-1241) with target REP. */
 int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t n,
                         int src_kind);
@@ -320,6 +323,39 @@ int64_t ipls_frame_parse(const uint8_t *frame, int64_t len, int16_t *pid, int32_
 int64_t ipls_frame_encode(const double *g, int64_t n, int g_kind, int32_t a, int32_t b,
                           int16_t pid, const uint8_t *origin, int32_t origin_len,
                           uint8_t *out, int64_t out_cap);
+
+/* ---- the partial-update object: Java-serialised Pair<Integer, double[]> ----
+ * IPLS_Comm.commit_partial_update (IPLS_Comm.java:51-61) and
+ * DStorage_Client.sendPartition(..., mod 1) (DStorage_Client.java:152-154,
+ * `-i 1`) write new Pair<>(workers, Aggregated_Gradients[p]) with
+ * ObjectOutputStream; Download_Scheduler (:324-325) and the storage merge
+ * (Decentralized_Storage_Receiver.java:249-256) read it back. */
+
+/* Parse such a stream: returns the number of doubles (the payload is that
+ * many big-endian doubles at byte *payload_off) and the Integer in *workers,
+ * or IPLS_E_FORMAT (not a Pair<Integer,double[]> object stream, or truncated). */
+int64_t ipls_pair_parse(const uint8_t *buf, int64_t len, int32_t *workers, int64_t *payload_off);
+
+/* The exact bytes ObjectOutputStream.writeObject(new Pair<>(workers, g)) writes
+ * for n doubles (g_kind HOST_F64 or HOST_BE).  Returns the byte count; with
+ * out == NULL only the count; IPLS_E_RANGE if out_cap is too small. */
+int64_t ipls_pair_encode(int32_t workers, const void *g, int64_t n, int g_kind, uint8_t *out,
+                         int64_t out_cap);
+
+/* commit_partial_update's file bytes for AGG[p] (IPLS.java:1423-1425):
+ * Pair<>(workers, Aggregated_Gradients[p]) with the payload packed on the
+ * device.  Returns the byte count (out == NULL: count only). */
+int64_t ipls_agg_commit_partial(ipls_agg *h, int p, int32_t workers, uint8_t *out, int64_t out_cap);
+
+/* The storage node's merge (Decentralized_Storage_Receiver.java:239-258) of k
+ * downloaded files: status 0 -> raw BE files (file_kind HOST_BE), status != 0
+ * -> Pair partial updates (HOST_PAIR).  Aggregation = the first file's doubles;
+ * then Aggregation[j] += g[j] for j < g.length, file by file; the result is
+ * written to out as the `<p>_partial_aggregation` file bytes (update_file: BE).
+ * Returns the byte count; IPLS_E_RANGE when a later file is longer than the
+ * first (the reference's ArrayIndexOutOfBoundsException) or out_cap is short. */
+int64_t ipls_agg_merge_files(ipls_agg *h, const uint8_t *const *files, const int64_t *lens, int k,
+                             int file_kind, uint8_t *out, int64_t out_cap);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@
 
 #include "../../include/ipls_agg.h"
 #include "ipls_kernels.hpp"
+#include "javaser.hpp"
 
 using namespace ipls;
 
@@ -89,6 +90,8 @@ struct ipls_agg {
   unsigned long long* d_sum = nullptr;
   double* d_cnt = nullptr;   // per-partition count slots of a fused round (P doubles)
   unsigned long long* d_gbuf = nullptr;   // Updater.run's Gradient_Buff (Updater.java:162), lazily
+  unsigned long long* d_merge = nullptr;  // storage-merge accumulator, grown on demand
+  int64_t merge_cap = 0;
   // PeerData.Other_Replica_Gradients / _Received, keyed (partition, aggregator);
   // std::map order = the canonical (ascending) Collect_Replicas order
   struct OtherRep {
@@ -614,6 +617,7 @@ int ipls_agg_close(ipls_agg* h) {
   if (h->d_sum) hipFree(h->d_sum);
   if (h->d_cnt) hipFree(h->d_cnt);
   if (h->d_gbuf) hipFree(h->d_gbuf);
+  if (h->d_merge) hipFree(h->d_merge);
   for (auto& kv : h->other)
     if (kv.second.d) hipFree(kv.second.d);
   if (h->arena) hipFree(h->arena);
@@ -720,6 +724,20 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
       if (int rc = host_decode_count(src_kind, nd, L, h)) return rc;
       if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
       // The payload starts at byte 14 (unaligned); staging realigns it.
+      if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
+      dptr = h->d_scratch;
+      be = true;
+      break;
+    }
+    case IPLS_HOST_PAIR: {
+      // Download_Partial_Updates(hash).getValue1() -> queue -> _Update (Download_Scheduler.java:324)
+      int32_t workers;
+      int64_t poff;
+      const char* why = nullptr;
+      const int64_t nd = javaser::parse_pair((const uint8_t*)src, n, &workers, &poff, &why);
+      if (nd < 0) return fail(h, IPLS_E_FORMAT, "partial update: %s (ObjectInputStream)", why ? why : "malformed");
+      if (int rc = host_decode_count(src_kind, nd, L, h)) return rc;
+      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
       if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
       dptr = h->d_scratch;
       be = true;
@@ -1629,6 +1647,118 @@ int64_t ipls_frame_parse(const uint8_t* frame, int64_t len, int16_t* pid, int32_
   if (payload_off) *payload_off = 14;
   if (origin_off) *origin_off = 14 + 8 * (int64_t)n;
   return n;
+}
+
+int64_t ipls_pair_parse(const uint8_t* buf, int64_t len, int32_t* workers, int64_t* payload_off) {
+  if (!buf || len < 0) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  const char* why = nullptr;
+  const int64_t nd = javaser::parse_pair(buf, len, workers, payload_off, &why);
+  if (nd < 0) return fail(nullptr, IPLS_E_FORMAT, "partial update: %s", why ? why : "malformed");
+  return nd;
+}
+
+int64_t ipls_pair_encode(int32_t workers, const void* g, int64_t n, int g_kind, uint8_t* out, int64_t out_cap) {
+  if (n < 0 || n > INT32_MAX || (n > 0 && out && !g)) return fail(nullptr, IPLS_E_INVAL, "bad argument");
+  if (g_kind != IPLS_HOST_F64 && g_kind != IPLS_HOST_BE) return fail(nullptr, IPLS_E_INVAL, "g_kind must be HOST_F64/BE");
+  const int64_t hl = javaser::pair_header_len(), total = hl + 8 * n + javaser::pair_trailer_len();
+  if (!out) return total;
+  if (out_cap < total) return fail(nullptr, IPLS_E_RANGE, "partial update needs %lld bytes", (long long)total);
+  javaser::write_pair_header(out, workers, (int32_t)n);
+  if (g_kind == IPLS_HOST_BE) {
+    std::memcpy(out + hl, g, (size_t)n * 8);
+  } else {
+    for (int64_t i = 0; i < n; ++i) {   // ObjectOutputStream: writeDouble = BE doubleToLongBits
+      uint64_t v;
+      std::memcpy(&v, (const char*)g + 8 * i, 8);
+      v = __builtin_bswap64(v);
+      std::memcpy(out + hl + 8 * i, &v, 8);
+    }
+  }
+  javaser::write_pair_trailer(out + hl + 8 * n);
+  return total;
+}
+
+int64_t ipls_agg_commit_partial(ipls_agg* h, int p, int32_t workers, uint8_t* out, int64_t out_cap) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (int rc = check_part(h, p)) return rc;
+  const int64_t L = h->len[p];
+  const int64_t hl = javaser::pair_header_len(), total = hl + 8 * L + javaser::pair_trailer_len();
+  if (!out) return total;
+  if (out_cap < total) return fail(h, IPLS_E_RANGE, "partial update needs %lld bytes", (long long)total);
+  HIP_TRY(h, hipSetDevice(h->device));
+  javaser::write_pair_header(out, workers, (int32_t)L);
+  if (h->agg_zero[p]) {
+    std::memset(out + hl, 0, (size_t)L * 8);   // +0.0 in any byte order
+  } else {
+    if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+    hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0, h->stream,
+                       (const unsigned long long*)(h->arena + h->agg_off[p]), (unsigned long long*)h->d_scratch, L);
+    HIP_TRY(h, hipGetLastError());
+    if (int rc = d2h(h, out + hl, h->d_scratch, (size_t)L * 8)) return rc;
+  }
+  javaser::write_pair_trailer(out + hl + 8 * L);
+  return total;
+}
+
+int64_t ipls_agg_merge_files(ipls_agg* h, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
+                             uint8_t* out, int64_t out_cap) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (k < 1 || !files || !lens) return fail(h, IPLS_E_INVAL, "need at least one file");
+  if (file_kind != IPLS_HOST_BE && file_kind != IPLS_HOST_PAIR) return fail(h, IPLS_E_INVAL, "file_kind BE or PAIR");
+  // decode every file's payload position first (GetParameters / Download_Partial_Updates)
+  std::vector<int64_t> nd(k), off(k);
+  for (int i = 0; i < k; ++i) {
+    if (!files[i] && lens[i] > 0) return fail(h, IPLS_E_INVAL, "file %d is NULL", i);
+    if (file_kind == IPLS_HOST_BE) {
+      nd[i] = lens[i] / 8;
+      off[i] = 0;
+    } else {
+      int32_t w;
+      const char* why = nullptr;
+      nd[i] = javaser::parse_pair(files[i], lens[i], &w, &off[i], &why);
+      if (nd[i] < 0) return fail(h, IPLS_E_FORMAT, "file %d: %s (ObjectInputStream)", i, why ? why : "malformed");
+    }
+    if (i > 0 && nd[i] > nd[0])   // Aggregation[j] += Gradient[j] for j < Gradient.length (:244-246)
+      return fail(h, IPLS_E_RANGE, "file %d has %lld doubles > %lld of the first "
+                  "(ArrayIndexOutOfBoundsException, Decentralized_Storage_Receiver.java:245)", i,
+                  (long long)nd[i], (long long)nd[0]);
+  }
+  const int64_t n0 = nd[0];
+  if (out_cap < 8 * n0 || (!out && n0 > 0)) return fail(h, IPLS_E_RANGE, "merge output needs %lld bytes", (long long)(8 * n0));
+  if (n0 == 0) return 0;
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (h->merge_cap < n0) {
+    if (h->d_merge) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      HIP_TRY(h, hipFree(h->d_merge));
+      h->d_merge = nullptr;
+      h->merge_cap = 0;
+    }
+    HIP_TRY(h, hipMalloc(&h->d_merge, (size_t)n0 * 8));
+    h->merge_cap = n0;
+  }
+  for (int i = 0; i < k; ++i) {
+    if (nd[i] == 0) continue;
+    if (int rc = ensure_scratch(h, (size_t)nd[i] * 8)) return rc;
+    if (int rc = stage_h2d(h, h->d_scratch, files[i] + off[i], (size_t)nd[i] * 8)) return rc;
+    const dim3 g(std::min<unsigned>(blocks_for(nd[i], kBlock), 4096));
+    if (i == 0)   // Aggregation = GetParameters(Hashes.get(0)): the first file as is
+      hipLaunchKernelGGL((k_fold_n<true, true>), g, dim3(kBlock), 0, h->stream, h->d_merge,
+                         (const unsigned long long*)h->d_scratch, nd[i]);
+    else
+      hipLaunchKernelGGL((k_fold_n<true, false>), g, dim3(kBlock), 0, h->stream, h->d_merge,
+                         (const unsigned long long*)h->d_scratch, nd[i]);
+    HIP_TRY(h, hipGetLastError());
+  }
+  // update_file(..., Aggregation): putDouble per element (MyIPFSClass.java:105-116)
+  if (int rc = ensure_scratch(h, (size_t)n0 * 8)) return rc;
+  hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(n0, kBlock), 4096)), dim3(kBlock), 0, h->stream,
+                     (const unsigned long long*)h->d_merge, (unsigned long long*)h->d_scratch, n0);
+  HIP_TRY(h, hipGetLastError());
+  if (int rc = d2h(h, out, h->d_scratch, (size_t)n0 * 8)) return rc;
+  return 8 * n0;
 }
 
 int64_t ipls_frame_encode(const double* g, int64_t n, int g_kind, int32_t a, int32_t b, int16_t pid,

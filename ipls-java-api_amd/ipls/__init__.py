@@ -6,12 +6,13 @@ The arithmetic runs in hand-written gfx950 HIP kernels inside
 binding plus the Middleware wire codec.
 """
 from ._native import (  # noqa: F401
-    ALL_PARTITIONS, DEV_BE, DEV_F64, HOST_BE, HOST_BE_CANON, HOST_F64, HOST_FRAME,
+    ALL_PARTITIONS, DEV_BE, DEV_F64, HOST_BE, HOST_BE_CANON, HOST_F64, HOST_FRAME, HOST_PAIR,
     START_ACCUM, START_FIRST, START_ZERO, TGT_AGG, TGT_FUTURE, TGT_REP, TGT_WADDR, TGT_WEIGHTS,
     IplsError, lib,
 )
 from .aggregator import (  # noqa: F401
-    Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, encode_secure, frame_encode, frame_parse, synth_fill,
+    Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, encode_secure, frame_encode, frame_parse, pair_encode,
+    pair_parse, synth_fill,
 )
 
 SEED = 0x1B5_2026  # synthetic workload seed (SURVEY.md §8(d))

@@ -21,7 +21,7 @@ IPLS_E_INVAL, IPLS_E_RANGE, IPLS_E_NEGSIZE, IPLS_E_NOMEM = -1, -2, -3, -4
 IPLS_E_DEVICE, IPLS_E_FORMAT, IPLS_E_NODEV = -5, -6, -7
 
 TGT_AGG, TGT_REP, TGT_WEIGHTS, TGT_WADDR, TGT_FUTURE = 0, 1, 2, 3, 4
-HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON = 0, 1, 2, 3, 4, 5
+HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON, HOST_PAIR = 0, 1, 2, 3, 4, 5, 6
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1
 
@@ -101,6 +101,10 @@ SIGNATURES = {
     "ipls_encode_secure": (_i, [_vp, _vp, _i64, _i, _i, _vp]),
     "ipls_frame_parse": (_i64, [_vp, _i64, _P(_i16), _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
     "ipls_frame_encode": (_i64, [_vp, _i64, _i, _i32, _i32, _i16, _vp, _i32, _vp, _i64]),
+    "ipls_pair_parse": (_i64, [_vp, _i64, _P(_i32), _P(_i64)]),
+    "ipls_pair_encode": (_i64, [_i32, _vp, _i64, _i, _vp, _i64]),
+    "ipls_agg_commit_partial": (_i64, [_vp, _i, _i32, _vp, _i64]),
+    "ipls_agg_merge_files": (_i64, [_vp, _P(_vp), _P(_i64), _i, _i, _vp, _i64]),
 }
 
 _lib = None

@@ -180,7 +180,7 @@ class Aggregator:
             self._h, ptr, n, kind, owned.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(owned)))
 
     def Update(self, gradient, partition: int, from_clients: bool = True, *, frame: bool = False,
-               from_future: bool = False):
+               pair: bool = False, from_future: bool = False):
         """Updater._Update: client buckets fold into Aggregated_Gradients
         (Updater.java:115-117), replica partial sums into Replicas_Gradients
         (Updater.java:40-44), and a client's bucket for a later iteration
@@ -191,10 +191,10 @@ class Aggregator:
         if gradient is None:
             return
         target = N.TGT_FUTURE if from_future else (N.TGT_AGG if from_clients else N.TGT_REP)
-        if frame:
+        if frame or pair:       # a pubsub frame / a Java-serialised Pair<Integer,double[]> partial update
             a = np.frombuffer(bytes(gradient), dtype=np.uint8)
             self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, a.ctypes.data,
-                                                    a.size, N.HOST_FRAME))
+                                                    a.size, N.HOST_PAIR if pair else N.HOST_FRAME))
             return
         ptr, n, kind, keep = _operand(gradient)
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
@@ -348,6 +348,35 @@ class Aggregator:
             ap = res.ctypes.data if res.size else None
         self._chk(self._lib.ipls_agg_aggregate_round(self._h, p_first, n_parts, arr, k, kind, ap, ak))
         return res
+
+    def commit_partial_update(self, partition: int, workers: int) -> bytes:
+        """IPLS_Comm.commit_partial_update (IPLS_Comm.java:51-61, called at
+        IPLS.java:1423-1425): the Java-serialised new Pair<>(workers,
+        Aggregated_Gradients[p]) file bytes, packed on the device."""
+        n = self._chk(self._lib.ipls_agg_commit_partial(self._h, partition, workers, None, 0))
+        out = np.empty(n, dtype=np.uint8)
+        self._chk(self._lib.ipls_agg_commit_partial(self._h, partition, workers, out.ctypes.data, n))
+        return out.tobytes()
+
+    def merge_files(self, files, *, partial_updates: bool = False) -> bytes:
+        """Storage node merge (Decentralized_Storage_Receiver.java:239-258) of
+        downloaded files -- raw BE gradient files (status 0) or Pair partial
+        updates (status != 0) -- into the `_partial_aggregation` file bytes."""
+        arrs = [np.frombuffer(bytes(f), dtype=np.uint8) for f in files]
+        k = len(arrs)
+        ptrs = (ctypes.c_void_p * max(1, k))(*[a.ctypes.data if a.size else None for a in arrs])
+        lens = (ctypes.c_int64 * max(1, k))(*[a.size for a in arrs])
+        kind = N.HOST_PAIR if partial_updates else N.HOST_BE
+        if k == 0:
+            raise ValueError("need at least one file")
+        if partial_updates:
+            n0, _, _ = pair_parse(arrs[0])
+            cap = 8 * len(n0)
+        else:
+            cap = 8 * (arrs[0].size // 8)
+        out = np.empty(max(1, cap), dtype=np.uint8)
+        nb = self._chk(self._lib.ipls_agg_merge_files(self._h, ptrs, lens, k, kind, out.ctypes.data, cap))
+        return out[:nb].tobytes()
 
     def Merge(self, partition: int, buckets, *, big_endian: bool = True, target: int = N.TGT_REP):
         """Storage-node merge (Decentralized_Storage_Receiver.java:239-247):
@@ -504,6 +533,26 @@ def frame_parse(frame: bytes):
     n = N.check(N.lib().ipls_frame_parse(a.ctypes.data, a.size, ctypes.byref(pid), ctypes.byref(x),
                                          ctypes.byref(y), ctypes.byref(po), ctypes.byref(oo)))
     return pid.value, n, x.value, y.value, po.value, oo.value
+
+
+def pair_parse(data):
+    """Download_Partial_Updates (MyIPFSClass.java:326-338) through the C-ABI:
+    (gradients as float64, workers, payload byte offset)."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8)
+    w, off = ctypes.c_int32(), ctypes.c_int64()
+    n = N.check(N.lib().ipls_pair_parse(a.ctypes.data, a.size, ctypes.byref(w), ctypes.byref(off)))
+    g = np.frombuffer(a[off.value:off.value + 8 * n].tobytes(), dtype=">f8").astype(np.float64)
+    return g, w.value, off.value
+
+
+def pair_encode(workers: int, gradients) -> bytes:
+    """ObjectOutputStream.writeObject(new Pair<>(workers, gradients)), as
+    MyIPFSClass.Update_file(String, Pair) writes it (MyIPFSClass.java:160-166)."""
+    g = np.ascontiguousarray(gradients, dtype=np.float64)
+    n = N.check(N.lib().ipls_pair_encode(workers, g.ctypes.data, g.size, N.HOST_F64, None, 0))
+    out = np.empty(n, dtype=np.uint8)
+    N.check(N.lib().ipls_pair_encode(workers, g.ctypes.data, g.size, N.HOST_F64, out.ctypes.data, n))
+    return out.tobytes()
 
 
 def frame_encode(gradient, a: int, b: int, pid: int, origin: bytes) -> bytes:

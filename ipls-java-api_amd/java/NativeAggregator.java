@@ -78,6 +78,22 @@ public final class NativeAggregator implements AutoCloseable {
         return participants;
     }
 
+    /** IPLS_Comm.commit_partial_update (IPLS_Comm.java:51-61): the Pair<Integer,double[]> file bytes. */
+    public byte[] commitPartial(int p, int workers) {
+        byte[] out = new byte[(int) commitPartialLen(handle, p, workers)];
+        commitPartial(handle, p, workers, out);
+        return out;
+    }
+
+    /** Download_Scheduler.java:324: a replica's Pair partial update, folded into REP. */
+    public void updateFromPartial(byte[] catBytes, int p) { accumulatePair(handle, p, TGT_REP, catBytes); }
+
+    /** Decentralized_Storage_Receiver.java:239-258: merge of downloaded files
+     *  (raw BE gradient files, or Pair partial updates when status != 0). */
+    public byte[] mergeFiles(byte[][] files, boolean partialUpdates) {
+        return mergeFiles(handle, files, partialUpdates);
+    }
+
     /** Tail of Update_Client_WaitAck_List (IPLS.java:1556-1562). */
     public void promoteFuture(int[] authList) { promoteFuture(handle, authList); }
 
@@ -140,6 +156,10 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void getPartitions(long h, double[] out);
     private static native void aggregateRound(long h, int pFirst, int nParts, double[] avgOut);
     private static native void promoteFuture(long h, int[] parts);
+    private static native long commitPartialLen(long h, int p, int workers);
+    private static native void commitPartial(long h, int p, int workers, byte[] out);
+    private static native void accumulatePair(long h, int p, int target, byte[] file);
+    private static native byte[] mergeFiles(long h, byte[][] files, boolean partialUpdates);
     private static native void otherReplicaDirect(long h, int p, int aggregator, ByteBuffer buf, long n);
     private static native void collectReplicas(long h, int[] participants);
     private static native void getPartitionsWire(long h, ByteBuffer direct);

@@ -7,6 +7,7 @@
  * has none, so it is compiled on the Java side's build host.
  */
 #include <jni.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/ipls_agg.h"
@@ -184,6 +185,66 @@ JNIEXPORT void JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass
     int rc = ipls_agg_collect_replicas(H(h), (int32_t *)ps);
     (*env)->ReleaseIntArrayElements(env, out, ps, 0);
     CHECK(rc, H(h));
+}
+
+JNIEXPORT jlong JNICALL Java_NativeAggregator_commitPartialLen(JNIEnv *env, jclass c, jlong h, jint p, jint w) {
+    (void)c;
+    int64_t n = ipls_agg_commit_partial(H(h), p, w, NULL, 0);
+    if (n < 0) { throw_for(env, (int)n, H(h)); return 0; }
+    return (jlong)n;
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_commitPartial(JNIEnv *env, jclass c, jlong h, jint p, jint w,
+                                                             jbyteArray out) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, out);
+    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    int64_t rc = ipls_agg_commit_partial(H(h), p, w, (uint8_t *)dst, n);
+    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    if (rc < 0) throw_for(env, (int)rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_accumulatePair(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
+                                                              jbyteArray file) {
+    (void)c;
+    jsize n = (*env)->GetArrayLength(env, file);
+    void *src = (*env)->GetPrimitiveArrayCritical(env, file, NULL);
+    int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_PAIR);
+    (*env)->ReleasePrimitiveArrayCritical(env, file, src, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclass c, jlong h, jobjectArray files,
+                                                                jboolean partial) {
+    (void)c;
+    jsize k = (*env)->GetArrayLength(env, files);
+    if (k < 1) { throw_for(env, IPLS_E_INVAL, H(h)); return NULL; }
+    jbyteArray *arr = (jbyteArray *)calloc((size_t)k, sizeof(jbyteArray));
+    const uint8_t **ptrs = (const uint8_t **)calloc((size_t)k, sizeof(uint8_t *));
+    int64_t *lens = (int64_t *)calloc((size_t)k, sizeof(int64_t));
+    jbyteArray res = NULL;
+    for (jsize i = 0; i < k; ++i) {   /* copies: several arrays cannot be held critical across a JNI call */
+        arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, files, i);
+        lens[i] = (*env)->GetArrayLength(env, arr[i]);
+        ptrs[i] = (const uint8_t *)(*env)->GetByteArrayElements(env, arr[i], NULL);
+    }
+    int64_t cap = 8 * (lens[0] / 8);
+    if (partial) {
+        int32_t w; int64_t off;
+        int64_t n0 = ipls_pair_parse(ptrs[0], lens[0], &w, &off);
+        cap = n0 < 0 ? 0 : 8 * n0;
+    }
+    uint8_t *out = (uint8_t *)malloc((size_t)(cap > 0 ? cap : 1));
+    int64_t nb = ipls_agg_merge_files(H(h), ptrs, lens, k, partial ? IPLS_HOST_PAIR : IPLS_HOST_BE, out, cap);
+    for (jsize i = 0; i < k; ++i) (*env)->ReleaseByteArrayElements(env, arr[i], (jbyte *)ptrs[i], JNI_ABORT);
+    if (nb < 0) {
+        throw_for(env, (int)nb, H(h));
+    } else {
+        res = (*env)->NewByteArray(env, (jsize)nb);
+        if (res) (*env)->SetByteArrayRegion(env, res, 0, (jsize)nb, (const jbyte *)out);
+    }
+    free(out); free(lens); free(ptrs); free(arr);
+    return res;
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf) {

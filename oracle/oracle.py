@@ -156,6 +156,18 @@ def collect_replicas(rep: list, store: dict, participants: list | None = None) -
     return n
 
 
+def storage_merge(gradients: list) -> np.ndarray:
+    """Decentralized_Storage_Receiver.java:239-256: Aggregation = the first
+    file's doubles; Aggregation[j] += g[j] for j < g.length, file by file
+    (IndexError where Java overruns the first array)."""
+    agg = np.array(gradients[0], dtype=np.float64, copy=True)
+    for g in gradients[1:]:
+        if len(g) > len(agg):
+            raise IndexError("ArrayIndexOutOfBoundsException (Decentralized_Storage_Receiver.java:245)")
+        agg[:len(g)] = agg[:len(g)] + g
+    return agg
+
+
 def promote_future(agg: np.ndarray, fut: np.ndarray) -> None:
     """IPLS.java:1557-1562 (Update_Client_WaitAck_List): for j < L,
     Aggregated_Gradients[p][j] = from_future[p].get(j); from_future[p].set(j, 0.0)."""

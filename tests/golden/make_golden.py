@@ -11,6 +11,13 @@ Outputs (all data, no reference source):
   golden.json        -- metadata, checksums of the full-size synthetic configs,
                         SHA-256 of the config-A outputs
 
+  ref_scheduler.ser  -- the reference's own `Scheduler` file, byte for byte: a
+                        Java ObjectOutputStream of an org.javatuples.Pair (data;
+                        pins the Pair/Tuple/Object[]/Integer/Number/
+                        Arrays$ArrayList descriptors of oracle/javaser.py)
+  ref_ethmodel_head.bin -- the first 136 bytes of ETHModel (its stream header,
+                        incl. the `[D` descriptor)
+
 Expected values come from the Python restatement (oracle/oracle.py) and are
 cross-checked bit for bit against the C restatement (oracle/ipls_oracle.c)
 before anything is written.  Parity status: unpinned.
@@ -152,6 +159,9 @@ def main():
     model = O.parse_ethmodel(ref.read_bytes())
     assert model.shape == (443610,)
     (HERE / "ethmodel.f64be.gz").write_bytes(gzip.compress(model.astype(">f8").tobytes(), 9, mtime=0))
+    (HERE / "ref_ethmodel_head.bin").write_bytes(ref.read_bytes()[:136])
+    sched = ref.parent.parent / "Scheduler"            # <reference>/Scheduler, written by Bootstraper_Services
+    (HERE / "ref_scheduler.ser").write_bytes(sched.read_bytes())
 
     meta = {"seed": SEED, "parity": "unpinned (no reference golden vectors; SURVEY.md §8(c))"}
     peers, sums, avg = config_a(model)

@@ -935,3 +935,39 @@ def test_async_pinned_arrivals(ipls, O):
     agg.close()
     for pb in bufs:
         pb.close()
+
+
+def test_partial_update_pair_files(ipls, O):
+    """-i 1 partial updates: commit_partial_update's Pair<Integer,double[]>
+    bytes (IPLS_Comm.java:51-61) from AGG on the device; a replica's Pair
+    folded into REP (Download_Scheduler.java:324); the storage merge of Pair
+    and raw BE files (Decentralized_Storage_Receiver.java:239-258)."""
+    from oracle import javaser as J
+    M, P = 40003, 2
+    agg = ipls.Aggregator(M, P, max_peers=4)
+    Ls = agg.lengths
+    own = [O.synth_bucket(Ls[0], 0, k) for k in range(3)]
+    for b in own:
+        agg.Update(b, 0)
+    S = O.reduce(own, Ls[0])
+    file0 = agg.commit_partial_update(0, workers=3)
+    assert file0 == J.encode_pair(3, S)
+    assert agg.commit_partial_update(1, workers=1) == J.encode_pair(1, np.zeros(Ls[1]))   # empty AGG
+    # a replica's partial update arrives as a Pair file -> REP
+    rep = O.synth_bucket(Ls[0], 0, 40)
+    agg.Update(J.encode_pair(2, rep), 0, from_clients=False, pair=True)
+    assert_bits_equal(agg.read(0, ipls.TGT_REP), O.reduce([rep], Ls[0]), "REP from Pair")
+    with pytest.raises(ipls.IplsError):
+        agg.Update(J.encode_pair(2, rep[:-1]), 0, from_clients=False, pair=True)        # shorter than L_p
+    with pytest.raises(ipls.IplsError):
+        agg.Update(file0[:-3], 0, pair=True)                                             # truncated stream
+    # storage merge: first file as is (-0.0 kept), later files folded, prefix rule
+    g = [O.synth_bucket(5000, 1, k) for k in range(4)]
+    g[0][::5] = -0.0
+    g[2] = g[2][:4000]
+    ref = O.storage_merge(g)
+    assert agg.merge_files([O.be_encode(x) for x in g]) == O.be_encode(ref)
+    assert agg.merge_files([J.encode_pair(k, x) for k, x in enumerate(g)], partial_updates=True) == O.be_encode(ref)
+    with pytest.raises(ipls.IplsError):
+        agg.merge_files([O.be_encode(g[2]), O.be_encode(g[1])])                          # later file longer
+    agg.close()

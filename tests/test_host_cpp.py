@@ -28,3 +28,17 @@ def test_host_mirror_on_gpu():
     r = subprocess.run([str(BIN), "--gpu", str(GOLDEN)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "6 passed, 0 failed" in r.stdout, r.stdout
+
+
+def test_partial_update_parser_under_asan():
+    """Fuzz the Java-serialisation parser (csrc/javaser.cpp) built for the
+    host with AddressSanitizer + UBSan (no GPU code involved)."""
+    out = ROOT / "tests" / "cpp" / "build" / "fuzz_javaser"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    csrc = ROOT / "ipls-java-api_amd" / "csrc"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", f"-I{csrc}", str(ROOT / "tests" / "cpp" / "fuzz_javaser.cpp"),
+                    str(csrc / "javaser.cpp"), "-o", str(out)], check=True)
+    r = subprocess.run([str(out), str(GOLDEN / "ref_scheduler.ser")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "fuzz ok" in r.stdout
