@@ -235,6 +235,17 @@ class IPLS {
     return file;
   }
 
+  // IPLS_Comm.commit_partial_update (IPLS_Comm.java:51-61): the file bytes of
+  // new Pair<>(workers, Aggregated_Gradients[Partition]) (ObjectOutputStream).
+  std::vector<uint8_t> commit_partial_update(int Partition, int32_t workers) {
+    const int64_t n = ipls_agg_commit_partial(h_.get(), Partition, workers, nullptr, 0);
+    if (n < 0) raise((int)n, h_.get());
+    std::vector<uint8_t> out((size_t)n);
+    const int64_t m = ipls_agg_commit_partial(h_.get(), Partition, workers, out.data(), n);
+    if (m < 0) raise((int)m, h_.get());
+    return out;
+  }
+
   // Tail of Update_Client_WaitAck_List (IPLS.java:1556-1562): for p in
   // Auth_List, Aggregated_Gradients[p] = from_future[p], from_future[p] = 0.
   void Update_Client_WaitAck_List() {
@@ -307,6 +318,13 @@ class Updater {
                               (int64_t)Gradient->size(), IPLS_HOST_F64),
           ipls_.handle());
   }
+  // Download_Scheduler.java:324: a replica's Pair<Integer,double[]> partial
+  // update (Download_Partial_Updates) queued with from_clients = false.
+  void _Update_from_partial(const std::vector<uint8_t>& pair_file, int Partiton) {
+    check(ipls_agg_accumulate(ipls_.handle(), Partiton, IPLS_TGT_REP, pair_file.data(), (int64_t)pair_file.size(),
+                              IPLS_HOST_PAIR),
+          ipls_.handle());
+  }
   // ThreadReceiver pid 3 -> queue -> _Update (IPLS.java:453-465): a decoded frame.
   void _Update_from_frame(const std::vector<uint8_t>& frame, int Partiton, bool from_clients) {
     check(ipls_agg_accumulate(ipls_.handle(), Partiton, from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP, frame.data(),
@@ -316,6 +334,38 @@ class Updater {
 
  private:
   IPLS& ipls_;
+};
+
+// ---- Decentralized_Storage_Receiver (storage node, -aggr 1) ----------------------
+// The merge of the files one request names (Decentralized_Storage_Receiver.java:
+// 239-258): status 0 -> raw gradient files, otherwise Pair partial updates;
+// returns the `<p>_partial_aggregation` file bytes.
+class Decentralized_Storage_Receiver {
+ public:
+  explicit Decentralized_Storage_Receiver(IPLS& node) : node_(node) {}
+  std::vector<uint8_t> merge(const std::vector<std::vector<uint8_t>>& files, int status) {
+    std::vector<const uint8_t*> ptrs;
+    std::vector<int64_t> lens;
+    for (const auto& f : files) ptrs.push_back(f.data()), lens.push_back((int64_t)f.size());
+    const int kind = status == 0 ? IPLS_HOST_BE : IPLS_HOST_PAIR;
+    int64_t cap = files.empty() ? 0 : (int64_t)(files[0].size() / 8) * 8;
+    if (status != 0 && !files.empty()) {
+      int32_t w;
+      int64_t off;
+      const int64_t n0 = ipls_pair_parse(files[0].data(), (int64_t)files[0].size(), &w, &off);
+      if (n0 < 0) raise((int)n0, nullptr);
+      cap = 8 * n0;
+    }
+    std::vector<uint8_t> out((size_t)std::max<int64_t>(cap, 1));
+    const int64_t nb = ipls_agg_merge_files(node_.handle(), ptrs.data(), lens.data(), (int)files.size(), kind,
+                                            out.data(), cap);
+    if (nb < 0) raise((int)nb, node_.handle());
+    out.resize((size_t)nb);
+    return out;
+  }
+
+ private:
+  IPLS& node_;
 };
 
 // ---- Light_IPLS_Daemon (Light_IPLS_Daemon.java) -----------------------------------

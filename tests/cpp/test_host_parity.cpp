@@ -212,6 +212,42 @@ int main(int argc, char** argv) {
       CHECK(second == ref, "promoted future gradients");
     });
 
+    run("partial updates (-i 1): commit, replica fold, storage merge", [&] {
+      PeerData pd;
+      pd._MODEL_SIZE = 20001;
+      pd._PARTITIONS = 2;
+      IPLS ipls(pd, {0, 1});
+      Updater u(ipls);
+      const int64_t L0 = ipls_oracle_partition_len(20001, 2, 0);
+      auto g = synth(L0, 0, 5);
+      u._Update(&g, 0, true);
+      auto file = ipls.commit_partial_update(0, 4);
+      int32_t w = 0;
+      int64_t off = 0;
+      CHECK(ipls_pair_parse(file.data(), (int64_t)file.size(), &w, &off) == L0 && w == 4, "Pair header");
+      std::vector<double> back((size_t)L0);
+      ipls_oracle_be_decode(file.data() + off, L0, back.data());
+      std::vector<double> s((size_t)L0);
+      const double* bp[1] = {g.data()};
+      ipls_oracle_reduce(s.data(), bp, 1, L0, 1);
+      CHECK(bits_equal(back.data(), s.data(), (size_t)L0), "Pair payload = AGG");
+      u._Update_from_partial(file, 0);                    // as a replica partial -> REP
+      auto sum = ipls.AggregatePartition(0);               // W = AGG + REP = 2 * S
+      std::vector<double> w2((size_t)L0), zero((size_t)L0, 0.0), wa((size_t)L0);
+      std::vector<double> a = s, r = s;
+      ipls_oracle_aggregate_partition(a.data(), r.data(), w2.data(), wa.data(), L0);
+      std::vector<uint8_t> ref(8 * (size_t)L0);
+      ipls_oracle_be_encode(w2.data(), L0, ref.data());
+      CHECK(sum == ref, "AGG + REP after the Pair fold");
+      Decentralized_Storage_Receiver store(ipls);
+      auto merged = store.merge({file, file}, 1);
+      std::vector<double> m2((size_t)L0);
+      const double* mp[2] = {s.data(), s.data()};
+      ipls_oracle_reduce(m2.data(), mp, 2, L0, 2);        // FIRST start: S + S
+      ipls_oracle_be_encode(m2.data(), L0, ref.data());
+      CHECK(merged == ref, "storage merge of two Pair files");
+    });
+
     run("exceptions", [] {
       PeerData pd;
       pd._MODEL_SIZE = 10;
