@@ -971,3 +971,76 @@ def test_partial_update_pair_files(ipls, O):
     with pytest.raises(ipls.IplsError):
         agg.merge_files([O.be_encode(g[2]), O.be_encode(g[1])])                          # later file longer
     agg.close()
+
+
+def test_full_ipls_round_four_peers(ipls, O):
+    """One synchronous IPLS round across 4 simulated peers on one GPU, every
+    transport of the path in play, checked end to end against the oracle:
+      * partition p is aggregated by A = p and by the replica B = p+1 (mod 4);
+      * each aggregator folds its own gradient (UpdateGradient, IPLS.java:1737),
+        A receives the others as pubsub texts (ThreadReceiver, double base64),
+        B as `ipfs cat` files through Gradient_Buff (Updater.run indirect);
+      * partials cross as -i 1 Pair<Integer,double[]> files (commit_partial_update
+        -> Download_Partial_Updates -> REP), except that the replica of
+        partition 3 stays silent and its aggregator folds the bucket it had
+        downloaded for it instead (Other_Replica_Gradients + Collect_Replicas);
+      * A commits W (AggregatePartition -> update_file bytes), every peer
+        caches every partition it does not aggregate (cache_partition) and
+        GetPartitions gives the model, identical on all peers."""
+    from oracle import javaser as J
+    M, P, NP = 100003, 4, 4
+    grads = [O.synth_bucket(M, 9, k) for k in range(NP)]           # flat List<Double> per peer
+    parts = [O.organize_gradients(g, M, P) for g in grads]
+    Ls = [O.partition_len(M, P, p) for p in range(P)]
+    A = lambda p: p                                                 # noqa: E731
+    B = lambda p: (p + 1) % NP                                      # noqa: E731
+    peers = [ipls.Aggregator(M, P, max_peers=NP) for _ in range(NP)]
+    auth = [[k, (k - 1) % P] for k in range(NP)]                   # own partition + the one it replicates
+    # ---- device: gradients to the aggregators ----
+    for k, agg in enumerate(peers):
+        agg.UpdateGradient(grads[k], auth_list=auth[k])
+    for p in range(P):
+        msgs = [O.pubsub_message(O.frame_encode(parts[k][p], p, 0, 3, f"QmPeer{k}".encode()))
+                for k in range(NP) if k != A(p)]
+        n_ok, st = peers[A(p)].ingest_pubsub(msgs, partitions=[p] * len(msgs))
+        assert n_ok == len(msgs) and st == [0] * len(msgs)
+        for k in range(NP):
+            if k != B(p):
+                peers[B(p)].UpdateIndirect(O.be_encode(parts[k][p]), p)
+    # ---- partial exchange ----
+    for p in range(P):
+        if p != 3:                                                  # replica answers with its partial
+            f = peers[B(p)].commit_partial_update(p, workers=NP)
+            peers[A(p)].Update(f, p, from_clients=False, pair=True)
+        else:                                                       # silent replica: use what A downloaded for it
+            peers[A(p)].OtherReplicaGradients(p, B(p), parts[B(p)][p])
+    for k in range(NP):
+        peers[k].Collect_Replicas()
+    # ---- commit and distribute ----
+    files = {}
+    for p in range(P):
+        s, _ = peers[A(p)].AggregatePartition(p, with_sum=True, sum_big_endian=True)
+        files[p] = bytes(s)
+    for k, agg in enumerate(peers):
+        for p in range(P):
+            if A(p) != k:
+                agg.cache_partition(p, files[p])
+    models = [agg.GetPartitions() for agg in peers]
+    # ---- oracle ----
+    W = []
+    for p in range(P):
+        own_a = [parts[A(p)][p]] + [parts[k][p] for k in range(NP) if k != A(p)]
+        agg_a = O.reduce(own_a, Ls[p])
+        if p != 3:
+            own_b = [parts[B(p)][p]] + [parts[k][p] for k in range(NP) if k != B(p)]
+            partial = J.parse_pair(J.encode_pair(NP, O.reduce(own_b, Ls[p])))[1]
+            rep = O.reduce([partial], Ls[p])
+        else:
+            rep = O.reduce([parts[B(p)][p]], Ls[p])
+        W.append(agg_a + rep)
+        assert files[p] == O.be_encode(W[p]), f"update_file of partition {p}"
+    ref = O.get_partitions(W)
+    for k in range(NP):
+        assert_bits_equal(models[k], ref, f"model on peer {k}")
+    for agg in peers:
+        agg.close()
