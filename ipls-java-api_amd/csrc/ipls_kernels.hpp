@@ -175,10 +175,11 @@ __device__ __forceinline__ void reduce_tiles(
 
   if (base + kTile <= L) {
     // ---------------- vector path: R x 16 B per lane ----------------
-    // (This form -- per-r offsets, loads of a peer group written before its
-    // adds -- is the one hipcc schedules as "all G x R loads, then counted
-    // vmcnt waits" within 128 VGPRs at R = 16; a single lane-base pointer
-    // made it interleave 2 loads at a time with vmcnt(0).  Checked in the ISA.)
+    // (hipcc, held to 128 VGPRs by the 1024-lane bound, issues a peer's R
+    // loads one or two at a time per wave (checked in the ISA); the 16 waves
+    // of a CU then sweep one 16 KiB window of the bucket at a time, which is
+    // the DRAM pattern that measured best -- forcing all R loads in flight
+    // with scheduling barriers was slower.)
     int64_t off[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * kBlock + tid);
