@@ -52,6 +52,42 @@ __global__ __launch_bounds__(kBlock) void k_readall(const unsigned long long* co
   if ((acc.x ^ acc.y) == 0x1234567ULL) sink[0] = acc.x;
 }
 
+// Experimental fold: uniform bucket base + 32-bit lane offset, and (FORCE)
+// scheduling groups that put all R loads of a peer in flight before its adds.
+// Full tiles only (L a multiple of BS*2*R); partition-major block order.
+template <bool BE, int R, int BS, bool FORCE>
+__global__ __launch_bounds__(BS) void k_exp(const unsigned long long* const* __restrict__ bufs,
+                                            unsigned long long* __restrict__ dst, int64_t dstride, int k,
+                                            int tpp) {
+  const int q = blockIdx.x / tpp, t = blockIdx.x - q * tpp;
+  const int64_t base = (int64_t)t * BS * 2 * R;
+  const unsigned lane16 = threadIdx.x * 16u;
+  const unsigned long long* const* pb = bufs + (size_t)q * k;
+  d2 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = d2{0.0, 0.0};
+  for (int j = 0; j < k; ++j) {
+    const char* src = (const char*)(pb[j] + base);
+    u2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load((gcu2)(src + (size_t)r * BS * 16 + lane16));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const d2 x = decode2<BE>(v[r]);
+      acc[r].x = acc[r].x + x.x;
+      acc[r].y = acc[r].y + x.y;
+    }
+    if constexpr (FORCE) {
+      __builtin_amdgcn_sched_group_barrier(0x020, R, 0);     // R VMEM reads
+      __builtin_amdgcn_sched_group_barrier(0x002, 1000, 0);  // then the VALU work
+    }
+  }
+  char* d = (char*)(dst + q * dstride + base);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    __builtin_nontemporal_store(encode2<false>(acc[r]), (gu2)(d + (size_t)r * BS * 16 + lane16));
+}
+
 __global__ __launch_bounds__(kBlock) void k_copy(const u2* __restrict__ in, u2* __restrict__ out, int64_t n2) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (int64_t)gridDim.x * kBlock)
     __builtin_nontemporal_store(__builtin_nontemporal_load((gcu2)(in + i)), (gu2)(out + i));
@@ -139,6 +175,26 @@ int main(int argc, char** argv) {
   ADDC(1, 16, 2, 256);
   ADDC(8, 1, 0, 256);
 #undef ADDC
+#define EXP(R, BS, FORCE)                                                                       \
+  vars.push_back(Var{"exp R=" #R " BS=" #BS " force=" #FORCE,                                    \
+                     [=](hipStream_t s) {                                                       \
+                       const int tpp = (int)(L / ((int64_t)BS * 2 * R));                        \
+                       auto bp = (const unsigned long long* const*)d_ptrs;                      \
+                       const int64_t ds = (L + 31) / 32 * 32;                                   \
+                       if (be)                                                                  \
+                         hipLaunchKernelGGL((k_exp<true, R, BS, FORCE>), dim3(tpp * P), dim3(BS), 0, s, bp, dst, ds, K, tpp); \
+                       else                                                                     \
+                         hipLaunchKernelGGL((k_exp<false, R, BS, FORCE>), dim3(tpp * P), dim3(BS), 0, s, bp, dst, ds, K, tpp); \
+                     },                                                                         \
+                     alg, {}})
+  if (L % (1024 * 2 * 16) == 0) {
+    EXP(16, 1024, false);
+    EXP(8, 1024, true);
+    EXP(16, 1024, true);
+    EXP(16, 512, true);
+    EXP(8, 512, true);
+  }
+#undef EXP
 #define RA(G, R)                                                                                   \
   vars.push_back(Var{"readall G=" #G " R=" #R " (read ceiling)",                                     \
                      [=](hipStream_t s) {                                                            \
