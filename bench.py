@@ -93,7 +93,17 @@ def cpu_baseline(L: int, K: int, passes: int) -> dict:
                       f"oracle/ipls_oracle.c ipls_oracle_updater_loop (JDK absent: C restatement)",
             "multi_thread": {"value": round(nbytes / dt_mt / 1e9, 3), "cores": threads,
                              "sample": f"{passes} partitions in parallel, one thread each"},
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dict:
