@@ -65,6 +65,13 @@ def parse():
     ap.add_argument("--cpu-passes", type=int, default=16,
                     help="CPU baseline sample: passes over one partition's K buckets")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-replica-leg", action="store_true",
+                    help="N>1: skip the cross-GPU replica exchange measurement (config E)")
+    ap.add_argument("--replica-reps", type=int, default=5)
+    ap.add_argument("--replica-timeout", type=float, default=120.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearsal of the N>1 code on one GPU (ranks share cuda:0, partials "
+                         "travel through host memory); numbers are not a measurement")
     return ap.parse_args()
 
 
@@ -165,6 +172,80 @@ def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dic
             "pcie_ceiling": "~56 GB/s per direction measured (tools/h2d_bench.hip, profiles/r01/h2d_bench.txt)"}
 
 
+def replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, reps, verify, backend="nccl") -> dict:
+    """Config E (N > 1): a partition's contributors span GPUs.  Every rank owns
+    its P partitions and folds their first K/2 peers; it is also the replica
+    aggregator of P partitions owned by the other ranks (ReplicaPlan.spread:
+    each rank sends partials to, and receives them from, every other rank),
+    folding their last K/2 peers into a second handle.  One round = both
+    folds, the exchange of the P partials each way over RCCL point-to-point
+    (one batched group, every xGMI link at once), the fixed-order fold of
+    the landed partials into REP and AggregatePartition (W = AGG + REP,
+    IPLS.java:1256).  Reuses the main bench's bucket pool: the last K/2
+    slots of each row are refilled with the replicated partitions' buckets."""
+    import torch
+    import torch.distributed as dist
+    from ipls.distributed import RankShard, ReplicaPlan, combine_replicas
+    plan = ReplicaPlan.spread(P * world, world)
+    rep_ids = plan.replicated_on(rank)
+    assert len(rep_ids) == P
+    kh = K // 2
+    for i, p in enumerate(rep_ids):
+        for k in range(kh, K):
+            ipls.synth_fill(rows[i][k], p, k, ipls.SEED)
+    torch.cuda.synchronize()
+    own_rows = [r[:kh] for r in rows]
+    rep_rows = [r[kh:] for r in rows]
+    rep = ipls.Aggregator(n_partitions=P, bucket_len=L, device=local)
+    xdev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+    shard = RankShard(agg, rank * P, rep, rep_ids, device=xdev)
+
+    def one_round():
+        agg.reduce_batch(0, own_rows, start_mode=ipls.START_ZERO)
+        rep.reduce_batch(0, rep_rows, start_mode=ipls.START_ZERO)
+        rep.sync()
+        agg.sync()
+        t0 = time.perf_counter()
+        combine_replicas(shard, plan, rank, device=xdev)
+        agg.sync()
+        t1 = time.perf_counter()
+        agg.AggregatePartition(ipls.ALL_PARTITIONS)
+        agg.sync()
+        return t1 - t0
+
+    one_round()                                     # warm: RCCL P2P channels, transport buffers
+    verified = None
+    if verify and rank == 0:
+        from oracle import oracle as O              # checker only
+        verified = agg.checksum(0, ipls.TGT_WEIGHTS) == O.c_synth_replica_checksum(L, 0, K, kh)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ex = 0.0
+    for _ in range(reps):
+        ex += one_round()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt, ex], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, ex = float(t[0].item()) / reps, float(t[1].item()) / reps
+    rep.close()
+    sent = P * L * 8                                # each rank sends P partials, receives P
+    return {
+        "workload": f"E-style: {P} partitions per GPU owned, K={K} peers split {kh}/{K - kh} between the owner "
+                    f"and one replica GPU (ReplicaPlan.spread: every rank exchanges with all {world - 1} others)",
+        "round_ms": round(dt * 1e3, 3),
+        "exchange_ms": round(ex * 1e3, 3),
+        "xgmi_bytes_per_rank_each_way": sent,
+        "exchange_GBps_per_rank_each_way": round(sent / ex / 1e9, 2),
+        "exchange_GBps_aggregate": round(world * sent / ex / 1e9, 2),
+        "round_GBps_algorithmic": round(world * P * (K + 1) * L * 8 / dt / 1e9, 1),
+        "verified_checksum_p0": verified,
+        "note": "exchange_ms = export of the partials, one batched RCCL send/recv group, fold into REP "
+                "(max over ranks); round adds both folds and AggregatePartition",
+    }
+
+
 def pmc_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass for this
     workload (profiles/pmc_traffic.json), or None."""
@@ -191,10 +272,15 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     if not torch.cuda.is_available():
         sys.exit("bench.py needs an MI355X (no HIP device visible)")
+    if args.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     import ipls
     P, L, K = CONFIGS[args.config]
@@ -253,7 +339,7 @@ def main():
     dt = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = float(t.item())
@@ -357,6 +443,28 @@ def main():
             out["host_inclusive"] = host_inclusive(ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, K, args.cpu_passes)
+    if world > 1 and not args.no_replica_leg and not args.be:
+        # the cross-GPU exchange is an extra measurement: a watchdog makes sure
+        # a stuck exchange can never cost the main line (every rank exits)
+        import threading
+
+        def expire():
+            if out is not None:
+                out["replica_exchange"] = {"error": f"timed out after {args.replica_timeout} s"}
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+        dog = threading.Timer(args.replica_timeout, expire)
+        dog.daemon = True
+        dog.start()
+        try:
+            leg = replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, args.replica_reps,
+                                   not args.no_verify, args.dist_backend)
+        except Exception as e:                       # reported, never fatal to the main line
+            leg = {"error": f"{type(e).__name__}: {e}"}
+        dog.cancel()
+        if out is not None:
+            out["replica_exchange"] = leg
+    if out is not None:
         print(json.dumps(out), flush=True)
     agg.close()
     if world > 1:

@@ -66,6 +66,27 @@ class ReplicaPlan:
             h[p] = sorted({o, *replicas.get(p, ())})
         return cls(n_partitions, world, h)
 
+    @classmethod
+    def spread(cls, n_partitions: int, world: int) -> "ReplicaPlan":
+        """Every partition gets one replica aggregator on another GPU, spread
+        so that each rank sends to and receives from every other rank: the
+        q-th partition of rank o is replicated on ``(o + 1 + q % (G-1)) % G``.
+        All G-1 xGMI links of a GPU carry partials at once (config E of
+        SURVEY.md §8(d): contributors of a partition span GPUs)."""
+        if world < 2:
+            return cls.build(n_partitions, world)
+        per = -(-n_partitions // world)
+        replicas = {}
+        for p in range(n_partitions):
+            o, q = p // per, p % per
+            replicas[p] = [(o + 1 + q % (world - 1)) % world]
+        return cls.build(n_partitions, world, replicas)
+
+    def replicated_on(self, rank: int) -> list[int]:
+        """Partitions rank holds a replica partial of (it is not their owner)."""
+        return [p for p, hs in self.holders.items()
+                if rank in hs and owner_of(p, self.n_partitions, self.world) != rank]
+
     def exchanges(self):
         """[(p, owner, [replica ranks in fold order])] for partitions whose
         contributors span GPUs."""
@@ -86,9 +107,9 @@ def combine_replicas(agg, plan: ReplicaPlan, rank: int, *, device=None, mode: st
     Every rank calls this with the same plan. Point-to-point operations are
     posted in one global order (partition ascending, replica ascending), so
     every pair of ranks sees its sends and receives in the same order and
-    no cycle can deadlock. All receives are posted up front, so the k partials
-    of a partition stream in concurrently over their own links. They are then
-    folded strictly in replica order as each lands."""
+    no cycle can deadlock. All sends and receives are posted as one batch, so
+    the k partials of a partition stream in concurrently over their own links.
+    Once the batch has landed they are folded strictly in replica order."""
     import torch
     import torch.distributed as dist
 
@@ -115,25 +136,64 @@ def combine_replicas(agg, plan: ReplicaPlan, rank: int, *, device=None, mode: st
                 filled.append(p)
         return filled
 
-    pending, sends, filled = [], [], []
+    # All of this rank's sends and receives go out as ONE batch
+    # (batch_isend_irecv: one RCCL group), so partials to and from every
+    # peer GPU move at once, each pair over its own xGMI link.  The ops are
+    # listed in the global (partition, replica) order on every rank.
+    ops, landing, filled = [], [], []
+    bufs = getattr(agg, "transport_buffers", None)
     for p, owner, others in exchanges:
-        L = agg.lengths[p]
         if rank == owner:
+            L = agg.lengths[p]
             for r in others:
-                buf = torch.empty(L, dtype=torch.float64, device=device)
-                pending.append((p, buf, dist.irecv(buf, src=r, group=group)))
+                buf = bufs(("in", p, r), L) if bufs else torch.empty(L, dtype=torch.float64, device=device)
+                ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
+                landing.append((p, buf))
             filled.append(p)
         elif rank in others:
-            buf = torch.empty(L, dtype=torch.float64, device=device)
+            L = agg.lengths[p]
+            buf = bufs(("out", p, rank), L) if bufs else torch.empty(L, dtype=torch.float64, device=device)
             agg.export_partial(p, buf)                    # AGG[p] -> the published partial
-            sends.append((buf, dist.isend(buf, dst=owner, group=group)))
-    for p, buf, work in pending:                          # fold in (partition, replica) order
-        work.wait()
-        _landed(buf)
+            ops.append(dist.P2POp(dist.isend, buf, owner, group=group))
+    if ops:
+        for work in dist.batch_isend_irecv(ops):
+            work.wait()
+    if landing:
+        _landed(landing[0][1])
+    for p, buf in landing:                                # fold in (partition, replica) order
         agg.import_partial(p, buf)                        # REP[p] += R_r (Updater.java:40-44)
-    for _, work in sends:
-        work.wait()
     return filled
+
+
+class RankShard:
+    """One rank's handles under node-wide partition ids, for combine_replicas.
+
+    ``own`` holds the partitions this GPU owns, ``[first, first + n)`` as local
+    ``0..n-1``; ``rep`` holds the partials it aggregates as a replica for other
+    GPUs' partitions (``rep_ids[i]`` is local partition ``i``).  Transport
+    buffers are allocated once and reused across rounds."""
+
+    def __init__(self, own, first: int, rep=None, rep_ids=(), device=None):
+        self.own, self.first, self.rep = own, first, rep
+        self.rep_index = {p: i for i, p in enumerate(rep_ids)}
+        self.device = device
+        self.lengths = {first + i: L for i, L in enumerate(own.lengths)}
+        if rep is not None:
+            self.lengths.update({p: rep.lengths[i] for p, i in self.rep_index.items()})
+        self._bufs = {}
+
+    def transport_buffers(self, key, L):
+        import torch
+        b = self._bufs.get(key)
+        if b is None:
+            b = self._bufs[key] = torch.empty(L, dtype=torch.float64, device=self.device)
+        return b
+
+    def export_partial(self, p, tensor):
+        self.rep.export_partial(self.rep_index[p], tensor)
+
+    def import_partial(self, p, tensor, replace_agg=False):
+        self.own.import_partial(p - self.first, tensor, replace_agg=replace_agg)
 
 
 def _landed(buf):

@@ -209,6 +209,29 @@ uint64_t ipls_oracle_synth_sum_checksum(uint64_t seed, int32_t p, int32_t k, int
     return s;
 }
 
+/* Checksum of W = AGG + REP when partition p's k peers are split over two
+ * aggregators: the owner folds peers [0, k_own) into Aggregated_Gradients
+ * (Updater.java:115-117), the replica folds peers [k_own, k) into its own
+ * partial, which lands in the owner's fresh Replicas_Gradients
+ * (Updater.java:40-44: +0.0 + R), and AggregatePartition adds the two
+ * (IPLS.java:1256). */
+uint64_t ipls_oracle_synth_replica_checksum(uint64_t seed, int32_t p, int32_t k, int32_t k_own, int64_t L) {
+    uint64_t s = 0;
+#pragma omp parallel for reduction(+ : s) schedule(static)
+    for (int64_t i = 0; i < L; i++) {
+        double own = 0.0, part = 0.0;
+        for (int32_t j = 0; j < k; j++) {
+            double g = (i == L - 1) ? 1.0 : ipls_oracle_synth_value(seed, p, j, i);
+            if (j < k_own) own = own + g;
+            else part = part + g;
+        }
+        double rep = 0.0;
+        rep = rep + part;
+        s += checksum_term(own + rep, i);
+    }
+    return s;
+}
+
 /* Checksum of the averaged output of the same fold (GetPartitions divide,
  * IPLS.java:1159-1174) over i < L-1, element index i: cnt = S[L-1] (the fold
  * of k count slots), out = cnt == 0 ? S[i] : S[i] / (secure ? 1e12*cnt : cnt). */

@@ -105,6 +105,9 @@ uint64_t ipls_oracle_checksum(const double *x, int64_t n);
  * order is unchanged, so this is still the reference's arithmetic. */
 uint64_t ipls_oracle_synth_sum_checksum(uint64_t seed, int32_t p, int32_t k, int64_t L);
 uint64_t ipls_oracle_synth_avg_checksum(uint64_t seed, int32_t p, int32_t k, int64_t L, int32_t secure);
+/* W = AGG(peers [0,k_own)) + (+0.0 + partial(peers [k_own,k))): one replica
+ * aggregator's partial folded into the owner's REP, then AggregatePartition. */
+uint64_t ipls_oracle_synth_replica_checksum(uint64_t seed, int32_t p, int32_t k, int32_t k_own, int64_t L);
 
 /* CPU baseline: the reference's Updater loop over k BE byte buckets,
  * 1 thread: decode each bucket into a reused double[] (Updater.java:162,177

@@ -384,6 +384,8 @@ def c_oracle():
         lib.ipls_oracle_synth_sum_checksum.argtypes = [u64, i32, i32, i64]
         lib.ipls_oracle_synth_avg_checksum.restype = u64
         lib.ipls_oracle_synth_avg_checksum.argtypes = [u64, i32, i32, i64, i32]
+        lib.ipls_oracle_synth_replica_checksum.restype = u64
+        lib.ipls_oracle_synth_replica_checksum.argtypes = [u64, i32, i32, i32, i64]
         lib.ipls_oracle_updater_loop.argtypes = [D, ctypes.POINTER(U8), ctypes.c_int, i64, D]
         lib.ipls_oracle_updater_loop_parts.restype = ctypes.c_int
         lib.ipls_oracle_updater_loop_parts.argtypes = [ctypes.c_int, ctypes.POINTER(U8), ctypes.c_int, i64, D]
@@ -412,6 +414,11 @@ def c_synth_bucket(L: int, p: int, k: int, seed: int = SEED) -> np.ndarray:
 
 def c_synth_sum_checksum(L: int, p: int, k: int, seed: int = SEED) -> int:
     return int(c_oracle().ipls_oracle_synth_sum_checksum(seed, p, k, L))
+
+
+def c_synth_replica_checksum(L: int, p: int, k: int, k_own: int, seed: int = SEED) -> int:
+    """W = AGG(peers < k_own) + (+0.0 + partial(peers >= k_own)) (IPLS.java:1256, Updater.java:40-44)."""
+    return int(c_oracle().ipls_oracle_synth_replica_checksum(seed, p, k, k_own, L))
 
 
 def c_synth_avg_checksum(L: int, p: int, k: int, secure: bool = False, seed: int = SEED) -> int:

@@ -117,6 +117,64 @@ def test_replica_exchange_fixed_order(world, replicas):
         assert_bits_equal(got[p], exp[p], f"partition {p}")
 
 
+def shard_worker(rank, world, port, P, L, K, q):
+    """The bench's config-E exchange (ReplicaPlan.spread + RankShard): each rank
+    owns P partitions, folds their first K/2 peers, and is the replica of P
+    other partitions (their last K/2 peers) in a second handle."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ipls.distributed import RankShard, ReplicaPlan, combine_replicas
+    plan = ReplicaPlan.spread(P * world, world)
+    rep_ids = plan.replicated_on(rank)
+    own, rep = NumpyAggregator(P, L), NumpyAggregator(len(rep_ids), L)
+    for i in range(P):
+        for k in range(K // 2):
+            own.Update(bucket(rank * P + i, k, L), i)
+    for i, p in enumerate(rep_ids):
+        for k in range(K // 2, K):
+            rep.Update(bucket(p, k, L), i)
+    shard = RankShard(own, rank * P, rep, rep_ids, device="cpu")
+    filled = combine_replicas(shard, plan, rank, device="cpu")
+    q.put((rank, len(rep_ids), {p: own.finalize(p - rank * P) for p in filled}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_spread_replica_shards(world):
+    P, L, K = 6, 515, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=shard_worker, args=(r, world, port, P, L, K, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = {}
+    for _ in range(world):
+        rank, n_rep, res = q.get(timeout=120)
+        assert n_rep == P                        # every rank replicates exactly P partitions
+        got.update(res)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert sorted(got) == list(range(P * world))
+    for p, w in got.items():
+        own = O.reduce([bucket(p, k, L) for k in range(K // 2)], L)
+        part = O.reduce([bucket(p, k, L) for k in range(K // 2, K)], L)
+        assert_bits_equal(w, own + O.reduce([part], L), f"partition {p}")
+
+
+def test_spread_plan_uses_every_link():
+    from ipls.distributed import ReplicaPlan, owner_of
+    for world, P in ((2, 16), (4, 16), (8, 16)):
+        plan = ReplicaPlan.spread(P * world, world)
+        for r in range(world):
+            reps = plan.replicated_on(r)
+            assert len(reps) == P
+            srcs = {owner_of(p, P * world, world) for p in reps}
+            assert srcs == set(range(world)) - {r}
+
+
 def test_owner_mapping():
     from ipls.distributed import owned_partitions, owner_of
     # config E: 64 partitions on 4 GPUs -> 16 per GPU; F: 128 on 8

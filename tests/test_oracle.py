@@ -190,3 +190,13 @@ def test_c_synth_avg_checksum_matches_numpy(secure):
     L, p, k = 5003, 2, 3
     S = O.reduce([O.synth_bucket(L, p, j) for j in range(k)], L)
     assert O.c_synth_avg_checksum(L, p, k, secure) == O.checksum(O.divide(S, secure))
+
+
+@pytest.mark.parametrize("k,k_own", [(6, 3), (5, 1), (4, 4)])
+def test_c_synth_replica_checksum_matches_numpy(k, k_own):
+    """The bench's cross-GPU replica leg checks W = AGG + (+0.0 + R) through this."""
+    L, p = 4099, 3
+    own = O.reduce([O.synth_bucket(L, p, j) for j in range(k_own)], L)
+    part = O.reduce([O.synth_bucket(L, p, j) for j in range(k_own, k)], L)
+    W = own + O.reduce([part], L)
+    assert O.c_synth_replica_checksum(L, p, k, k_own) == O.checksum(W)
