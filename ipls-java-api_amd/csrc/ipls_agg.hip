@@ -277,12 +277,13 @@ unsigned blocks_for(int64_t n, int64_t per_block) { return (unsigned)((n + per_b
 constexpr int kBigG = 1, kBigMap = 0, kBigBS = 1024;
 constexpr int kSmallG = 8, kSmallR = 1, kSmallMap = 0;
 constexpr int64_t kBigMinBlocks = 512;
-// 16 x 16 B per lane fits the 128-VGPR budget of a 1024-lane workgroup only
-// for native-double input without an ACCUM read of the target; the BE-input
-// and ACCUM variants use 8 (16 spilled to scratch -- checked in the ISA).
-// The fused round (FIN) uses the same R: 128 VGPRs, no scratch (checked).
+// 16 x 16 B per lane in the 128-VGPR budget of a 1024-lane workgroup:
+// native doubles 126 VGPRs; big-endian input 110 with the SEQ schedule of
+// reduce_tiles (hipcc's own schedule hoisted the loads around the bswap and
+// spilled 184 B).  The ACCUM start keeps 8 (at 16 it still spills around
+// the loop -- checked with -Rpass-analysis=kernel-resource-usage).
 template <bool BE_IN, int START, bool FIN = false>
-constexpr int big_r() { return (!BE_IN && START != kAccum) ? 16 : 8; }
+constexpr int big_r() { return START != kAccum ? 16 : 8; }
 
 template <bool BE_IN, bool BE_OUT, int START, bool FIN = false>
 void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,

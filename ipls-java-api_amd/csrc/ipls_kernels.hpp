@@ -136,7 +136,7 @@ __device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_pa
 //   FIN    : fused round -- dst is Weights[p] and receives fold + REP
 //            (AggregatePartition, IPLS.java:1256), and parts[q].avg (if set)
 //            the GetPartitions divide (IPLS.java:1159-1174), in the same pass
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP, int BS, bool FIN>
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP, int BS, bool FIN, int SEQF>
 __device__ __forceinline__ void reduce_tiles(
     const unsigned long long* const* __restrict__ bufs, const PartDesc* __restrict__ parts,
     int k, int tiles_per_part, int n_parts, int secure, const double* __restrict__ cnts) {
@@ -184,6 +184,12 @@ __device__ __forceinline__ void reduce_tiles(
 #pragma unroll
     for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * kBlock + tid);
 
+    // SEQ: one peer per step, each of its R vectors loaded, decoded and added
+    // before the next is issued (a scheduling fence between them).  This is
+    // the schedule hipcc picks by itself for native doubles; with the bswap
+    // (or the ACCUM read of the target) in between it would hoist the loads
+    // instead and spill at R = 16.
+    constexpr bool SEQ = SEQF > 0 && (G == 1) && (BE_IN || START == kAccum) && R > 8;
     d2 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -194,8 +200,21 @@ __device__ __forceinline__ void reduce_tiles(
       } else {  // kAccum: the target holds native doubles (or BE if BE_OUT)
         acc[r] = decode2<BE_OUT>(ld16<false>(init + off[r]));
       }
+      if constexpr (SEQ && START != kZero) __builtin_amdgcn_sched_barrier(0);
     }
     int j = j0;
+    if constexpr (SEQ) {
+      for (; j < k; ++j) {
+        const unsigned long long* __restrict__ src = pb[j];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const d2 x = decode2<BE_IN>(ld16<NT>(src + off[r]));
+          acc[r].x = acc[r].x + x.x;
+          acc[r].y = acc[r].y + x.y;
+          if constexpr (SEQF > 0) if ((r + 1) % SEQF == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
     for (; j + G <= k; j += G) {
       u2 v[G][R];
 #pragma unroll
@@ -226,6 +245,7 @@ __device__ __forceinline__ void reduce_tiles(
         acc[r].y = acc[r].y + x.y;
       }
     }
+    }  // !SEQ
     if constexpr (FIN) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -299,18 +319,19 @@ __device__ __forceinline__ void reduce_tiles(
 
 // The batched fold (the benchmarked kernel) and the fused round are two
 // kernels over the same tile code, so profiles name them apart.
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock>
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock, int SEQF = 2>
 __global__ __launch_bounds__(BS) void k_reduce(const unsigned long long* const* __restrict__ bufs,
                                                const PartDesc* __restrict__ parts, int k, int tiles_per_part,
                                                int n_parts) {
-  reduce_tiles<BE_IN, BE_OUT, START, G, R, NT, MAP, BS, false>(bufs, parts, k, tiles_per_part, n_parts, 0, nullptr);
+  reduce_tiles<BE_IN, BE_OUT, START, G, R, NT, MAP, BS, false, SEQF>(bufs, parts, k, tiles_per_part, n_parts, 0,
+                                                                     nullptr);
 }
 
 template <bool BE_IN, int START, int G, int R, int MAP = 0, int BS = kBlock>
 __global__ __launch_bounds__(BS) void k_round(const unsigned long long* const* __restrict__ bufs,
                                               const PartDesc* __restrict__ parts, int k, int tiles_per_part,
                                               int n_parts, int secure, const double* __restrict__ cnts) {
-  reduce_tiles<BE_IN, false, START, G, R, true, MAP, BS, true>(bufs, parts, k, tiles_per_part, n_parts, secure,
+  reduce_tiles<BE_IN, false, START, G, R, true, MAP, BS, true, 2>(bufs, parts, k, tiles_per_part, n_parts, secure,
                                                                cnts);
 }
 

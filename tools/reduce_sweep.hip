@@ -162,18 +162,45 @@ int main(int argc, char** argv) {
                        const int tpp = (int)((L + tile - 1) / tile);                            \
                        const dim3 grid((unsigned)grid_blocks(MAP, (int64_t)tpp * P));           \
                        auto bp = (const unsigned long long* const*)d_ptrs;                      \
-                       if (be)                                                                  \
+                       if (be && be_out)                                                        \
+                         hipLaunchKernelGGL((k_reduce<true, true, kZero, G, R, true, MAP, BS>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                       else if (be)                                                             \
                          hipLaunchKernelGGL((k_reduce<true, false, kZero, G, R, true, MAP, BS>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
                        else                                                                     \
                          hipLaunchKernelGGL((k_reduce<false, false, kZero, G, R, true, MAP, BS>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
+  const bool be_out = getenv("SWEEP_BE_OUT") != nullptr;
+  const bool quick = getenv("SWEEP_QUICK") != nullptr;   // the shipped big shape and its neighbours only
   ADDC(1, 8, 0, 1024);
   ADDC(1, 16, 0, 1024);
   ADDC(1, 16, 2, 1024);
-  ADDC(1, 16, 0, 256);
-  ADDC(1, 16, 2, 256);
-  ADDC(8, 1, 0, 256);
+#define ADDS(R, MAP, F)                                                                           \
+  vars.push_back(Var{"reduce R=" #R " MAP=" #MAP " BS=1024 SEQF=" #F,                              \
+                     [=](hipStream_t s) {                                                       \
+                       const int64_t tile = (int64_t)1024 * 2 * R;                              \
+                       const int tpp = (int)((L + tile - 1) / tile);                            \
+                       const dim3 grid((unsigned)grid_blocks(MAP, (int64_t)tpp * P));           \
+                       auto bp = (const unsigned long long* const*)d_ptrs;                      \
+                       if (be_out)                                                              \
+                         hipLaunchKernelGGL((k_reduce<true, true, kZero, 1, R, true, MAP, 1024, F>), grid, dim3(1024), 0, s, bp, d_pd, K, tpp, P); \
+                       else                                                                     \
+                         hipLaunchKernelGGL((k_reduce<true, false, kZero, 1, R, true, MAP, 1024, F>), grid, dim3(1024), 0, s, bp, d_pd, K, tpp, P); \
+                     },                                                                         \
+                     alg, {}})
+  if (quick && be) {       // big-endian input: fence interval of the SEQ schedule
+    ADDS(16, 0, 1);
+    ADDS(16, 0, 4);
+    ADDS(16, 2, 1);
+    ADDS(16, 2, 4);
+  }
+#undef ADDS
+  if (quick) {
+  } else {
+    ADDC(1, 16, 0, 256);
+    ADDC(1, 16, 2, 256);
+    ADDC(8, 1, 0, 256);
+  }
 #undef ADDC
 #define EXP(R, BS, FORCE)                                                                       \
   vars.push_back(Var{"exp R=" #R " BS=" #BS " force=" #FORCE,                                    \
@@ -187,7 +214,7 @@ int main(int argc, char** argv) {
                          hipLaunchKernelGGL((k_exp<false, R, BS, FORCE>), dim3(tpp * P), dim3(BS), 0, s, bp, dst, ds, K, tpp); \
                      },                                                                         \
                      alg, {}})
-  if (L % (1024 * 2 * 16) == 0) {
+  if (L % (1024 * 2 * 16) == 0 && !quick) {
     EXP(16, 1024, false);
     EXP(8, 1024, true);
     EXP(16, 1024, true);
@@ -202,7 +229,7 @@ int main(int argc, char** argv) {
                                           dim3(kBlock), 0, s, (const unsigned long long* const*)d_ptrs, K, L, sink); \
                      },                                                                              \
                      (double)P * K * (L / (2 * kBlock * R)) * (2 * kBlock * R) * 8, {}})
-  RA(8, 1);
+  if (!quick) RA(8, 1);
   RA(1, 16);
   RA(2, 16);
 #undef RA
