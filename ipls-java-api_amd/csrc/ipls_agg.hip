@@ -284,6 +284,10 @@ constexpr int64_t kBigMinBlocks = 512;
 // the loop -- checked with -Rpass-analysis=kernel-resource-usage).
 template <bool BE_IN, int START, bool FIN = false>
 constexpr int big_r() { return START != kAccum ? 16 : 8; }
+// SEQ fence interval of the big shape (0 = hipcc's own schedule): big-endian
+// input at R = 16 fences every 2 loads (profiles/r01/sweep_be_seqf*.txt).
+template <bool BE_IN, int START>
+constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 2 : 0; }
 
 template <bool BE_IN, bool BE_OUT, int START, bool FIN = false>
 void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,
@@ -294,11 +298,12 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
   if (big_tpp * n_parts >= kBigMinBlocks) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
     if constexpr (FIN)
-      hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, kBigMap, kBigBS>), grid, dim3(kBigBS), 0, st, bufs, parts,
+      hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, kBigMap, kBigBS, big_seqf<BE_IN, START>()>), grid,
+                         dim3(kBigBS), 0, st, bufs, parts,
                          k, (int)big_tpp, n_parts, secure, cnts);
     else
-      hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS>), grid, dim3(kBigBS), 0,
-                         st, bufs, parts, k, (int)big_tpp, n_parts);
+      hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS, big_seqf<BE_IN, START>()>),
+                         grid, dim3(kBigBS), 0, st, bufs, parts, k, (int)big_tpp, n_parts);
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
     const int64_t tpp = (maxL + tile - 1) / tile;

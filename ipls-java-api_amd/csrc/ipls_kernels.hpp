@@ -189,7 +189,7 @@ __device__ __forceinline__ void reduce_tiles(
     // the schedule hipcc picks by itself for native doubles; with the bswap
     // (or the ACCUM read of the target) in between it would hoist the loads
     // instead and spill at R = 16.
-    constexpr bool SEQ = SEQF > 0 && (G == 1) && (BE_IN || START == kAccum) && R > 8;
+    constexpr bool SEQ = SEQF > 0 && G == 1;
     d2 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -319,7 +319,7 @@ __device__ __forceinline__ void reduce_tiles(
 
 // The batched fold (the benchmarked kernel) and the fused round are two
 // kernels over the same tile code, so profiles name them apart.
-template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock, int SEQF = 2>
+template <bool BE_IN, bool BE_OUT, int START, int G, int R, bool NT, int MAP = 0, int BS = kBlock, int SEQF = 0>
 __global__ __launch_bounds__(BS) void k_reduce(const unsigned long long* const* __restrict__ bufs,
                                                const PartDesc* __restrict__ parts, int k, int tiles_per_part,
                                                int n_parts) {
@@ -327,11 +327,11 @@ __global__ __launch_bounds__(BS) void k_reduce(const unsigned long long* const* 
                                                                      nullptr);
 }
 
-template <bool BE_IN, int START, int G, int R, int MAP = 0, int BS = kBlock>
+template <bool BE_IN, int START, int G, int R, int MAP = 0, int BS = kBlock, int SEQF = 0>
 __global__ __launch_bounds__(BS) void k_round(const unsigned long long* const* __restrict__ bufs,
                                               const PartDesc* __restrict__ parts, int k, int tiles_per_part,
                                               int n_parts, int secure, const double* __restrict__ cnts) {
-  reduce_tiles<BE_IN, false, START, G, R, true, MAP, BS, true, 2>(bufs, parts, k, tiles_per_part, n_parts, secure,
+  reduce_tiles<BE_IN, false, START, G, R, true, MAP, BS, true, SEQF>(bufs, parts, k, tiles_per_part, n_parts, secure,
                                                                cnts);
 }
 

@@ -182,17 +182,20 @@ int main(int argc, char** argv) {
                        const int tpp = (int)((L + tile - 1) / tile);                            \
                        const dim3 grid((unsigned)grid_blocks(MAP, (int64_t)tpp * P));           \
                        auto bp = (const unsigned long long* const*)d_ptrs;                      \
-                       if (be_out)                                                              \
+                       if (be && be_out)                                                        \
                          hipLaunchKernelGGL((k_reduce<true, true, kZero, 1, R, true, MAP, 1024, F>), grid, dim3(1024), 0, s, bp, d_pd, K, tpp, P); \
-                       else                                                                     \
+                       else if (be)                                                             \
                          hipLaunchKernelGGL((k_reduce<true, false, kZero, 1, R, true, MAP, 1024, F>), grid, dim3(1024), 0, s, bp, d_pd, K, tpp, P); \
+                       else                                                                     \
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, R, true, MAP, 1024, F>), grid, dim3(1024), 0, s, bp, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
-  if (quick && be) {       // big-endian input: fence interval of the SEQ schedule
+  if (quick) {             // fence interval of the SEQ schedule (0 = hipcc's own)
+    ADDS(16, 0, 0);
     ADDS(16, 0, 1);
+    ADDS(16, 0, 2);
     ADDS(16, 0, 4);
-    ADDS(16, 2, 1);
-    ADDS(16, 2, 4);
+    ADDS(16, 2, 2);
   }
 #undef ADDS
   if (quick) {
