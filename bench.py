@@ -129,46 +129,50 @@ def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dic
         pb.view()[:] = t.cpu().numpy()
         pinned.append(pb)
     pageable = [pb.view().copy() for pb in pinned]
+    sum_pinned = ipls.PinnedBuffer(8 * L)     # the commit_update bytes land in pinned memory too
     out = {}
     # batched: all K pinned buckets in one launch, read over PCIe (zero copy)
     row = [[ipls.DeviceBuffer(pb.ptr, L, big_endian=True) for pb in pinned]]
     agg.reduce_batch(0, row, start_mode=ipls.START_ZERO, big_endian=True)
-    agg.AggregatePartition(0, with_sum=True)
+    agg.AggregatePartition(0, sum_out=sum_pinned)
     t0 = time.perf_counter()
     for _ in range(reps):
         agg.reduce_batch(0, row, start_mode=ipls.START_ZERO, big_endian=True)
-        s, _ = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True)
+        agg.AggregatePartition(0, sum_out=sum_pinned)
     out["pinned_batched"] = round(reps * (K + 1) * L * 8 / (time.perf_counter() - t0) / 1e9, 2)
     for name, bufs in (("pinned", [pb.view() for pb in pinned]), ("pageable", pageable)):
+        so = sum_pinned if name == "pinned" else None   # pageable: a heap byte[] for the sum as well
         for b in bufs:                                   # warm
             agg.Update(b, 0)
-        agg.AggregatePartition(0, with_sum=True)
+        agg.AggregatePartition(0, with_sum=True, sum_out=so)
         t0 = time.perf_counter()
         for _ in range(reps):
             for b in bufs:
                 agg.Update(b, 0)
-            s, _ = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True)
+            agg.AggregatePartition(0, with_sum=True, sum_big_endian=True, sum_out=so)
         dt = time.perf_counter() - t0
         out[name] = round(reps * (K + 1) * L * 8 / dt / 1e9, 2)
     # per arrival, asynchronous: each fold is queued (ipls_agg_accumulate_async)
     # and the round waits once, at AggregatePartition
     for pb in pinned:                                    # warm
         agg.UpdateAsync(pb, 0)
-    agg.AggregatePartition(0, with_sum=True)
+    agg.AggregatePartition(0, sum_out=sum_pinned)
     t0 = time.perf_counter()
     for _ in range(reps):
         for pb in pinned:
             agg.UpdateAsync(pb, 0)
-        s, _ = agg.AggregatePartition(0, with_sum=True, sum_big_endian=True)
+        agg.AggregatePartition(0, sum_out=sum_pinned)
     out["pinned_async"] = round(reps * (K + 1) * L * 8 / (time.perf_counter() - t0) / 1e9, 2)
     agg.close()
     for pb in pinned:
         pb.close()
+    sum_pinned.close()
     return {"unit": "GB/s", **out,
             "sample": f"{reps} rounds x 1 partition x {K} peers x {L} doubles: each BE bucket from host memory "
                       f"(pinned: per-arrival zero-copy fold; pinned_async: the same, queued without waiting; "
                       f"pinned_batched: one launch over all K; pageable: "
-                      f"staged H2D) + finalize + D2H of the BE sum, algorithmic bytes (K+1)*L*8 per round",
+                      f"staged H2D) + finalize + D2H of the BE sum (into pinned memory, pageable for the pageable "
+                      f"leg), algorithmic bytes (K+1)*L*8 per round, Python/ctypes caller",
             "pcie_ceiling": "~56 GB/s per direction measured (tools/h2d_bench.hip, profiles/r01/h2d_bench.txt)"}
 
 

@@ -368,9 +368,12 @@ struct FinOut {
   unsigned long long* avg;   // averages of p_first.. at flat_off[p] - flat_off[p_first], or null
 };
 
+// host_src: the bucket is pinned host memory read over PCIe (zero copy); the
+// single-bucket fold then runs on 128 workgroups, which measured 1-2.5 GB/s
+// above 256..4096 (tools/h2d_bench.hip, profiles/r01/h2d_bench_fold1.txt).
 int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, bool be_in,
                int start_mode, int target, void* const* ext_dst = nullptr, bool be_out = false,
-               const FinOut* fin = nullptr) {
+               const FinOut* fin = nullptr, bool host_src = false) {
   auto dst_of = [&](int q) -> unsigned long long* {
     if (fin) return (unsigned long long*)(h->arena + h->w_off[p_first + q]);
     return ext_dst ? (unsigned long long*)ext_dst[q]
@@ -410,7 +413,8 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
     const int64_t L = h->len[p_first];
     if (d0 && !((uintptr_t)bufs[0] & 15) && !((uintptr_t)d0 & 15) && L > 0) {
       const auto* s0 = (const unsigned long long*)bufs[0];
-      const unsigned blocks = std::max(1u, std::min<unsigned>(blocks_for((L >> 1), kBlock * 4), 4096));
+      const unsigned blocks =
+          std::max(1u, std::min<unsigned>(blocks_for((L >> 1), kBlock * 4), host_src ? 128u : 4096u));
 #define F1(BI, BO, ST) hipLaunchKernelGGL((k_fold1<BI, BO, ST>), dim3(blocks), dim3(kBlock), 0, h->stream, d0, s0, L)
 #define F1S(BI, BO) do { if (start == kZero) F1(BI, BO, kZero); else if (start == kFirst) F1(BI, BO, kFirst); else F1(BI, BO, kAccum); } while (0)
       if (be_in) { if (be_out) F1S(true, true); else F1S(true, false); }
@@ -711,7 +715,8 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
         // staging copy, no second pass).  The call returns once the kernel
         // is done with the caller's bytes.
         const void* bl[1] = {alias};
-        if (int rc = reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target)) return rc;
+        if (int rc = reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target, nullptr, false, nullptr, true))
+          return rc;
         HIP_TRY(h, hipStreamSynchronize(h->stream));
         return IPLS_OK;
       }
@@ -781,7 +786,9 @@ int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, i
     h->ticket_done = t - ipls_agg::kTickets;
   }
   const void* bl[1] = {alias};   // zero copy: the kernel reads the pinned bucket over PCIe
-  if (int rc = reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target)) return rc;
+  if (int rc = reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target, nullptr, false, nullptr,
+                          true))
+    return rc;
   HIP_TRY(h, hipEventRecord(ev, h->stream));
   h->ticket_next = t + 1;
   *ticket = t;

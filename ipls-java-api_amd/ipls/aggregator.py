@@ -388,13 +388,20 @@ class Aggregator:
         return self.read(partition, target, big_endian=True)
 
     def AggregatePartition(self, partition: int, *, with_sum: bool = False, sum_big_endian: bool = True,
-                           with_average: bool = False):
+                           with_average: bool = False, sum_out=None):
         """IPLS.java:1248-1274.  Optionally returns the committed sum (the
-        update_file bytes of IPLS_Comm.commit_update) and the averaged values."""
+        update_file bytes of IPLS_Comm.commit_update) and the averaged values.
+        ``sum_out`` (a PinnedBuffer of at least 8*L_p bytes) receives the sum
+        instead of a new pageable array: the D2H then runs at the PCIe rate."""
         L = self.lengths[partition] if partition >= 0 else 0
         s = a = None
         sp, sk = None, N.HOST_F64
-        if with_sum:
+        if sum_out is not None:
+            if not isinstance(sum_out, PinnedBuffer) or sum_out.nbytes < 8 * L:
+                raise ValueError("sum_out must be a PinnedBuffer of at least 8*L_p bytes")
+            s = sum_out.view(np.uint8 if sum_big_endian else np.float64)[:8 * L if sum_big_endian else L]
+            sp, sk = sum_out.ptr, (N.HOST_BE if sum_big_endian else N.HOST_F64)
+        elif with_sum:
             s = np.empty(8 * L, dtype=np.uint8) if sum_big_endian else np.empty(L)
             sp, sk = s.ctypes.data, (N.HOST_BE if sum_big_endian else N.HOST_F64)
         ap = None

@@ -84,6 +84,26 @@ int main(int argc, char** argv) {
     }
     printf("zero-copy fold from pinned host, grid %4d: %7.2f GB/s\n", grid, bytes * K / best / 1e9);
   }
+  // the shipped per-arrival kernel (k_fold1, 4 pairs per lane in flight) reading
+  // pinned host memory: per-arrival sync (ipls_agg_accumulate) and queued
+  // (ipls_agg_accumulate_async), by grid size
+  for (int sync_each : {1, 0})
+    for (int grid : {128, 256, 512, 1024, 4096}) {
+      double best = 1e30;
+      for (int r = 0; r < REPS; ++r) {
+        CK(hipDeviceSynchronize());
+        const double t0 = now();
+        for (int k = 0; k < K; ++k) {
+          hipLaunchKernelGGL((k_fold1<true, false, kAccum, 4>), dim3(grid), dim3(kBlock), 0, st[0],
+                             (unsigned long long*)acc, (const unsigned long long*)host[k], L);
+          if (sync_each) CK(hipStreamSynchronize(st[0]));
+        }
+        CK(hipStreamSynchronize(st[0]));
+        best = std::min(best, now() - t0);
+      }
+      printf("k_fold1 from pinned host, %s, grid %4d: %7.2f GB/s\n", sync_each ? "sync each" : "queued   ", grid,
+             bytes * K / best / 1e9);
+    }
   // pageable sources (a Java heap byte[] pinned by GetPrimitiveArrayCritical)
   {
     std::vector<char*> pg(K);
