@@ -421,6 +421,35 @@ def test_pinned_host_operands(ipls, O):
     agg.close()
 
 
+def test_pinned_zero_copy_long_bucket_and_pinned_sum(ipls, O):
+    """Zero-copy single-bucket folds from pinned memory run on 128 workgroups:
+    a 2,000,003-double bucket takes several grid-stride passes plus the odd
+    tail.  The BE sum is written into a caller PinnedBuffer (sum_out)."""
+    L = 2000003
+    vals = [O.synth_bucket(L, 9, k) for k in range(3)]
+    bufs = []
+    for v in vals:
+        pb = ipls.PinnedBuffer(8 * L)
+        pb.view()[:] = np.frombuffer(O.be_encode(v), dtype=np.uint8)
+        bufs.append(pb)
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    agg.Update(bufs[0].view(), 0)                   # synchronous zero copy
+    t = agg.UpdateAsync(bufs[1], 0)                 # queued zero copy
+    agg.Update(bufs[2].view(), 0)
+    agg.Wait(t)
+    out = ipls.PinnedBuffer(8 * L)
+    s, _ = agg.AggregatePartition(0, sum_out=out)
+    ref = O.reduce(vals, L)
+    assert s.nbytes == 8 * L
+    assert bytes(s) == O.be_encode(ref)
+    assert_bits_equal(np.frombuffer(bytes(out.view()), dtype=">f8").astype(np.float64), ref, "pinned sum_out")
+    with pytest.raises(ValueError):
+        agg.AggregatePartition(0, sum_out=ipls.PinnedBuffer(8))
+    agg.close()
+    for pb in [*bufs, out]:
+        pb.close()
+
+
 def test_export_import_partial(ipls, O):
     """The GPU half of the replica exchange: a replica's partial leaves through
     export_partial (AGG -> device tensor) and the owner folds it into REP;
