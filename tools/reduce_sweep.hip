@@ -128,6 +128,16 @@ int main(int argc, char** argv) {
   const unsigned long long** d_ptrs;
   CK(hipMalloc(&d_ptrs, ptrs.size() * 8));
   CK(hipMemcpy(d_ptrs, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice));
+  // SWEEP_SHIFT=B: a second pointer table with every bucket start moved by B
+  // bytes (16-B multiple, < PAD*8), for same-process alignment comparisons.
+  const int64_t shift = getenv("SWEEP_SHIFT") ? atoll(getenv("SWEEP_SHIFT")) : 0;
+  const unsigned long long** d_ptrs_sh = nullptr;
+  if (shift) {
+    std::vector<const unsigned long long*> sp(ptrs.size());
+    for (size_t i = 0; i < ptrs.size(); ++i) sp[i] = (const unsigned long long*)((const char*)ptrs[i] + shift);
+    CK(hipMalloc(&d_ptrs_sh, sp.size() * 8));
+    CK(hipMemcpy(d_ptrs_sh, sp.data(), sp.size() * 8, hipMemcpyHostToDevice));
+  }
   std::vector<PartDesc> pd(P);
   int64_t off = 0;
   for (int p = 0; p < P; ++p) {
@@ -198,6 +208,35 @@ int main(int argc, char** argv) {
     ADDS(16, 2, 2);
   }
 #undef ADDS
+  if (shift && !be) {
+    // the same big-shape kernels over the shifted buckets: nt vs plain loads
+#define ADDSH(NT, tag)                                                                             \
+    vars.push_back(Var{"shifted reduce R=16 BS=1024 " tag,                                         \
+                       [=](hipStream_t s) {                                                        \
+                         const int64_t tile = (int64_t)1024 * 2 * 16;                              \
+                         const int tpp = (int)((L - 2 + tile - 1) / tile);                         \
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, 16, NT, 0, 1024>), dim3(tpp * P), \
+                                            dim3(1024), 0, s, (const unsigned long long* const*)d_ptrs_sh, d_pd, K, tpp, P); \
+                       },                                                                          \
+                       alg, {}})
+    ADDSH(true, "nt");
+    ADDSH(false, "plain loads");
+#undef ADDSH
+    vars.push_back(Var{"aligned reduce R=16 BS=1024 plain loads",
+                       [=](hipStream_t s) {
+                         const int64_t tile = (int64_t)1024 * 2 * 16;
+                         const int tpp = (int)((L + tile - 1) / tile);
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, 16, false, 0, 1024>), dim3(tpp * P),
+                                            dim3(1024), 0, s, (const unsigned long long* const*)d_ptrs, d_pd, K, tpp, P);
+                       },
+                       alg, {}});
+    vars.push_back(Var{"shifted readall G=1 R=16",
+                       [=](hipStream_t s) {
+                         hipLaunchKernelGGL((k_readall<1, 16>), dim3((unsigned)(L / (2 * kBlock * 16)), P), dim3(kBlock), 0,
+                                            s, (const unsigned long long* const*)d_ptrs_sh, K, L - 2, sink);
+                       },
+                       (double)P * K * (L / (2 * kBlock * 16)) * (2 * kBlock * 16) * 8, {}});
+  }
   if (quick) {
   } else {
     ADDC(1, 16, 0, 256);
