@@ -953,7 +953,7 @@ static int finalize_range(ipls_agg* h, int p0, int np) {
   }
   void* dtab = nullptr;
   if (int rc = upload_table(h, fd.data(), fd.size() * sizeof(FinDesc), &dtab)) return rc;
-  const int64_t tile = (int64_t)kBlock * 8;  // == k_finalize / k_divide tile (256 lanes x 2 x 4)
+  const int64_t tile = kFinTile;
   const int tpp = (int)((maxL + tile - 1) / tile);
   // AGG/REP are left in place and flagged logically zero (IPLS.java:1268-1269
   // zeroes them; the next fold starts from +0.0 without reading them).
@@ -981,7 +981,7 @@ static int divide_range(ipls_agg* h, int p0, int np, unsigned long long* d_out, 
   if (maxn <= 0) return IPLS_OK;
   void* dtab = nullptr;
   if (int rc = upload_table(h, dd.data(), dd.size() * sizeof(DivDesc), &dtab)) return rc;
-  const int64_t tile = (int64_t)kBlock * 8;
+  const int64_t tile = kDivTile;
   const int tpp = (int)((maxn + tile - 1) / tile);
   const dim3 g((unsigned)tpp * np);
 #define DIV(B, S) hipLaunchKernelGGL((k_divide<B, S>), g, dim3(kBlock), 0, h->stream, (const DivDesc*)dtab, (const double*)h->arena, d_out, tpp)
