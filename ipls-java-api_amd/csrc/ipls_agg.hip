@@ -297,13 +297,21 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   if (big_tpp * n_parts >= kBigMinBlocks) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
-    if constexpr (FIN)
-      hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, kBigMap, kBigBS, big_seqf<BE_IN, START>()>), grid,
-                         dim3(kBigBS), 0, st, bufs, parts,
-                         k, (int)big_tpp, n_parts, secure, cnts);
-    else
-      hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, kBigMap, kBigBS, big_seqf<BE_IN, START>()>),
-                         grid, dim3(kBigBS), 0, st, bufs, parts, k, (int)big_tpp, n_parts);
+    // partial last tiles are scheduled first (map 3, ipls_kernels.hpp map_block)
+    const bool partial = big_tpp > 1 && maxL % big_tile != 0;
+#define BIG(MAP)                                                                                          \
+    do {                                                                                                  \
+      if constexpr (FIN)                                                                                  \
+        hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, MAP, kBigBS, big_seqf<BE_IN, START>()>), grid, \
+                           dim3(kBigBS), 0, st, bufs, parts, k, (int)big_tpp, n_parts, secure, cnts);     \
+      else                                                                                                \
+        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, MAP, kBigBS,                   \
+                                     big_seqf<BE_IN, START>()>),                                          \
+                           grid, dim3(kBigBS), 0, st, bufs, parts, k, (int)big_tpp, n_parts);             \
+    } while (0)
+    if (partial) BIG(3);
+    else BIG(kBigMap);
+#undef BIG
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
     const int64_t tpp = (maxL + tile - 1) / tile;

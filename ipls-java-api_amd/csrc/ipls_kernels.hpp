@@ -116,8 +116,25 @@ __host__ __device__ constexpr int64_t grid_blocks(int map, int64_t tiles) {
   return map == 2 ? (tiles + 7) / 8 * 8 : tiles;
 }
 
+//            3 = partial tiles first: blocks [0, n_parts) take the last tile of
+//                each partition (partial when L is not a multiple of the tile),
+//                the rest the full tiles partition-major.  With 1 workgroup per
+//                CU the short partial blocks then run beside the first round of
+//                full tiles instead of pushing full tiles into an extra round
+//                (L = 4194305: 2064 blocks = 8 rounds + 15 full tiles alone).
 __device__ __forceinline__ void map_block(int map, int nblocks, int tiles_per_part, int n_parts, int& q, int& t) {
   int b = blockIdx.x;
+  if (map == 3) {
+    if (b < n_parts) {
+      q = b;
+      t = tiles_per_part - 1;
+    } else {
+      b -= n_parts;
+      q = b / (tiles_per_part - 1);
+      t = b - q * (tiles_per_part - 1);
+    }
+    return;
+  }
   if (map == 2) {
     const int per = nblocks >> 3;  // nblocks % 8 == 0 (grid_blocks)
     b = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -283,7 +300,8 @@ __device__ __forceinline__ void reduce_tiles(
       for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
     }
   } else {
-    // ------- partial last tile: 512-element vector steps, scalar remainder -------
+    // ------- partial last tile: 2*BS-element vector steps, scalar remainder -------
+    constexpr int kPB = 8;
     for (int64_t sb = base; sb < L; sb += 2 * kBlock) {
       const int64_t i = sb + 2 * tid;
       if (sb + 2 * kBlock <= L) {
@@ -291,7 +309,22 @@ __device__ __forceinline__ void reduce_tiles(
         if constexpr (START == kZero) acc = d2{0.0, 0.0};
         else if constexpr (START == kFirst) acc = decode2<BE_IN>(ld16<NT>(pb[0] + i));
         else acc = decode2<BE_OUT>(ld16<false>(init + i));
-        for (int jj = j0; jj < k; ++jj) {
+        // peers in groups of kPB loads in flight (the fold order is unchanged):
+        // a one-at-a-time chain of k dependent loads made this block take longer
+        // than a full tile
+        int jj = j0;
+        for (; jj + kPB <= k; jj += kPB) {
+          u2 v[kPB];
+#pragma unroll
+          for (int g = 0; g < kPB; ++g) v[g] = ld16<NT>(pb[jj + g] + i);
+#pragma unroll
+          for (int g = 0; g < kPB; ++g) {
+            const d2 x = decode2<BE_IN>(v[g]);
+            acc.x = acc.x + x.x;
+            acc.y = acc.y + x.y;
+          }
+        }
+        for (; jj < k; ++jj) {
           const d2 x = decode2<BE_IN>(ld16<NT>(pb[jj] + i));
           acc.x = acc.x + x.x;
           acc.y = acc.y + x.y;
@@ -308,7 +341,15 @@ __device__ __forceinline__ void reduce_tiles(
           if constexpr (START == kZero) acc = 0.0;
           else if constexpr (START == kFirst) acc = decode1<BE_IN>(ld8(pb[0] + e));
           else acc = decode1<BE_OUT>(ld8(init + e));
-          for (int jj = j0; jj < k; ++jj) acc = acc + decode1<BE_IN>(ld8(pb[jj] + e));
+          int jj = j0;
+          for (; jj + kPB <= k; jj += kPB) {
+            unsigned long long v[kPB];
+#pragma unroll
+            for (int g = 0; g < kPB; ++g) v[g] = ld8(pb[jj + g] + e);
+#pragma unroll
+            for (int g = 0; g < kPB; ++g) acc = acc + decode1<BE_IN>(v[g]);
+          }
+          for (; jj < k; ++jj) acc = acc + decode1<BE_IN>(ld8(pb[jj] + e));
           if constexpr (FIN) fin1(e, acc);
           else st8(dst + e, BE_OUT ? f64_to_be(acc) : __builtin_bit_cast(unsigned long long, acc));
         }

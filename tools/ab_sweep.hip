@@ -1,0 +1,107 @@
+// ab_sweep.hip -- dev tool: same-process A/B of the shipped k_reduce against a
+// previous revision of ipls_kernels.hpp (built from git into namespace
+// ipls_old by tools/ab_build.sh), interleaved round-robin so both see the same
+// bucket layout (layout moves results by +-5 % across processes).
+//
+// Usage: ab_sweep P L K PAD REPS
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../ipls-java-api_amd/csrc/ipls_kernels.hpp"
+#include AB_OLD_HEADER
+
+#define CK(x)                                                                               \
+  do {                                                                                      \
+    hipError_t e = (x);                                                                     \
+    if (e != hipSuccess) {                                                                  \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));      \
+      exit(1);                                                                              \
+    }                                                                                       \
+  } while (0)
+
+struct Var {
+  std::string name;
+  std::function<void(hipStream_t)> run;
+  std::vector<float> ms;
+};
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 16;
+  const int64_t L = argc > 2 ? atoll(argv[2]) : 4194304;
+  const int K = argc > 3 ? atoi(argv[3]) : 32;
+  const int64_t PAD = argc > 4 ? atoll(argv[4]) : 32;
+  const int REPS = argc > 5 ? atoi(argv[5]) : 10;
+  const int64_t stride = L + PAD;
+  unsigned long long* arena;
+  CK(hipMalloc(&arena, (size_t)P * K * stride * 8 + 4096));
+  auto* base = (unsigned long long*)(((uintptr_t)arena + 255) / 256 * 256);
+  std::vector<const unsigned long long*> ptrs(P * K);
+  for (int p = 0; p < P; ++p)
+    for (int k = 0; k < K; ++k) {
+      unsigned long long* b = base + (int64_t)(p * K + k) * stride;
+      ptrs[p * K + k] = b;
+      const unsigned long long key = 0x1B52026ULL ^ ((unsigned long long)p << 40) ^ ((unsigned long long)k << 32);
+      hipLaunchKernelGGL(ipls::k_synth<false>, dim3(4096), dim3(ipls::kBlock), 0, 0, b, L, key);
+    }
+  const unsigned long long** d_ptrs;
+  CK(hipMalloc(&d_ptrs, ptrs.size() * 8));
+  CK(hipMemcpy(d_ptrs, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice));
+  const int64_t dl = (L + 31) / 32 * 32;
+  unsigned long long* dst;
+  CK(hipMalloc(&dst, (size_t)P * dl * 8));
+  std::vector<ipls::PartDesc> pd(P);
+  for (int p = 0; p < P; ++p) pd[p] = ipls::PartDesc{L, dst + p * dl, nullptr, nullptr, nullptr};
+  ipls::PartDesc* d_pd;
+  CK(hipMalloc(&d_pd, P * sizeof(ipls::PartDesc)));
+  CK(hipMemcpy(d_pd, pd.data(), P * sizeof(ipls::PartDesc), hipMemcpyHostToDevice));
+  CK(hipDeviceSynchronize());
+  const double alg = (double)P * (K + 1) * L * 8;
+  const int64_t tile = 1024 * 2 * 16;
+  const int tpp = (int)((L + tile - 1) / tile);
+  auto bp = (const unsigned long long* const*)d_ptrs;
+  auto opd = (const ipls_old::PartDesc*)d_pd;
+  std::vector<Var> vars;
+  vars.push_back({"old k_reduce f64 R=16 MAP=0", [=](hipStream_t s) {
+                    hipLaunchKernelGGL((ipls_old::k_reduce<false, false, ipls_old::kZero, 1, 16, true, 0, 1024>),
+                                       dim3(tpp * P), dim3(1024), 0, s, bp, opd, K, tpp, P);
+                  }});
+  vars.push_back({"new k_reduce f64 R=16 MAP=0", [=](hipStream_t s) {
+                    hipLaunchKernelGGL((ipls::k_reduce<false, false, ipls::kZero, 1, 16, true, 0, 1024>),
+                                       dim3(tpp * P), dim3(1024), 0, s, bp, d_pd, K, tpp, P);
+                  }});
+  if (L % tile)
+    vars.push_back({"new k_reduce f64 R=16 MAP=3 (partial tiles first)", [=](hipStream_t s) {
+                      hipLaunchKernelGGL((ipls::k_reduce<false, false, ipls::kZero, 1, 16, true, 3, 1024>),
+                                         dim3(tpp * P), dim3(1024), 0, s, bp, d_pd, K, tpp, P);
+                    }});
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& v : vars) v.run(0);
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < REPS; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(e0, 0));
+      v.run(0);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms);
+    }
+  printf("# P=%d L=%lld K=%d PAD=%lld REPS=%d  algorithmic bytes/launch=%.0f\n", P, (long long)L, K, (long long)PAD,
+         REPS, alg);
+  for (auto& v : vars) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2];
+    printf("%-52s median %8.4f ms  min %8.4f ms  %5.1f%% of 8 TB/s\n", v.name.c_str(), med, v.ms[0],
+           alg / med / 1e6 / 80.0);
+  }
+  return 0;
+}

@@ -12,8 +12,9 @@ sys.path[:0] = [str(ROOT), str(ROOT / "ipls-java-api_amd")]
 import ipls  # noqa: E402
 
 
-def run(P, L, K, reps=10):
-    elem = (L + 1) // 2 * 2 + 32      # keep every bucket 16-B aligned
+def run(P, L, K, reps=10, align=16):
+    a = align // 8
+    elem = (L + a - 1) // a * a + 32  # every bucket `align`-B aligned
     arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
     base = (int(arena.data_ptr()) + 255) // 256 * 256
     rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L) for k in range(K)] for q in range(P)]
@@ -47,5 +48,5 @@ def run(P, L, K, reps=10):
 
 
 if __name__ == "__main__":
-    for L in (4194304, 4194305):
-        print(f"P=16 L={L} K=32", run(16, L, 32), flush=True)
+    for L, align in ((4194304, 16), (4194305, 16), (4194305, 256), (4194306, 16)):
+        print(f"P=16 L={L} K=32 bucket alignment {align} B", run(16, L, 32, align=align), flush=True)
