@@ -130,6 +130,12 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jcla
     CHECK(rc, H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartitionDirect(JNIEnv *env, jclass c, jlong h, jint p,
+                                                                       jobject sum) {
+    (void)c;
+    CHECK(ipls_agg_finalize(H(h), p, (*env)->GetDirectBufferAddress(env, sum), IPLS_HOST_BE, NULL), H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclass c, jlong h, jint p, jobject buf,
                                                                 jlong n) {
     (void)c;

@@ -76,3 +76,21 @@ def test_open_without_gpu_fails_loudly():
     with pytest.raises(ipls.IplsError) as e:
         ipls.Aggregator(443610, 3)
     assert e.value.java_name == "NoDevice"
+
+
+def test_jni_shim_matches_java_natives():
+    """No JDK here, so the JNI shim is not compiled; this keeps it consistent
+    with NativeAggregator.java (every native has its Java_NativeAggregator_*
+    function and no function is orphaned) and with include/ipls_agg.h (every
+    ipls_* it calls is declared)."""
+    import re
+    pkg = ROOT / "ipls-java-api_amd"
+    java = (pkg / "java" / "NativeAggregator.java").read_text()
+    jni = (pkg / "jni" / "ipls_jni.c").read_text()
+    natives = set(re.findall(r"\bnative\s+[\w\[\]<>.]+\s+(\w+)\s*\(", java))
+    exported = set(re.findall(r"JNICALL\s+Java_NativeAggregator_(\w+)\s*\(", jni))
+    assert natives and natives == exported, (natives ^ exported)
+    header = (ROOT / "include" / "ipls_agg.h").read_text()
+    declared = set(re.findall(r"\b(ipls_\w+)\s*\(", header))
+    called = set(re.findall(r"\b(ipls_\w+)\s*\(", jni))
+    assert called <= declared, called - declared

@@ -80,6 +80,37 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((ipls::k_reduce<false, false, ipls::kZero, 1, 16, true, 3, 1024>),
                                          dim3(tpp * P), dim3(1024), 0, s, bp, d_pd, K, tpp, P);
                     }});
+  // fused round (k_round, new kernels only): averages written at the real flat
+  // offsets p*(L-1) (mostly not 128-B aligned) vs at 256-B aligned offsets,
+  // vs no averages (SWEEP_ROUND=1)
+  std::vector<ipls::PartDesc> rpd[3];
+  ipls::PartDesc* d_rpd[3] = {nullptr, nullptr, nullptr};
+  double* d_cnt = nullptr;
+  unsigned long long* avg = nullptr;
+  if (getenv("SWEEP_ROUND")) {
+    CK(hipMalloc(&avg, (size_t)P * dl * 8 + 4096));
+    std::vector<double> cnt(P, (double)K);
+    CK(hipMalloc(&d_cnt, P * 8));
+    CK(hipMemcpy(d_cnt, cnt.data(), P * 8, hipMemcpyHostToDevice));
+    for (int v = 0; v < 3; ++v) {
+      rpd[v] = pd;
+      for (int p = 0; p < P; ++p) {
+        rpd[v][p].init = pd[p].dst;
+        rpd[v][p].avg = v == 0 ? avg + (int64_t)p * (L - 1) : v == 1 ? avg + p * dl : nullptr;
+      }
+      CK(hipMalloc(&d_rpd[v], P * sizeof(ipls::PartDesc)));
+      CK(hipMemcpy(d_rpd[v], rpd[v].data(), P * sizeof(ipls::PartDesc), hipMemcpyHostToDevice));
+    }
+    const char* names[3] = {"k_round, averages at p*(L-1) (real)", "k_round, averages 256-B aligned",
+                            "k_round, no averages"};
+    for (int v = 0; v < 3; ++v) {
+      ipls::PartDesc* dp = d_rpd[v];
+      vars.push_back({names[v], [=](hipStream_t s) {
+                        hipLaunchKernelGGL((ipls::k_round<false, ipls::kZero, 1, 16, 0, 1024>), dim3(tpp * P),
+                                           dim3(1024), 0, s, bp, dp, K, tpp, P, 0, d_cnt);
+                      }});
+    }
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
