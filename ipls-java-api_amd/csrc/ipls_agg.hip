@@ -1317,6 +1317,7 @@ int ipls_agg_get_partitions(ipls_agg* h, void* out, int64_t n, int out_kind) {
   HIP_TRY(h, hipSetDevice(h->device));
   unsigned long long* d_out;
   if (out_kind == IPLS_DEV_F64) {
+    if ((uintptr_t)out & 7) return fail(h, IPLS_E_INVAL, "device output not 8-byte aligned");
     d_out = (unsigned long long*)out;
   } else {
     if (int rc = ensure_scratch(h, (size_t)std::max<int64_t>(M, 1) * 8)) return rc;
@@ -1403,6 +1404,7 @@ int ipls_agg_aggregate_round(ipls_agg* h, int p_first, int n_parts, const void* 
   unsigned long long* d_avg = nullptr;
   if (avg_out && n_avg > 0) {
     if (avg_kind == IPLS_DEV_F64) {
+      if ((uintptr_t)avg_out & 7) return fail(h, IPLS_E_INVAL, "device output not 8-byte aligned");
       d_avg = (unsigned long long*)avg_out;
     } else {
       if (int rc = ensure_scratch(h, (size_t)n_avg * 8)) return rc;

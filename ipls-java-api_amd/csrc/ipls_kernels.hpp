@@ -568,9 +568,12 @@ __global__ __launch_bounds__(kBlock) void k_divide(const DivDesc* __restrict__ p
                                                    const double* __restrict__ arena,
                                                    unsigned long long* __restrict__ out,
                                                    int tiles_per_part) {
-  // W reads are 16-B aligned; the flat output offset p*chunk is arbitrary, so
-  // each lane stores the element pair that is aligned in the OUTPUT and reads
-  // its two W values with 8-B loads.
+  // The flat output offset p*chunk is arbitrary, so the tiles are laid over
+  // the OUTPUT: block 0 first writes the `head` elements up to the first 128-B
+  // line boundary of this partition's output, then every wave stores whole
+  // lines (64 lanes x 16 B = 8 lines), and each lane reads its two W values
+  // with 8-B loads (W's alignment relative to the output is arbitrary; reads
+  // of partial lines cost little, partial-line writes do).
   constexpr int kV = kDivV;
   constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
   const int q = blockIdx.x / tiles_per_part;
@@ -590,9 +593,11 @@ __global__ __launch_bounds__(kBlock) void k_divide(const DivDesc* __restrict__ p
     }
     return bits;
   };
-  const int64_t shift = (d.out_off & 1);         // first element whose output index is even
-  const int64_t base = (int64_t)t * kTile + shift;
-  if (t == 0 && shift && threadIdx.x == 0 && n > 0) out[d.out_off] = f(w[0]);
+  unsigned long long* o = out + d.out_off;
+  const int64_t to_line = (16 - (int64_t)(((uintptr_t)o >> 3) & 15)) & 15;   // elements to a 128-B boundary
+  const int64_t head = to_line < n ? to_line : n;
+  if (t == 0 && threadIdx.x < head) o[threadIdx.x] = f(w[threadIdx.x]);
+  const int64_t base = (int64_t)t * kTile + head;
   if (base >= n) return;
   if (base + kTile <= n) {
     double x[kV][2];
@@ -605,14 +610,14 @@ __global__ __launch_bounds__(kBlock) void k_divide(const DivDesc* __restrict__ p
 #pragma unroll
     for (int v = 0; v < kV; ++v) {
       const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
-      u2 o;
-      o.x = f(x[v][0]);
-      o.y = f(x[v][1]);
-      __builtin_nontemporal_store(o, (gu2)(out + d.out_off + i));
+      u2 v2;
+      v2.x = f(x[v][0]);
+      v2.y = f(x[v][1]);
+      __builtin_nontemporal_store(v2, (gu2)(o + i));
     }
     return;
   }
-  for (int64_t i = base + threadIdx.x; i < n; i += kBlock) out[d.out_off + i] = f(w[i]);
+  for (int64_t i = base + threadIdx.x; i < n; i += kBlock) o[i] = f(w[i]);
 }
 
 // ---------------------------------------------------------------------------
