@@ -311,6 +311,9 @@ def test_errors(ipls, O):
         agg.Update(np.zeros(100), 2)
     with pytest.raises(ipls.IplsError):
         agg.cache_partition(0, np.zeros(101))
+    t = torch.empty(2 * 100 + 2, dtype=torch.float64, device="cuda")
+    with pytest.raises(ipls.IplsError):   # device outputs must be 8-B aligned
+        agg.GetPartitions(out=ipls.DeviceBuffer(int(t.data_ptr()) + 4, 2 * 99))
     agg.Update(np.ones(100), 1)            # still usable after errors
     assert agg.read(1).sum() == 100.0
     agg.close()
