@@ -103,6 +103,13 @@ int main(int argc, char** argv) {
     }
     const char* names[3] = {"k_round, averages at p*(L-1) (real)", "k_round, averages 256-B aligned",
                             "k_round, no averages"};
+    {
+      auto odp = (const ipls_old::PartDesc*)d_rpd[0];
+      vars.push_back({"old k_round, averages at p*(L-1) (real)", [=](hipStream_t s) {
+                        hipLaunchKernelGGL((ipls_old::k_round<false, ipls_old::kZero, 1, 16, 0, 1024>), dim3(tpp * P),
+                                           dim3(1024), 0, s, bp, odp, K, tpp, P, 0, d_cnt);
+                      }});
+    }
     for (int v = 0; v < 3; ++v) {
       ipls::PartDesc* dp = d_rpd[v];
       vars.push_back({names[v], [=](hipStream_t s) {
