@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-passes", type=int, default=16,
                     help="CPU baseline sample: passes over one partition's K buckets")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="N=1: skip the config-B and config-D (BE in/out) lines measured after the headline")
     ap.add_argument("--no-replica-leg", action="store_true",
                     help="N>1: skip the cross-GPU replica exchange measurement (config E)")
     ap.add_argument("--replica-reps", type=int, default=5)
@@ -248,6 +250,55 @@ def replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, reps, verify,
         "note": "exchange_ms = export of the partials, one batched RCCL send/recv group, fold into REP "
                 "(max over ranks); round adds both folds and AggregatePartition",
     }
+
+
+def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, verify: bool = True) -> dict:
+    """One more BASELINE config on the same box, N=1: B
+    (16 x 1M x 8, native doubles) or D (64 x 4M x 32) with big-endian IPFS
+    bytes in and the sum packed to big-endian bytes out, i.e. config D's
+    'double<->byte pack/unpack in the timed region'.  Same algorithmic-bytes
+    accounting as the headline; kernel time by HIP events on the handle's
+    stream; partition 0 checked against the oracle's checksum."""
+    P, L, K = CONFIGS[name]
+    elem = L + 32
+    arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
+    base = (int(arena.data_ptr()) + 255) // 256 * 256
+    rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L, big_endian=be) for k in range(K)] for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[q][k], q, k, ipls.SEED)
+    out_arena = torch.empty(P * elem + 32, dtype=torch.float64, device="cuda")
+    obase = (int(out_arena.data_ptr()) + 255) // 256 * 256
+    dsts = [obase + 8 * q * elem for q in range(P)]
+    torch.cuda.synchronize()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=device)
+    stream = torch.cuda.ExternalStream(agg.stream, device=torch.device("cuda", device))
+
+    def step():
+        agg.reduce_batch_out(0, rows, dsts, start_mode=ipls.START_ZERO, big_endian_in=be, big_endian_out=be)
+    step()
+    step()
+    agg.sync()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    ev[0].record(stream)
+    for i in range(steps):
+        step()
+        ev[i + 1].record(stream)
+    agg.sync()
+    ms = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)]))
+    nbytes = P * (K + 1) * L * 8
+    verified = None
+    if verify:
+        from oracle import oracle as O   # checker only
+        verified = ipls.checksum_dev(ipls.DeviceBuffer(dsts[0], L, big_endian=be)) == O.c_synth_sum_checksum(L, 0, K)
+    agg.close()
+    del arena, out_arena, rows
+    torch.cuda.empty_cache()
+    return {"workload": f"{name}: {P} partitions x {L} doubles x {K} peers"
+                        + (" (BE IPFS bytes in, BE sum bytes out: fused unpack/pack)" if be else ""),
+            "kernel_ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
+            "frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes,
+            "verified_checksum_p0": verified}
 
 
 def pmc_traffic(workload_key: str):
@@ -447,6 +498,12 @@ def main():
             out["host_inclusive"] = host_inclusive(ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, K, args.cpu_passes)
+        if world == 1 and not args.no_other_configs and args.config == "C" and not args.be:
+            # the other single-GPU BASELINE configs, measured in the same run (never the value)
+            del arena, rows
+            torch.cuda.empty_cache()
+            out["other_configs"] = {nm: config_leg(ipls, torch, nm, be, local, verify=not args.no_verify)
+                                    for nm, be in (("B", False), ("D", True))}
     if world > 1 and not args.no_replica_leg and not args.be:
         # the cross-GPU exchange is an extra measurement: a watchdog makes sure
         # a stuck exchange can never cost the main line (every rank exits)
