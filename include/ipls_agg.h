@@ -212,7 +212,10 @@ int ipls_agg_reduce_batch_out(ipls_agg *h, int p_first, int n_parts,
  * as the Java receiver drops it after printing the exception:
  * status[i] = 0 folded, 1 null gradient (n == 0, no fold), IPLS_E_FORMAT
  * (bad base64 / short frame), IPLS_E_RANGE (partition out of range or
- * payload shorter than L_p).  Returns the number of messages folded. */
+ * payload shorter than L_p).  Returns the number of messages folded.
+ * The texts are copied by IPLS_INGEST_COPY_THREADS (default 2) short-lived
+ * host threads, each on its own stream, while the device decodes the texts
+ * that have already landed; msgs must stay valid until the call returns. */
 int ipls_agg_ingest_pubsub(ipls_agg *h, int target, const uint8_t *const *msgs,
                            const int64_t *lens, int n_msgs, int layers,
                            const int32_t *parts, int32_t *status);

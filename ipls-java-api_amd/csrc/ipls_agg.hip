@@ -12,13 +12,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ipls_agg.h"
@@ -81,6 +85,12 @@ struct ipls_agg {
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   hipEvent_t copy_ev = nullptr;
+  // pubsub ingest pipeline: text copies on their own stream, the decodes on
+  // `stream` behind an event per message (created on first use)
+  static constexpr int kCopyThreads = 4;
+  hipStream_t copy_stream[kCopyThreads] = {};
+  hipEvent_t ingest_ev = nullptr;
+  std::vector<hipEvent_t> msg_ev;
   // asynchronous folds of pinned host buckets: ticket t completes at fold_ev[t % kTickets]
   static constexpr int kTickets = 64;
   hipEvent_t fold_ev[kTickets] = {};
@@ -627,6 +637,13 @@ int ipls_agg_close(ipls_agg* h) {
     if (s.ev) hipEventDestroy(s.ev);
   }
   if (h->copy_ev) hipEventDestroy(h->copy_ev);
+  for (hipStream_t cs : h->copy_stream)
+    if (cs) {
+      hipStreamSynchronize(cs);
+      hipStreamDestroy(cs);
+    }
+  if (h->ingest_ev) hipEventDestroy(h->ingest_ev);
+  for (hipEvent_t e : h->msg_ev) hipEventDestroy(e);
   for (auto& e : h->fold_ev)
     if (e) hipEventDestroy(e);
   for (void* d : h->d_table)
@@ -1449,8 +1466,48 @@ int64_t b64_data_chars(const uint8_t* t, int64_t n) {
 
 int64_t b64_out_len(int64_t d) { return 3 * (d / 4) + (d % 4 == 2 ? 1 : d % 4 == 3 ? 2 : 0); }
 
+// Copy-issuing threads of the pubsub ingest (IPLS_INGEST_COPY_THREADS, 1..4).
+int ingest_copy_threads() {
+  static const int n = [] {
+    const char* e = std::getenv("IPLS_INGEST_COPY_THREADS");
+    const int v = e ? std::atoi(e) : 2;
+    return std::max(1, std::min(v, (int)ipls_agg::kCopyThreads));
+  }();
+  return n;
+}
+
+// Host decode of output bytes [lo, hi) of a base64url text with `d` data chars
+// (hi <= b64_out_len(d)), as Decoder.decode0 produces them.  false if a char
+// of the units touched is outside the alphabet; the device flags it too.
+bool b64_host_bytes(const uint8_t* t, int64_t d, int64_t lo, int64_t hi, uint8_t* out) {
+  bool ok = true;
+  for (int64_t u = lo / 3; 3 * u < hi; ++u) {
+    unsigned v = 0;
+    for (int c = 0; c < 4; ++c) {
+      const int64_t i = 4 * u + c;
+      if (i >= d) break;
+      const unsigned ch = t[i];
+      unsigned x = ch - 'A' < 26u ? ch - 'A' : ch - 'a' < 26u ? ch - 'a' + 26 : ch - '0' < 10u ? ch - '0' + 52
+                 : ch == '-' ? 62u : ch == '_' ? 63u : 0x100u;
+      if (x > 63) ok = false;
+      v |= (x & 63u) << (18 - 6 * c);
+    }
+    for (int b = 0; b < 3; ++b) {
+      const int64_t j = 3 * u + b;
+      if (j >= lo && j < hi) out[j - lo] = (uint8_t)(v >> (16 - 8 * b));
+    }
+  }
+  return ok;
+}
+
 }  // namespace
 
+// Pipeline: the host reads each text's ends (the '=' rules of both layers and
+// the 14-byte frame header need only the first 28 and last 8 chars), so no
+// device round trip sits between the copies and the decodes.  Texts go up on
+// copy_stream while `stream` decodes the previous ones behind a per-message
+// event; one sync reads the invalid-char flags, then each partition's frames
+// are folded in message order.
 int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
                            int layers, const int32_t* parts, int32_t* status) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
@@ -1460,116 +1517,151 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
   if (target_off(h, 0, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (n_msgs == 0) return 0;
   HIP_TRY(h, hipSetDevice(h->device));
-  std::vector<int32_t> st(n_msgs, 0);
-  std::vector<int64_t> cur_len(n_msgs), text_off(n_msgs), mid_off(n_msgs), frame_off(n_msgs);
-  // layout in scratch: [texts][layer-1 output][frames]; every region 256-B aligned per message
-  int64_t off = 0;
-  for (int i = 0; i < n_msgs; ++i) {
-    text_off[i] = off;
-    off = align_up(off + std::max<int64_t>(lens[i], 0) + 16, 256);
-  }
-  const int64_t text_total = off;
-  for (int i = 0; i < n_msgs; ++i) {
-    mid_off[i] = off;
-    off = align_up(off + lens[i] + 16, 256);
-  }
-  for (int i = 0; i < n_msgs; ++i) {     // frames start 2 bytes in: the payload (frame byte 14) is 16-B aligned
-    frame_off[i] = off + 2;
-    off = align_up(off + 2 + lens[i] + 16, 256);
-  }
-  if (int rc = ensure_scratch(h, (size_t)off + 64 * (size_t)n_msgs + 4096)) return rc;
-  unsigned char* base = (unsigned char*)h->d_scratch;
-  int* d_err = (int*)(base + off);
-  HIP_TRY(h, hipMemsetAsync(d_err, 0, sizeof(int) * n_msgs, h->stream));
-  for (int i = 0; i < n_msgs; ++i)
-    if (lens[i] > 0) HIP_TRY(h, hipMemcpyAsync(base + text_off[i], msgs[i], lens[i], hipMemcpyHostToDevice, h->stream));
-  (void)text_total;
 
-  // host-side tail rules for the layer we can see (the caller's text)
-  std::vector<B64Desc> desc(n_msgs);
-  std::vector<int64_t> out_len(n_msgs, 0);
-  auto decode_layer = [&](const std::vector<int64_t>& src_off, const std::vector<int64_t>& dst_off,
-                          const std::vector<int64_t>& data_chars) -> int {
-    int64_t max_units = 0;
+  // 1. host: tail rules, frame header, routing (GET_GRADIENTS, MyIPFSClass.java:1437-1459).
+  //    post[i] = the status if the device finds no invalid char; decode[i] = needs the device.
+  std::vector<int32_t> st(n_msgs, 0), post(n_msgs, 0), route(n_msgs, -1);
+  std::vector<int64_t> dc(n_msgs, 0), dc2(n_msgs, 0);
+  std::vector<uint8_t> decode(n_msgs, 0);
+  for (int i = 0; i < n_msgs; ++i) {
+    const int64_t d = lens[i] >= 0 ? b64_data_chars(msgs[i], lens[i]) : -1;
+    if (d < 0) { st[i] = IPLS_E_FORMAT; continue; }
+    dc[i] = d;
+    bool ok = true;
+    int64_t fl = 0;   // frame length
+    uint8_t hdr[14];
+    if (layers == 2) {
+      const int64_t n = b64_out_len(d), k = std::min<int64_t>(4, n);
+      uint8_t tail[4];
+      ok = b64_host_bytes(msgs[i], d, n - k, n, tail);
+      const int64_t t = ok ? b64_data_chars(tail, k) : -1;
+      if (t < 0 || (n - k + t) % 4 == 1) { st[i] = IPLS_E_FORMAT; continue; }
+      dc2[i] = n - k + t;
+      fl = b64_out_len(dc2[i]);
+      if (fl >= 14) {
+        uint8_t mid[20];
+        const int64_t c = std::min<int64_t>(dc2[i], 20);   // 20 inner chars -> frame bytes 0..14
+        ok = b64_host_bytes(msgs[i], d, 0, c, mid) && b64_host_bytes(mid, c, 0, 14, hdr);
+      }
+    } else {
+      dc2[i] = d;
+      fl = b64_out_len(d);
+      if (fl >= 14) ok = b64_host_bytes(msgs[i], d, 0, 14, hdr);
+    }
+    if (!ok) { st[i] = IPLS_E_FORMAT; continue; }
+    // [i16 pid][i32 n][i32 partition][i32 iteration] -- n against the real frame length
+    const int32_t n = fl >= 14 ? (int32_t)rd_be32_host(&hdr[2]) : 0;
+    if (fl < 14 || n < 0 || 14 + 8 * (int64_t)n > fl) { st[i] = IPLS_E_FORMAT; continue; }
+    decode[i] = 1;
+    if (n == 0) { post[i] = 1; continue; }          // arr_len == 0 -> null gradient: no fold
+    const int p = parts ? parts[i] : (int32_t)rd_be32_host(&hdr[6]);
+    if (p < 0 || p >= h->P || n < h->len[p]) { post[i] = IPLS_E_RANGE; continue; }
+    route[i] = p;
+  }
+
+  // 2. device: scratch [texts][layer-1 output][frames], 256-B aligned per message;
+  //    frames start 2 bytes in so the payload (frame byte 14) is 16-B aligned.
+  std::vector<int64_t> text_off(n_msgs, 0), mid_off(n_msgs, 0), frame_off(n_msgs, 0);
+  int64_t off = 0;
+  for (int i = 0; i < n_msgs; ++i)
+    if (decode[i]) { text_off[i] = off; off = align_up(off + lens[i] + 16, 256); }
+  if (layers == 2)
+    for (int i = 0; i < n_msgs; ++i)
+      if (decode[i]) { mid_off[i] = off; off = align_up(off + lens[i] + 16, 256); }
+  for (int i = 0; i < n_msgs; ++i)
+    if (decode[i]) { frame_off[i] = off + 2; off = align_up(off + 2 + lens[i] + 16, 256); }
+  int n_dec = 0;
+  for (int i = 0; i < n_msgs; ++i) n_dec += decode[i];
+  if (n_dec) {
+    if (int rc = ensure_scratch(h, (size_t)off + 64 * (size_t)n_msgs + 4096)) return rc;
+    unsigned char* base = (unsigned char*)h->d_scratch;
+    int* d_err = (int*)(base + off);
+    std::vector<B64Desc> desc(2 * (size_t)n_msgs);
     for (int i = 0; i < n_msgs; ++i) {
-      const int64_t d = st[i] ? 0 : data_chars[i];
-      desc[i] = B64Desc{src_off[i], d / 4, dst_off[i], (int32_t)(d % 4), 0};
-      out_len[i] = st[i] ? 0 : b64_out_len(d);
-      max_units = std::max(max_units, d / 4);
+      if (!decode[i]) continue;
+      desc[i] = B64Desc{text_off[i], dc[i] / 4, layers == 2 ? mid_off[i] : frame_off[i], (int32_t)(dc[i] % 4), 0};
+      desc[n_msgs + i] = B64Desc{mid_off[i], dc2[i] / 4, frame_off[i], (int32_t)(dc2[i] % 4), 0};
     }
     void* dtab = nullptr;
-    if (int rc = upload_table(h, desc.data(), sizeof(B64Desc) * n_msgs, &dtab)) return rc;
-    const dim3 grid(blocks_for(max_units / 4 + 1, kBlock), (unsigned)n_msgs);
-    hipLaunchKernelGGL(k_b64url_decode, grid, dim3(kBlock), 0, h->stream, (const unsigned char*)base,
-                       (const B64Desc*)dtab, base, d_err);
-    HIP_TRY(h, hipGetLastError());
-    return IPLS_OK;
-  };
-  std::vector<int64_t> dc(n_msgs);
-  for (int i = 0; i < n_msgs; ++i) {
-    dc[i] = lens[i] >= 0 ? b64_data_chars(msgs[i], lens[i]) : -1;
-    if (dc[i] < 0) st[i] = IPLS_E_FORMAT;
-  }
-  std::vector<int> herr(n_msgs);
-  if (layers == 2) {
-    if (int rc = decode_layer(text_off, mid_off, dc)) return rc;
-    // the inner text's tail is on the device: fetch its last 4 chars
-    std::vector<unsigned char> tails(4 * (size_t)n_msgs, 'A');
-    for (int i = 0; i < n_msgs; ++i) {
-      const int64_t n = out_len[i];
-      if (st[i] || n == 0) continue;
-      const int64_t k = std::min<int64_t>(4, n);
-      HIP_TRY(h, hipMemcpyAsync(&tails[4 * i + (4 - k)], base + mid_off[i] + n - k, k, hipMemcpyDeviceToHost,
-                                h->stream));
+    if (int rc = upload_table(h, desc.data(), sizeof(B64Desc) * desc.size(), &dtab)) return rc;
+    const B64Desc* d1 = (const B64Desc*)dtab;
+    HIP_TRY(h, hipMemsetAsync(d_err, 0, sizeof(int) * n_msgs, h->stream));
+    // Texts are pageable: each hipMemcpyAsync blocks its calling thread and
+    // pays ~45 us of setup between transfers, so T threads issue the copies
+    // (message j of the batch on thread j % T, its own stream) and this thread
+    // queues each message's decodes behind that copy's event as it lands.
+    const int T = std::max(1, std::min(ingest_copy_threads(), n_dec));
+    for (int t = 0; t < T; ++t)
+      if (!h->copy_stream[t]) HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream[t], hipStreamNonBlocking));
+    if (!h->ingest_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->ingest_ev, hipEventDisableTiming));
+    while ((int)h->msg_ev.size() < n_msgs) {
+      hipEvent_t e;
+      HIP_TRY(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      h->msg_ev.push_back(e);
     }
+    // the scratch may still be read by earlier work on `stream`
+    HIP_TRY(h, hipEventRecord(h->ingest_ev, h->stream));
+    for (int t = 0; t < T; ++t) HIP_TRY(h, hipStreamWaitEvent(h->copy_stream[t], h->ingest_ev, 0));
+    std::vector<int> order;
+    for (int i = 0; i < n_msgs; ++i)
+      if (decode[i]) order.push_back(i);
+    std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[n_dec]);   // 0 pending, 1 recorded, <0 error
+    for (int j = 0; j < n_dec; ++j) ready[j].store(0);
+    auto copier = [&](int t) {
+      hipSetDevice(h->device);
+      for (int j = t; j < n_dec; j += T) {
+        const int i = order[j];
+        hipError_t e = hipMemcpyAsync(base + text_off[i], msgs[i], lens[i], hipMemcpyHostToDevice, h->copy_stream[t]);
+        if (e == hipSuccess) e = hipEventRecord(h->msg_ev[i], h->copy_stream[t]);
+        ready[j].store(e == hipSuccess ? 1 : -(int)e, std::memory_order_release);
+        if (e != hipSuccess) {
+          for (int r = j + T; r < n_dec; r += T) ready[r].store(-(int)e, std::memory_order_release);
+          return;
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(copier, t);
+    if (T == 1) copier(0);
+    else pool.emplace_back(copier, 0);
+    int copy_err = 0;
+    for (int j = 0; j < n_dec && !copy_err; ++j) {
+      int r;
+      while ((r = ready[j].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+      if (r < 0) { copy_err = -r; break; }
+      const int i = order[j];
+      hipStreamWaitEvent(h->stream, h->msg_ev[i], 0);
+      hipLaunchKernelGGL(k_b64url_decode, dim3(blocks_for(dc[i] / 16 + 1, kBlock)), dim3(kBlock), 0, h->stream,
+                         (const unsigned char*)base, d1 + i, base, d_err + i);
+      if (layers == 2)
+        hipLaunchKernelGGL(k_b64url_decode, dim3(blocks_for(dc2[i] / 16 + 1, kBlock)), dim3(kBlock), 0, h->stream,
+                           (const unsigned char*)base, d1 + n_msgs + i, base, d_err + i);
+    }
+    for (auto& th : pool) th.join();
+    if (copy_err) return fail(h, IPLS_E_DEVICE, "pubsub text copy failed: %s", hipGetErrorString((hipError_t)copy_err));
+    HIP_TRY(h, hipGetLastError());
+    std::vector<int> herr(n_msgs, 0);
     HIP_TRY(h, hipMemcpyAsync(herr.data(), d_err, sizeof(int) * n_msgs, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
-    std::vector<int64_t> dc2(n_msgs, 0);
-    for (int i = 0; i < n_msgs; ++i) {
-      if (st[i]) continue;
-      if (herr[i]) { st[i] = IPLS_E_FORMAT; continue; }
-      const int64_t n = out_len[i];
-      // only the last (up to 4) chars matter for the '=' rules
-      const int64_t k = std::min<int64_t>(4, n);
-      int64_t d = b64_data_chars(&tails[4 * i + (4 - k)], k);
-      if (d < 0) { st[i] = IPLS_E_FORMAT; continue; }
-      dc2[i] = n - k + d;
-      if (dc2[i] % 4 == 1) st[i] = IPLS_E_FORMAT;
+    for (int i = 0; i < n_msgs; ++i)
+      if (decode[i]) st[i] = herr[i] ? IPLS_E_FORMAT : post[i];
+    // 3. fold each partition's frames in message order
+    std::vector<std::vector<const void*>> per_part(h->P);
+    for (int i = 0; i < n_msgs; ++i)
+      if (decode[i] && st[i] == 0) per_part[route[i]].push_back(base + frame_off[i] + 14);
+    int folded = 0;
+    for (int p = 0; p < h->P; ++p) {
+      if (per_part[p].empty()) continue;
+      if (int rc = reduce_dev(h, p, 1, per_part[p].data(), (int)per_part[p].size(), true, IPLS_START_ACCUM, target))
+        return rc;
+      folded += (int)per_part[p].size();
     }
-    if (int rc = decode_layer(mid_off, frame_off, dc2)) return rc;
-  } else {
-    if (int rc = decode_layer(text_off, frame_off, dc)) return rc;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (status) std::memcpy(status, st.data(), sizeof(int32_t) * n_msgs);
+    return folded;
   }
-  // frame headers (14 bytes) + error flags back to the host
-  std::vector<uint8_t> hdr(16 * (size_t)n_msgs, 0);
-  for (int i = 0; i < n_msgs; ++i)
-    if (!st[i] && out_len[i] >= 14)
-      HIP_TRY(h, hipMemcpyAsync(&hdr[16 * i], base + frame_off[i], 14, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(h, hipMemcpyAsync(herr.data(), d_err, sizeof(int) * n_msgs, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
-  // route + validate (GET_GRADIENTS, MyIPFSClass.java:1437-1459)
-  std::vector<std::vector<const void*>> per_part(h->P);
-  for (int i = 0; i < n_msgs; ++i) {
-    if (st[i]) continue;
-    if (herr[i]) { st[i] = IPLS_E_FORMAT; continue; }
-    // [i16 pid][i32 n][i32 partition][i32 iteration] -- n against the real frame length
-    const int32_t n = (int32_t)rd_be32_host(&hdr[16 * i + 2]);
-    if (out_len[i] < 14 || n < 0 || 14 + 8 * (int64_t)n > out_len[i]) { st[i] = IPLS_E_FORMAT; continue; }
-    if (n == 0) { st[i] = 1; continue; }          // arr_len == 0 -> null gradient: no fold
-    const int p = parts ? parts[i] : (int32_t)rd_be32_host(&hdr[16 * i + 6]);
-    if (p < 0 || p >= h->P || n < h->len[p]) { st[i] = IPLS_E_RANGE; continue; }
-    per_part[p].push_back(base + frame_off[i] + 14);
-  }
-  int folded = 0;
-  for (int p = 0; p < h->P; ++p) {
-    if (per_part[p].empty()) continue;
-    if (int rc = reduce_dev(h, p, 1, per_part[p].data(), (int)per_part[p].size(), true, IPLS_START_ACCUM, target))
-      return rc;
-    folded += (int)per_part[p].size();
-  }
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
   if (status) std::memcpy(status, st.data(), sizeof(int32_t) * n_msgs);
-  return folded;
+  return 0;
 }
 
 int ipls_agg_blend(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind, double a, double b) {

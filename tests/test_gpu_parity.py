@@ -610,6 +610,82 @@ def test_ingest_pubsub_errors_dropped(ipls, O):
     agg.close()
 
 
+def _ingest_expected(O, m, layers, P, lengths, part=None):
+    """Status the ingest must report for one text, from the oracle's Java
+    restatement: -6 IllegalArgument/BufferUnderflow, 1 null gradient, -2 out
+    of range (GET_GRADIENTS, MyIPFSClass.java:1437-1459), 0 folded."""
+    try:
+        fr = O.pubsub_decode(m) if layers == 2 else O.java_b64url_decode(m)
+        pid, nn, a, b, gg, origin = O.frame_decode(fr)
+    except ValueError:
+        return -6, None
+    if gg is None:
+        return 1, None
+    p = a if part is None else part
+    if not 0 <= p < P or nn < lengths[p]:
+        return -2, None
+    return 0, (p, gg)
+
+
+@pytest.mark.parametrize("layers", [1, 2])
+def test_ingest_pubsub_mutations(ipls, O, layers):
+    """Every status the pipelined ingest reports (host-read text ends, device-
+    checked bodies) against the oracle: invalid chars in the header, body or
+    tail of either base64 layer, '=' in the middle, truncations, wrong
+    partition or n, and combinations (an invalid body char beats a bad route)."""
+    rng = np.random.default_rng(11 + layers)
+    M, P = 9001, 3
+    agg = ipls.Aggregator(M, P)
+    L = agg.lengths
+    enc = (lambda fr: O.pubsub_message(fr)) if layers == 2 else (lambda fr: O.java_b64url_encode(fr))
+    bad_chars = b"+/=*\n.\x80 "
+    msgs = []
+    for t in range(120):
+        p = int(rng.integers(0, P))
+        g = O.synth_bucket(int(L[p]) + int(rng.integers(0, 3)), 4, t)
+        fr = bytearray(O.frame_encode(g, p, 3, 3, b"QmM%d" % t))
+        kind = t % 10
+        if kind == 1:                                  # wrong partition field
+            fr[6:10] = int(rng.choice([P, 7, -1])).to_bytes(4, "big", signed=True)
+        elif kind == 2:                                # n too big / negative / short
+            fr[2:6] = int(rng.choice([len(g) + 5, -3, 10])).to_bytes(4, "big", signed=True)
+        elif kind == 3:
+            fr = fr[:int(rng.integers(0, 40))]         # truncated frame (header cut too)
+        elif kind == 4:
+            fr[2:6] = (0).to_bytes(4, "big")           # null gradient
+        m = bytearray(enc(bytes(fr)))
+        if kind in (5, 6, 7) and len(m) > 4:
+            # one bad char in the outer text: first 28 chars (header), body, last 8 (tail)
+            pos = {5: int(rng.integers(0, min(28, len(m)))),
+                   6: int(rng.integers(0, len(m))),
+                   7: max(0, len(m) - 1 - int(rng.integers(0, 8)))}[kind]
+            m[pos] = bad_chars[int(rng.integers(0, len(bad_chars)))]
+        elif kind == 8 and layers == 2:                # bad char in the inner text, re-encoded
+            inner = bytearray(O.java_b64url_encode(bytes(fr)))
+            pos = int(rng.choice([0, 5, 19, len(inner) // 2, len(inner) - 1, len(inner) - 3]))
+            inner[pos] = bad_chars[int(rng.integers(0, len(bad_chars)))]
+            m = bytearray(O.java_b64url_encode(bytes(inner)))
+        elif kind == 9:
+            m = m[:len(m) - int(rng.integers(1, 6))]   # truncated text
+            if t % 20 == 9:
+                m[len(m) // 2] = ord("+")               # and a bad body char
+        if t % 7 == 0:
+            m = m.rstrip(b"=")                          # Java accepts unpadded text
+        if t % 11 == 0 and kind == 1 and len(m) > 40:
+            m[len(m) // 2] = ord("*")                   # bad route AND bad body char -> -6
+        msgs.append(bytes(m))
+    exp = [_ingest_expected(O, m, layers, P, L) for m in msgs]
+    n, st = agg.ingest_pubsub(msgs, layers=layers)
+    assert st == [e[0] for e in exp]
+    assert n == sum(1 for e in exp if e[0] == 0)
+    assert len(set(st)) >= 4, st
+    for p in range(P):
+        gs = [e[1][1] for e in exp if e[0] == 0 and e[1][0] == p]
+        assert gs, p
+        assert_bits_equal(agg.read(p), O.reduce(gs, L[p]), f"p{p}")
+    agg.close()
+
+
 def test_ingest_pubsub_single_layer_large(ipls, O):
     """One base64 layer (Marshall_Packet text as published), 1M-double
     payloads (vector decode path), replica frames routed by caller partitions."""
