@@ -504,13 +504,16 @@ def main():
             torch.cuda.empty_cache()
             out["other_configs"] = {nm: config_leg(ipls, torch, nm, be, local, verify=not args.no_verify)
                                     for nm, be in (("B", False), ("D", True))}
+    dog = None
+    printed = []
     if world > 1 and not args.no_replica_leg and not args.be:
         # the cross-GPU exchange is an extra measurement: a watchdog makes sure
-        # a stuck exchange can never cost the main line (every rank exits)
+        # a stuck exchange (or a teardown stuck behind a peer that failed in
+        # it) can never cost the main line -- every rank exits
         import threading
 
         def expire():
-            if out is not None:
+            if out is not None and not printed:
                 out["replica_exchange"] = {"error": f"timed out after {args.replica_timeout} s"}
                 print(json.dumps(out), flush=True)
             os._exit(0)
@@ -522,14 +525,16 @@ def main():
                                    not args.no_verify, args.dist_backend)
         except Exception as e:                       # reported, never fatal to the main line
             leg = {"error": f"{type(e).__name__}: {e}"}
-        dog.cancel()
         if out is not None:
             out["replica_exchange"] = leg
     if out is not None:
+        printed.append(True)
         print(json.dumps(out), flush=True)
     agg.close()
     if world > 1:
         dist.destroy_process_group()
+    if dog is not None:
+        dog.cancel()
 
 
 if __name__ == "__main__":
