@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="N=1: skip the config-B and config-D (BE in/out) lines measured after the headline")
+    ap.add_argument("--no-per-arrival", action="store_true",
+                    help="N=1: skip the per-arrival (one call per bucket) leg measured after the headline")
     ap.add_argument("--no-replica-leg", action="store_true",
                     help="N>1: skip the cross-GPU replica exchange measurement (config E)")
     ap.add_argument("--replica-reps", type=int, default=5)
@@ -301,6 +303,49 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
             "verified_checksum_p0": verified}
 
 
+def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, verify: bool, reps: int = 3) -> dict:
+    """The headline workload folded the way Updater._Update folds its queue
+    (Updater.java:115-117): one call per arriving bucket, peers arriving in
+    turn (peer 0's P buckets, then peer 1's ...).  'each' is one fold launch
+    per arrival (ipls_agg_accumulate: 24 B of HBM traffic per element);
+    'coalesced' queues the device buckets (ipls_agg_accumulate_async) and folds
+    them together when the queues fill.  Time = HIP events on the handle's
+    stream around the K*P calls, so it includes the host-side queueing; bytes
+    are the batch's algorithmic P*(K+1)*L*8.  Never the value."""
+    nbytes = P * (K + 1) * L * 8
+    out = {}
+    want = None
+    if verify:
+        from oracle import oracle as O   # checker only
+        want = O.c_synth_sum_checksum(L, 0, K)
+    for mode in ("each", "coalesced"):
+        best = None
+        for _ in range(reps):
+            agg.reset()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            t = 0
+            for k in range(K):
+                for q in range(P):
+                    if mode == "each":
+                        agg.Update(rows[q][k], q)
+                    else:
+                        t = agg.UpdateAsync(rows[q][k], q)
+            if mode == "coalesced":
+                agg.Wait(t)
+            e1.record(stream)
+            agg.sync()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        out[mode] = {"ms": round(best, 4), "GBps": round(nbytes / best / 1e6, 1),
+                     "frac": round(nbytes / best / 1e6 / HBM_PEAK_GBS, 4),
+                     "verified_checksum_p0": (agg.checksum(0) == want) if verify else None}
+    out["note"] = ("one call per arriving bucket (peer-major); each = a fold launch per arrival, "
+                   "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), best of "
+                   f"{reps}; algorithmic bytes P*(K+1)*L*8")
+    return out
+
+
 def pmc_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass for this
     workload (profiles/pmc_traffic.json), or None."""
@@ -494,6 +539,8 @@ def main():
         }
         if round_info:
             out["round"] = round_info
+        if world == 1 and not args.be and not args.no_per_arrival:
+            out["per_arrival"] = per_arrival_leg(ipls, torch, agg, rows, P, L, K, stream, not args.no_verify)
         if world == 1 and not args.no_e2e:
             out["host_inclusive"] = host_inclusive(ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_cpu_baseline:

@@ -141,18 +141,31 @@ int ipls_agg_update_gradient(ipls_agg *h, const void *flat, int64_t n, int src_k
 int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t n,
                         int src_kind);
 
-/* Asynchronous form of ipls_agg_accumulate for a bucket in pinned host memory
- * (ipls_host_alloc, 16-B aligned, HOST_F64/HOST_BE): the fold is queued to
- * read the bucket over PCIe and the call returns at once with *ticket.  The
- * caller keeps the buffer untouched until ipls_agg_wait(h, ticket) -- or any
- * synchronising call -- returns, so the next `ipfs cat` can fill another
- * buffer meanwhile.  Other sources run synchronously (ticket already done).
- * Folds still apply in call order. */
+/* Asynchronous form of ipls_agg_accumulate (Updater._Update without waiting,
+ * Updater.java:115-117); returns at once with *ticket.
+ *  - DEV_F64 / DEV_BE (8-B aligned): the bucket is queued, not read.  Each
+ *    partition's queued buckets are folded together in one launch, in call
+ *    order (bit-identical to folding them one by one), when the queues fill
+ *    (ipls_agg_set_coalesce, default 32), at ipls_agg_wait, or at the first
+ *    other call on the handle.
+ *  - pinned host memory (ipls_host_alloc, 16-B aligned, HOST_F64/HOST_BE):
+ *    the fold is queued at once and reads the bucket over PCIe, so the next
+ *    `ipfs cat` can fill another buffer meanwhile.
+ *  - other sources run synchronously (ticket already done).
+ * The caller keeps the bucket untouched (and allocated) until
+ * ipls_agg_wait(h, ticket) -- or any other call on the handle -- returns.
+ * Folds apply in call order. */
 int ipls_agg_accumulate_async(ipls_agg *h, int p, int target, const void *src, int64_t n,
                               int src_kind, uint64_t *ticket);
 
 /* Wait until fold `ticket` (and every fold queued before it) has finished. */
 int ipls_agg_wait(ipls_agg *h, uint64_t ticket);
+
+/* Coalescing group g (>= 1; 1 = fold each arrival at once) of asynchronous
+ * device buckets: the queues are flushed when they average g buckets per
+ * partition or one of them holds 2g.  Device traffic per element is
+ * (g + 2) * 8 bytes for a group of g buckets, against 24 * g one by one. */
+int ipls_agg_set_coalesce(ipls_agg *h, int max_group);
 
 /* Updater.run's indirect request (Updater.java:176-187): the queue item holds
  * only a hash, so the bucket is `ipfs cat` bytes read into the Updater's one

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -91,10 +92,29 @@ struct ipls_agg {
   hipStream_t copy_stream[kCopyThreads] = {};
   hipEvent_t ingest_ev = nullptr;
   std::vector<hipEvent_t> msg_ev;
-  // asynchronous folds of pinned host buckets: ticket t completes at fold_ev[t % kTickets]
-  static constexpr int kTickets = 64;
-  hipEvent_t fold_ev[kTickets] = {};
-  uint64_t ticket_next = 1, ticket_done = 0;
+  // Asynchronous folds (ipls_agg_accumulate_async).  Device buckets are not
+  // folded on arrival: per (target, partition) their pointers queue up and the
+  // next flush folds each queue in one launch, in call order -- the same
+  // expression (((acc + b0) + b1) + ...) the per-arrival folds evaluate, at
+  // (k+2)/k x 8 B per element instead of 24.  Every other entry point flushes
+  // first (IPLS_LOCK).  Pinned host buckets fold at once (zero copy).
+  struct Pending {
+    std::vector<const void*> bufs;
+    bool be = false;
+  };
+  std::map<std::pair<int, int>, Pending> pending;   // (target, p) -> queued buckets
+  int pending_n = 0;
+  int coalesce = 32;                                // queue length that triggers a flush (ipls_agg_set_coalesce)
+  // Tickets complete in issue order: a launch happens only after every earlier
+  // ticket was launched, and batch b completes tickets (prev.max, b.max_ticket].
+  struct Batch {
+    uint64_t max_ticket;
+    hipEvent_t ev;
+  };
+  static constexpr int kMaxBatches = 64;
+  std::deque<Batch> batches;
+  std::vector<hipEvent_t> ev_free;
+  uint64_t ticket_next = 1, ticket_done = 0, launched_upto = 0;
 
   // checksum result
   unsigned long long* d_sum = nullptr;
@@ -125,6 +145,14 @@ int fail(ipls_agg* h, int code, const char* fmt, ...) {
   g_tls_err = buf;
   return code;
 }
+
+int flush_pending(ipls_agg* h);
+
+// Take the handle's lock and fold any queued asynchronous device arrivals
+// first, so every entry point sees the accumulators in call order.
+#define IPLS_LOCK(h)                            \
+  std::lock_guard<std::mutex> lk_(h->mu);       \
+  if (int rc_ = flush_pending(h)) return rc_
 
 #define HIP_TRY(h, expr)                                                                \
   do {                                                                                  \
@@ -277,16 +305,28 @@ int d2h(ipls_agg* h, void* dst, const void* src, size_t bytes) {
 unsigned blocks_for(int64_t n, int64_t per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 
 // ---- kernel dispatch: k_reduce ----
-// Two shapes (tools/reduce_sweep.hip, profiles/r01/sweep*.txt):
-//  * big batches: 1024-lane workgroups, 1 peer in flight x 16 x 16 B per lane,
-//    i.e. each CU streams one 256 KiB contiguous chunk of one bucket at a time
+// Three shapes (tools/reduce_sweep.hip, profiles/r01/sweep*.txt), the first
+// whose tiles fill the 256 CUs (fill()):
+//  * big: 1024-lane workgroups, 1 peer in flight x 16 x 16 B per lane, i.e.
+//    each CU streams one 256 KiB contiguous chunk of one bucket at a time
 //    (fewer, longer DRAM streams): 85-89 % of 8 TB/s on config C over every
 //    bucket layout tried, vs 80-86 % for 256-lane / 64 KiB blocks;
-//  * small batches (< kBigMinBlocks big tiles): 256 lanes, 8 peers in flight
-//    x 16 B per lane, partition-major -- enough blocks to fill 256 CUs.
-constexpr int kBigG = 1, kBigMap = 0, kBigBS = 1024;
+//  * mid: the same per-lane work on 256-lane workgroups (64 KiB chunks), for
+//    batches of one or a few partitions: 1 x 4M x 32 at 86.2 % vs 72.7 % for
+//    the small shape and 55.8 % for the big one on 128 CUs
+//    (profiles/r01/sweep_few_partitions.txt);
+//  * small: 256 lanes, 8 peers in flight x 16 B per lane, partition-major --
+//    enough blocks for short partitions (ETHModel's 3 x 147,872).
+constexpr int kBigG = 1, kBigMap = 0, kBigBS = 1024, kMidBS = 256;
 constexpr int kSmallG = 8, kSmallR = 1, kSmallMap = 0;
-constexpr int64_t kBigMinBlocks = 512;
+// A tile count fills the chip when it is at least two waves of 256 CUs, or
+// one or more waves with at most a fifth of the last one idle.
+inline bool fill(int64_t tiles) {
+  if (tiles >= 512) return true;
+  if (tiles < 256) return false;
+  const int64_t waves = (tiles + 255) / 256;
+  return tiles * 5 >= waves * 256 * 4;
+}
 // 16 x 16 B per lane in the 128-VGPR budget of a 1024-lane workgroup:
 // native doubles 126 VGPRs; big-endian input 110 with the SEQ schedule of
 // reduce_tiles (hipcc's own schedule hoisted the loads around the bswap and
@@ -305,7 +345,9 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
   constexpr int R = big_r<BE_IN, START, FIN>();
   const int64_t big_tile = (int64_t)kBigBS * 2 * R;
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
-  if (big_tpp * n_parts >= kBigMinBlocks) {
+  const int64_t mid_tile = (int64_t)kMidBS * 2 * R;
+  const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
+  if (fill(big_tpp * n_parts)) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
     // partial last tiles are scheduled first (map 3, ipls_kernels.hpp map_block)
     const bool partial = big_tpp > 1 && maxL % big_tile != 0;
@@ -322,6 +364,22 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
     if (partial) BIG(3);
     else BIG(kBigMap);
 #undef BIG
+  } else if (fill(mid_tpp * n_parts)) {
+    const dim3 grid((unsigned)grid_blocks(kBigMap, mid_tpp * n_parts));
+    const bool partial = mid_tpp > 1 && maxL % mid_tile != 0;
+#define MID(MAP)                                                                                          \
+    do {                                                                                                  \
+      if constexpr (FIN)                                                                                  \
+        hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, MAP, kMidBS, big_seqf<BE_IN, START>()>), grid, \
+                           dim3(kMidBS), 0, st, bufs, parts, k, (int)mid_tpp, n_parts, secure, cnts);     \
+      else                                                                                                \
+        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, MAP, kMidBS,                   \
+                                     big_seqf<BE_IN, START>()>),                                          \
+                           grid, dim3(kMidBS), 0, st, bufs, parts, k, (int)mid_tpp, n_parts);             \
+    } while (0)
+    if (partial) MID(3);
+    else MID(kBigMap);
+#undef MID
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
     const int64_t tpp = (maxL + tile - 1) / tile;
@@ -644,8 +702,8 @@ int ipls_agg_close(ipls_agg* h) {
     }
   if (h->ingest_ev) hipEventDestroy(h->ingest_ev);
   for (hipEvent_t e : h->msg_ev) hipEventDestroy(e);
-  for (auto& e : h->fold_ev)
-    if (e) hipEventDestroy(e);
+  for (auto& b : h->batches) hipEventDestroy(b.ev);
+  for (hipEvent_t e : h->ev_free) hipEventDestroy(e);
   for (void* d : h->d_table)
     if (d) hipFree(d);
   if (h->d_scratch) hipFree(h->d_scratch);
@@ -681,7 +739,7 @@ void* ipls_agg_stream(ipls_agg* h) { return h ? (void*)h->stream : nullptr; }
 
 int ipls_agg_sync(ipls_agg* h) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return IPLS_OK;
 }
@@ -690,18 +748,87 @@ int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   std::lock_guard<std::mutex> lk(h->mu);
   if (ticket >= h->ticket_next) return fail(h, IPLS_E_INVAL, "ticket %llu was never issued", (unsigned long long)ticket);
-  // a slot is only reused after its previous ticket completed, so anything
-  // older than the ring is already <= ticket_done
   if (ticket <= h->ticket_done) return IPLS_OK;
-  HIP_TRY(h, hipEventSynchronize(h->fold_ev[ticket % ipls_agg::kTickets]));
-  h->ticket_done = ticket;
+  if (ticket > h->launched_upto)
+    if (int rc = flush_pending(h)) return rc;
+  while (!h->batches.empty()) {
+    const ipls_agg::Batch b = h->batches.front();
+    HIP_TRY(h, hipEventSynchronize(b.ev));
+    h->batches.pop_front();
+    h->ev_free.push_back(b.ev);
+    h->ticket_done = std::max(h->ticket_done, b.max_ticket);
+    if (b.max_ticket >= ticket) break;
+  }
   return IPLS_OK;
 }
+
+int ipls_agg_set_coalesce(ipls_agg* h, int max_group) {
+  IPLS_LOCK(h);
+  h->coalesce = std::max(1, max_group);
+  return IPLS_OK;
+}
+
+namespace {
+
+// Close the launches queued since the last batch: tickets up to ticket_next-1
+// complete at the event recorded now.
+int end_batch(ipls_agg* h) {
+  hipEvent_t ev;
+  if (!h->ev_free.empty()) {
+    ev = h->ev_free.back();
+    h->ev_free.pop_back();
+  } else {
+    HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  HIP_TRY(h, hipEventRecord(ev, h->stream));
+  h->batches.push_back({h->ticket_next - 1, ev});
+  h->launched_upto = h->ticket_next - 1;
+  while ((int)h->batches.size() > ipls_agg::kMaxBatches) {   // bound the events in flight
+    const ipls_agg::Batch b = h->batches.front();
+    HIP_TRY(h, hipEventSynchronize(b.ev));
+    h->batches.pop_front();
+    h->ev_free.push_back(b.ev);
+    h->ticket_done = std::max(h->ticket_done, b.max_ticket);
+  }
+  return IPLS_OK;
+}
+
+// Fold every queued device arrival: runs of consecutive partitions of one
+// target with the same queue length and byte order go as one launch (the
+// batch kernel's table is [partition][peer]).
+int flush_pending(ipls_agg* h) {
+  if (h->pending.empty()) return IPLS_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  int rc = IPLS_OK;
+  std::vector<const void*> tab;
+  for (auto it = h->pending.begin(); it != h->pending.end() && !rc;) {
+    const int target = it->first.first, p0 = it->first.second;
+    const size_t k = it->second.bufs.size();
+    const bool be = it->second.be;
+    auto jt = std::next(it);
+    int n = 1;
+    while (jt != h->pending.end() && jt->first.first == target && jt->first.second == p0 + n &&
+           jt->second.bufs.size() == k && jt->second.be == be) {
+      ++n;
+      ++jt;
+    }
+    tab.clear();
+    for (auto q = it; q != jt; ++q) tab.insert(tab.end(), q->second.bufs.begin(), q->second.bufs.end());
+    rc = reduce_dev(h, p0, n, tab.data(), (int)k, be, IPLS_START_ACCUM, target);
+    it = jt;
+  }
+  h->pending.clear();
+  h->pending_n = 0;
+  if (rc) return rc;
+  return end_batch(h);
+}
+
+}  // namespace
 
 int ipls_agg_reduce_batch(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k,
                           int src_kind, int start_mode, int target) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > h->P)
     return fail(h, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, h->P);
   if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE)
@@ -715,7 +842,7 @@ int ipls_agg_reduce_batch(ipls_agg* h, int p_first, int n_parts, const void* con
 
 int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (!src) return IPLS_OK;  // Gradient == null: the Updater loops do nothing (Updater.java:115)
@@ -789,6 +916,30 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
 int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind,
                               uint64_t* ticket) {
   if (!h || !ticket) return fail(h, IPLS_E_INVAL, "null argument");
+  if (src && (src_kind == IPLS_DEV_F64 || src_kind == IPLS_DEV_BE)) {
+    // device bucket: queued, folded with the partition's other queued buckets
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (int rc = check_part(h, p)) return rc;
+    if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+    if (n < h->len[p])
+      return fail(h, IPLS_E_RANGE, "bucket of %lld doubles shorter than partition length %lld", (long long)n,
+                  (long long)h->len[p]);
+    if ((uintptr_t)src & 7) return fail(h, IPLS_E_INVAL, "device bucket not 8-byte aligned");
+    const bool be = src_kind == IPLS_DEV_BE;
+    auto& q = h->pending[{target, p}];
+    if (!q.bufs.empty() && q.be != be)
+      if (int rc = flush_pending(h)) return rc;
+    auto& q2 = h->pending[{target, p}];
+    q2.be = be;
+    q2.bufs.push_back(src);
+    ++h->pending_n;
+    *ticket = h->ticket_next++;
+    // flush when the queues average `coalesce` buckets (arrivals spread over
+    // partitions flush as one rectangular launch), or one queue holds twice that
+    if ((int)q2.bufs.size() >= 2 * h->coalesce || h->pending_n >= h->coalesce * (int)h->pending.size())
+      return flush_pending(h);
+    return IPLS_OK;
+  }
   void* alias = nullptr;
   const bool host = src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE;
   if (!src || !host || ((uintptr_t)src & 15) || !is_pinned_host(src, &alias) || !alias) {
@@ -798,31 +949,22 @@ int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, i
     *ticket = h->ticket_done;
     return rc;
   }
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);   // earlier queued device buckets fold first
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (int rc = host_decode_count(src_kind, n, h->len[p], h)) return rc;
   HIP_TRY(h, hipSetDevice(h->device));
-  const uint64_t t = h->ticket_next;
-  hipEvent_t& ev = h->fold_ev[t % ipls_agg::kTickets];
-  if (!ev) HIP_TRY(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  if (t > (uint64_t)ipls_agg::kTickets && t - ipls_agg::kTickets > h->ticket_done) {
-    HIP_TRY(h, hipEventSynchronize(ev));   // the slot's previous fold (and all before it) is done
-    h->ticket_done = t - ipls_agg::kTickets;
-  }
   const void* bl[1] = {alias};   // zero copy: the kernel reads the pinned bucket over PCIe
   if (int rc = reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target, nullptr, false, nullptr,
                           true))
     return rc;
-  HIP_TRY(h, hipEventRecord(ev, h->stream));
-  h->ticket_next = t + 1;
-  *ticket = t;
-  return IPLS_OK;
+  *ticket = h->ticket_next++;
+  return end_batch(h);
 }
 
 int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, int64_t n_bytes) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
@@ -870,7 +1012,7 @@ int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, 
 
 int ipls_agg_reset(ipls_agg* h, int p) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (p == IPLS_ALL_PARTITIONS) {
     for (int q = 0; q < h->P; ++q) h->agg_zero[q] = h->rep_zero[q] = 1;
     return IPLS_OK;
@@ -882,7 +1024,7 @@ int ipls_agg_reset(ipls_agg* h, int p) {
 
 int ipls_agg_promote_future(ipls_agg* h, const int32_t* parts, int n_parts) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n_parts < 0 || (n_parts > 0 && !parts)) return fail(h, IPLS_E_INVAL, "bad partition list");
   for (int i = 0; i < n_parts; ++i)
     if (int rc = check_part(h, parts[i])) return rc;
@@ -898,7 +1040,7 @@ int ipls_agg_promote_future(ipls_agg* h, const int32_t* parts, int n_parts) {
 
 int ipls_agg_device_ptr(ipls_agg* h, int p, int target, void** ptr) {
   if (!h || !ptr) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   HIP_TRY(h, hipSetDevice(h->device));
@@ -909,7 +1051,7 @@ int ipls_agg_device_ptr(ipls_agg* h, int p, int target, void** ptr) {
 
 int ipls_agg_read(ipls_agg* h, int p, int target, void* dst, int64_t n, int dst_kind) {
   if (!h || !dst) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   const int64_t L = h->len[p];
@@ -942,7 +1084,7 @@ int ipls_agg_read(ipls_agg* h, int p, int target, void* dst, int64_t n, int dst_
 
 int ipls_agg_checksum(ipls_agg* h, int p, int target, uint64_t* out) {
   if (!h || !out) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   HIP_TRY(h, hipSetDevice(h->device));
@@ -1019,7 +1161,7 @@ static int divide_range(ipls_agg* h, int p0, int np, unsigned long long* d_out, 
 
 int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* avg_out) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   int p0 = p, np = 1;
   if (p == IPLS_ALL_PARTITIONS) {
     p0 = 0;
@@ -1058,7 +1200,7 @@ int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* a
 
 int ipls_agg_set_weights(ipls_agg* h, int p, const void* src, int64_t n, int src_kind) {
   if (!h || !src) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   const int64_t L = h->len[p];
   if (src_kind == IPLS_HOST_FRAME) {
@@ -1137,7 +1279,7 @@ static int flat_to_device(ipls_agg* h, const void* flat, int64_t n, int kind, co
 
 int ipls_agg_other_replica(ipls_agg* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (n < 0 || (n > 0 && !src)) return fail(h, IPLS_E_INVAL, "bad bucket");
   if ((src_kind == IPLS_DEV_F64 || src_kind == IPLS_DEV_BE) && ((uintptr_t)src & 7))
@@ -1177,7 +1319,7 @@ int ipls_agg_other_replica(ipls_agg* h, int p, int32_t aggregator, const void* s
 
 int ipls_agg_collect_replicas(ipls_agg* h, int32_t* participants) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   HIP_TRY(h, hipSetDevice(h->device));
   // REP[p] is a double[L_p]: a longer stored array overruns it (IPLS.java:1225).
   for (auto& kv : h->other)
@@ -1210,7 +1352,7 @@ int ipls_agg_collect_replicas(ipls_agg* h, int32_t* participants) {
 
 int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {
   if (!h || !src) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n < h->flat_total)
     return fail(h, IPLS_E_RANGE, "model of %lld values < model size %lld", (long long)n, (long long)h->flat_total);
   HIP_TRY(h, hipSetDevice(h->device));
@@ -1247,7 +1389,7 @@ static int split_bounds(ipls_agg* h, int p, int64_t n, int64_t* ncopy) {
 
 int ipls_agg_split(ipls_agg* h, const void* flat, int64_t n, int src_kind, int p, void* dst, int dst_kind) {
   if (!h || !flat || !dst) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   int64_t ncopy;
   if (int rc = split_bounds(h, p, n, &ncopy)) return rc;
@@ -1292,7 +1434,7 @@ int ipls_agg_update_gradient(ipls_agg* h, const void* flat, int64_t n, int src_k
                              int n_owned) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   if (!flat) return IPLS_OK;  // Gradients == null (IPLS.java:1708-1713, 1738 `&& Gradients != null`)
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n_owned < 0 || (n_owned > 0 && !owned)) return fail(h, IPLS_E_INVAL, "bad owned list");
   // OrganizeGradients splits every partition before anything is accumulated
   // (IPLS.java:1709), so a length error leaves the accumulators untouched.
@@ -1326,7 +1468,7 @@ int ipls_agg_update_gradient(ipls_agg* h, const void* flat, int64_t n, int src_k
 
 int ipls_agg_get_partitions(ipls_agg* h, void* out, int64_t n, int out_kind) {
   if (!h || !out) return fail(h, IPLS_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   const int64_t M = h->flat_total;
   if (n < M) return fail(h, IPLS_E_RANGE, "output of %lld < model size %lld", (long long)n, (long long)M);
   if (out_kind != IPLS_HOST_F64 && out_kind != IPLS_HOST_BE_CANON && out_kind != IPLS_DEV_F64)
@@ -1390,7 +1532,7 @@ int ipls_checksum_dev(const void* src, int64_t n, int src_kind, uint64_t* out, v
 int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                               int start_mode, void* const* dst, int dst_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > h->P)
     return fail(h, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, h->P);
   if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE)
@@ -1407,7 +1549,7 @@ int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void*
 int ipls_agg_aggregate_round(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                              void* avg_out, int avg_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > h->P)
     return fail(h, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, h->P);
   if (src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE)
@@ -1511,7 +1653,7 @@ bool b64_host_bytes(const uint8_t* t, int64_t d, int64_t lo, int64_t hi, uint8_t
 int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
                            int layers, const int32_t* parts, int32_t* status) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (n_msgs < 0 || (n_msgs > 0 && (!msgs || !lens))) return fail(h, IPLS_E_INVAL, "bad message list");
   if (layers < 1 || layers > 2) return fail(h, IPLS_E_INVAL, "layers must be 1 or 2");
   if (target_off(h, 0, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
@@ -1666,7 +1808,7 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
 
 int ipls_agg_blend(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind, double a, double b) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (!src) return IPLS_OK;
@@ -1693,7 +1835,7 @@ int ipls_agg_blend(ipls_agg* h, int p, int target, const void* src, int64_t n, i
 
 int ipls_agg_scale(ipls_agg* h, int p, int dst_target, int src_target, double c) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, dst_target) < 0 || target_off(h, p, src_target) < 0) return fail(h, IPLS_E_INVAL, "bad target");
   HIP_TRY(h, hipSetDevice(h->device));
@@ -1795,7 +1937,7 @@ int64_t ipls_pair_encode(int32_t workers, const void* g, int64_t n, int g_kind, 
 
 int64_t ipls_agg_commit_partial(ipls_agg* h, int p, int32_t workers, uint8_t* out, int64_t out_cap) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   const int64_t L = h->len[p];
   const int64_t hl = javaser::pair_header_len(), total = hl + 8 * L + javaser::pair_trailer_len();
@@ -1819,7 +1961,7 @@ int64_t ipls_agg_commit_partial(ipls_agg* h, int p, int32_t workers, uint8_t* ou
 int64_t ipls_agg_merge_files(ipls_agg* h, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
                              uint8_t* out, int64_t out_cap) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  IPLS_LOCK(h);
   if (k < 1 || !files || !lens) return fail(h, IPLS_E_INVAL, "need at least one file");
   if (file_kind != IPLS_HOST_BE && file_kind != IPLS_HOST_PAIR) return fail(h, IPLS_E_INVAL, "file_kind BE or PAIR");
   // decode every file's payload position first (GetParameters / Download_Partial_Updates)

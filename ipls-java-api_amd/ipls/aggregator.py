@@ -200,17 +200,27 @@ class Aggregator:
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
 
     def UpdateAsync(self, gradient, partition: int, from_clients: bool = True, *, big_endian: bool = True) -> int:
-        """Updater._Update without waiting: ``gradient`` is a PinnedBuffer (the
+        """Updater._Update without waiting.  ``gradient`` is a PinnedBuffer (the
         `ipfs cat` bytes, big-endian unless ``big_endian=False``) that the fold
-        reads over PCIe.  Returns a ticket; keep the buffer until Wait(ticket)."""
-        if not isinstance(gradient, PinnedBuffer):
-            raise TypeError("UpdateAsync takes a PinnedBuffer (ipls_host_alloc memory)")
+        reads over PCIe, or a DeviceBuffer that is queued and folded with the
+        partition's other queued buckets in one launch (set_coalesce).  Returns
+        a ticket; keep the buffer until Wait(ticket)."""
         target = N.TGT_AGG if from_clients else N.TGT_REP
         t = ctypes.c_uint64()
+        if isinstance(gradient, DeviceBuffer):
+            self._chk(self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr, gradient.n,
+                                                          gradient.kind, ctypes.byref(t)))
+            return t.value
+        if not isinstance(gradient, PinnedBuffer):
+            raise TypeError("UpdateAsync takes a PinnedBuffer (ipls_host_alloc memory) or a DeviceBuffer")
         self._chk(self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr,
                                                       gradient.nbytes // 8,
                                                       N.HOST_BE if big_endian else N.HOST_F64, ctypes.byref(t)))
         return t.value
+
+    def set_coalesce(self, max_group: int):
+        """Largest group of queued device buckets folded per partition in one launch."""
+        self._chk(self._lib.ipls_agg_set_coalesce(self._h, max_group))
 
     def Wait(self, ticket: int):
         """Block until the UpdateAsync fold ``ticket`` (and all before it) is done."""

@@ -1045,6 +1045,68 @@ def test_async_pinned_arrivals(ipls, O):
         pb.close()
 
 
+@pytest.mark.parametrize("group", [1, 3, 8, 32])
+def test_async_device_coalesced(ipls, O, group):
+    """Queued device arrivals (ipls_agg_accumulate_async, DEV_F64/DEV_BE) fold
+    in call order with the same bits as one-by-one Updates, whatever flushes
+    the queues: the group size, a byte-order change, a synchronous Update, a
+    pinned-host async fold, a read, Wait.  Ragged queues across partitions,
+    an odd length, an 8-B (not 16-B) aligned bucket, both targets."""
+    P, L = 5, 70001
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.set_coalesce(group)
+    vals = [O.synth_bucket(L + 1, 6, k)[:L] for k in range(12)]
+    keep = []
+
+    def devbuf(k, be=False, shift=False):
+        raw = O.be_encode(vals[k]) if be else np.asarray(vals[k]).tobytes()
+        t = torch.zeros(len(raw) + 16, dtype=torch.uint8, device="cuda")
+        off = 8 if shift else 0
+        t[off:off + len(raw)] = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()).to("cuda")
+        keep.append(t)
+        torch.cuda.synchronize()          # the handle's stream does not order after torch's
+        return ipls.DeviceBuffer(int(t.data_ptr()) + off, L, big_endian=be)
+
+    ref = {(tg, p): None for tg in (ipls.TGT_AGG, ipls.TGT_REP) for p in range(P)}
+
+    def fold(tg, p, k):
+        acc = ref[(tg, p)]
+        ref[(tg, p)] = O.reduce([vals[k]], L) if acc is None else O.reduce([vals[k]], L, O.START_ACCUM, acc=acc)
+
+    pb = ipls.PinnedBuffer(8 * L)
+    pb.view()[:] = np.frombuffer(O.be_encode(vals[11]), dtype=np.uint8)
+    tickets = []
+    rng = np.random.default_rng(group)
+    for j in range(90):
+        p = int(rng.integers(0, P)) if j % 3 else j % P
+        tg = ipls.TGT_REP if j % 7 == 3 else ipls.TGT_AGG
+        k = j % 11
+        if j == 40:
+            agg.Update(vals[k], p, from_clients=tg == ipls.TGT_AGG)     # synchronous host fold
+        elif j == 55:
+            tickets.append(agg.UpdateAsync(pb, p, from_clients=tg == ipls.TGT_AGG))   # pinned, zero copy
+            k = 11
+        elif j == 70:
+            assert_bits_equal(agg.read(0), ref[(ipls.TGT_AGG, 0)], "mid-stream read")
+            continue
+        else:
+            b = devbuf(k, be=(j // 9) % 2 == 1, shift=j % 13 == 5)
+            tickets.append(agg.UpdateAsync(b, p, from_clients=tg == ipls.TGT_AGG))
+        fold(tg, p, k)
+    assert tickets == sorted(tickets) and len(set(tickets)) == len(tickets)
+    agg.Wait(tickets[len(tickets) // 2])
+    agg.Wait(tickets[-1])
+    for (tg, p), r in ref.items():
+        if r is not None:
+            assert_bits_equal(agg.read(p, tg), r, f"target {tg} p{p}")
+    with pytest.raises(ipls.IplsError):
+        agg.UpdateAsync(ipls.DeviceBuffer(int(keep[0].data_ptr()) + 4, L), 0)   # not 8-B aligned
+    with pytest.raises(ipls.IplsError):
+        agg.UpdateAsync(ipls.DeviceBuffer(int(keep[0].data_ptr()), L - 1), 0)   # shorter than L_p
+    agg.close()
+    pb.close()
+
+
 def test_partial_update_pair_files(ipls, O):
     """-i 1 partial updates: commit_partial_update's Pair<Integer,double[]>
     bytes (IPLS_Comm.java:51-61) from AGG on the device; a replica's Pair
