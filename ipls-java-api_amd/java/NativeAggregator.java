@@ -60,6 +60,18 @@ public final class NativeAggregator implements AutoCloseable {
         accumulateDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
     }
 
+    /** The same fold without waiting (one call per queue.take(), Updater.java:169-211):
+     *  beDoubles is a direct buffer from hostAllocDirect (pinned), folded over PCIe
+     *  while the next `ipfs cat` fills another buffer.  Keep it until await(ticket). */
+    public long updateFromBytesAsync(ByteBuffer beDoubles, int p, boolean fromClients) {
+        return accumulateAsyncDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
+    }
+
+    /** Block until fold `ticket` (and every fold queued before it) has finished. */
+    public void await(long ticket) {
+        waitTicket(handle, ticket);
+    }
+
     /** Updater.java:99-101: a client's bucket for a later iteration. */
     public void updateFromFuture(double[] gradient, int p) {
         if (gradient != null) accumulate(handle, p, TGT_FUTURE, gradient);
@@ -156,6 +168,8 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void updateGradient(long h, double[] flat, int[] owned);
     private static native void accumulate(long h, int p, int target, double[] g);
     private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
+    private static native long accumulateAsyncDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
+    private static native void waitTicket(long h, long ticket);
     private static native void accumulateFrame(long h, int p, int target, byte[] frame);
     private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, long nBytes);
     private static native void finalizePartition(long h, int p, byte[] sumOut);

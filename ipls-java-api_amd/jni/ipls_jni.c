@@ -104,6 +104,20 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclas
     CHECK(ipls_agg_accumulate(H(h), p, tgt, src, n, kind), H(h));
 }
 
+JNIEXPORT jlong JNICALL Java_NativeAggregator_accumulateAsyncDirect(JNIEnv *env, jclass c, jlong h, jint p,
+                                                                      jint tgt, jobject buf, jlong n, jint kind) {
+    (void)c;
+    void *src = (*env)->GetDirectBufferAddress(env, buf);
+    uint64_t t = 0;
+    CHECK(ipls_agg_accumulate_async(H(h), p, tgt, src, n, kind, &t), H(h));
+    return (jlong)t;
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_waitTicket(JNIEnv *env, jclass c, jlong h, jlong ticket) {
+    (void)c;
+    CHECK(ipls_agg_wait(H(h), (uint64_t)ticket), H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                               jobject buf, jlong nBytes) {
     (void)c;
