@@ -1107,6 +1107,66 @@ def test_async_device_coalesced(ipls, O, group):
     pb.close()
 
 
+def test_concurrent_callers_one_handle(ipls, O):
+    """The reference's producer threads, Updater thread and daemon thread all
+    reach the accumulators (serialised by PeerData.mtx, PeerData.java:27).
+    Four Python threads (ctypes drops the GIL) share one handle, each owning
+    its own partitions so the per-partition order is fixed: synchronous host
+    and device folds, queued device folds, pubsub ingest and reads interleave.
+    Every partition must end bit-identical to the oracle's fold in that
+    thread's order."""
+    import threading
+    P, L, T = 8, 30011, 4
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.set_coalesce(3)
+    vals = [O.synth_bucket(L, 7, k) for k in range(6)]
+    dev = []
+    for v in vals:
+        t = torch.from_numpy(np.asarray(v)).to("cuda")
+        dev.append((t, ipls.DeviceBuffer.from_tensor(t)))
+    torch.cuda.synchronize()
+    msgs = [O.pubsub_message(O.frame_encode(v, 0, 1, 3, b"QmT")) for v in vals]
+    plans = {}
+    errors = []
+
+    def worker(w):
+        rng = np.random.default_rng(100 + w)
+        mine = [p for p in range(P) if p % T == w]
+        seq = []
+        try:
+            for j in range(60):
+                p = mine[j % len(mine)]
+                k = int(rng.integers(0, len(vals)))
+                how = int(rng.integers(0, 4))
+                if how == 0:
+                    agg.Update(vals[k], p)
+                elif how == 1:
+                    agg.Update(dev[k][1], p)
+                elif how == 2:
+                    agg.UpdateAsync(dev[k][1], p)
+                else:
+                    n, st = agg.ingest_pubsub([msgs[k]], partitions=[p])
+                    assert n == 1 and st == [0]
+                seq.append((p, k))
+                if j % 17 == 0:
+                    agg.read(p)
+            plans[w] = seq
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    ths = [threading.Thread(target=worker, args=(w,)) for w in range(T)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    for w, seq in plans.items():
+        for p in {p for p, _ in seq}:
+            ks = [k for q, k in seq if q == p]
+            assert_bits_equal(agg.read(p), O.reduce([vals[k] for k in ks], L), f"thread {w} p{p}")
+    agg.close()
+
+
 def test_partial_update_pair_files(ipls, O):
     """-i 1 partial updates: commit_partial_update's Pair<Integer,double[]>
     bytes (IPLS_Comm.java:51-61) from AGG on the device; a replica's Pair
