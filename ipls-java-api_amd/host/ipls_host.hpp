@@ -7,6 +7,8 @@
 //
 //   IPLS                 IPLS.java:880-2305  (aggregation methods only)
 //   Updater              Updater.java:14-218 (_Update)
+//   UpdaterThread        Updater.run, Updater.java:155-216 (the reducer thread
+//                        draining PeerData.queue, PeerData.java:117)
 //   Light_IPLS_Daemon    Light_IPLS_Daemon.java:9-114 (UpdateModel / Get_Partitions)
 //   MyIPFSClass          MyIPFSClass.java codecs used on the path
 //   Middleware           Middleware.java:26-210 (flags, wire stream, Encode)
@@ -17,13 +19,17 @@
 #pragma once
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ipls_agg.h"
@@ -334,6 +340,108 @@ class Updater {
 
  private:
   IPLS& ipls_;
+};
+
+// ---- Updater.run (Updater.java:155-216): the reducer thread ----------------------
+// One consumer drains the request queue (PeerData.queue, PeerData.java:117) in
+// arrival order: a request with a payload folds through _Update; a hash-only
+// request reads the `ipfs cat` bytes into the one Gradient_Buff and folds that
+// (Updater.java:176-187).  Device-resident payloads are queued on the handle
+// (ipls_agg_accumulate_async), so a burst of arrivals folds in one launch per
+// partition.  Producers (ThreadReceiver, GGP_Receiver, Download_Scheduler) call
+// put() from any thread; the daemon calls drain() before AggregatePartition.
+// Java's thread dies on the first exception (the catch sits outside
+// while(true), :168-215); here the request is dropped, its exception message
+// kept in failures(), and the loop goes on.
+class UpdaterThread {
+ public:
+  // Sextet<origins, partition, iteration, from_clients, double[], hash>
+  struct Request {
+    int partition = 0;
+    bool from_clients = true;
+    std::vector<double> gradient;   // value4 (the payload); empty and no file/device -> null, no fold
+    std::vector<uint8_t> file;      // a hash-only request: the `ipfs cat` bytes of value5
+    const void* device = nullptr;   // or a device-resident bucket, kept alive by the caller until drain()
+    int64_t device_n = 0;
+    bool device_big_endian = false;
+  };
+
+  explicit UpdaterThread(IPLS& ipls) : ipls_(ipls), th_([this] { loop(); }) {}
+  ~UpdaterThread() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  UpdaterThread(const UpdaterThread&) = delete;
+  UpdaterThread& operator=(const UpdaterThread&) = delete;
+
+  // PeerData.queue.put
+  void put(Request r) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(r));
+      ++put_n_;
+    }
+    cv_.notify_one();
+  }
+  // Block until every request put so far has been folded on the device.
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_.wait(lk, [this] { return done_n_ == put_n_; });
+    lk.unlock();
+    check(ipls_agg_sync(ipls_.handle()), ipls_.handle());   // folds queued device buckets, waits
+  }
+  std::vector<std::string> failures() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return failures_;
+  }
+
+ private:
+  void loop() {
+    Updater u(ipls_);
+    for (;;) {
+      Request r;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;   // stop_ and nothing left
+        r = std::move(q_.front());
+        q_.pop_front();
+      }
+      try {
+        if (r.device) {
+          uint64_t t = 0;
+          check(ipls_agg_accumulate_async(ipls_.handle(), r.partition, r.from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
+                                          r.device, r.device_n, r.device_big_endian ? IPLS_DEV_BE : IPLS_DEV_F64, &t),
+                ipls_.handle());
+        } else if (!r.gradient.empty()) {
+          u._Update(&r.gradient, r.partition, r.from_clients);
+        } else if (!r.file.empty()) {
+          u._Update_from_file(r.file, r.partition, r.from_clients);
+        }
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(mu_);
+        failures_.push_back(e.what());
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        ++done_n_;
+      }
+      idle_.notify_all();
+    }
+  }
+
+  IPLS& ipls_;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_;
+  std::deque<Request> q_;
+  bool stop_ = false;
+  uint64_t put_n_ = 0, done_n_ = 0;
+  std::vector<std::string> failures_;
+  std::thread th_;   // last: starts after every member above exists
 };
 
 // ---- Decentralized_Storage_Receiver (storage node, -aggr 1) ----------------------

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ipls_host.hpp"
@@ -210,6 +211,71 @@ int main(int argc, char** argv) {
       auto second = ipls.AggregatePartition(0);         // next round starts from `later`
       ipls_oracle_be_encode(later.data(), L0, ref.data());
       CHECK(second == ref, "promoted future gradients");
+    });
+
+    run("UpdaterThread: producers, hash-only files, device buckets, a bad request", [&] {
+      PeerData pd;
+      pd._MODEL_SIZE = 200003;
+      pd._PARTITIONS = 6;
+      IPLS ipls(pd, {0, 1, 2, 3, 4, 5});
+      IPLS src(pd);   // its AGG arrays stand in for device-resident buckets (e.g. RCCL partials)
+      std::vector<int64_t> L(6);
+      std::vector<std::vector<double>> dval(6);
+      std::vector<const void*> dptr(6);
+      for (int p = 0; p < 6; ++p) {
+        L[p] = ipls.partition_length(p);
+        dval[p] = synth(L[p], p, 9);
+        check(ipls_agg_accumulate(src.handle(), p, IPLS_TGT_AGG, dval[p].data(), L[p], IPLS_HOST_F64), src.handle());
+        void* d = nullptr;
+        check(ipls_agg_device_ptr(src.handle(), p, IPLS_TGT_AGG, &d), src.handle());
+        dptr[p] = d;
+      }
+      check(ipls_agg_sync(src.handle()), src.handle());
+      std::vector<std::vector<std::vector<double>>> seq(6);   // per partition, the buckets in fold order
+      {
+        UpdaterThread ut(ipls);
+        auto producer = [&](int t) {
+          for (int j = 0; j < 24; ++j) {
+            const int p = j % 2 ? t + 3 : t;   // each partition has one producer: a fixed order
+            UpdaterThread::Request r;
+            r.partition = p;
+            const int kind = (j + t) % 3;
+            std::vector<double> g = synth(L[p], p, (t * 7 + j) % 5);
+            if (kind == 0) {
+              r.gradient = g;
+            } else if (kind == 1) {
+              r.file.resize(8 * (size_t)L[p]);
+              ipls_oracle_be_encode(g.data(), L[p], r.file.data());
+            } else {
+              r.device = dptr[p];
+              r.device_n = L[p];
+              g = dval[p];
+            }
+            seq[p].push_back(g);
+            ut.put(std::move(r));
+            if (t == 0 && j == 11) {
+              UpdaterThread::Request bad;
+              bad.partition = 0;
+              bad.gradient.assign(3, 1.0);   // shorter than L_0: dropped, reported
+              ut.put(std::move(bad));
+            }
+          }
+        };
+        std::vector<std::thread> ths;
+        for (int t = 0; t < 3; ++t) ths.emplace_back(producer, t);
+        for (auto& th : ths) th.join();
+        ut.drain();
+        auto fails = ut.failures();
+        CHECK(fails.size() == 1, "one dropped request");
+      }
+      for (int p = 0; p < 6; ++p) {
+        std::vector<const double*> bp;
+        for (auto& g : seq[p]) bp.push_back(g.data());
+        std::vector<double> ref((size_t)L[p]), got((size_t)L[p]);
+        ipls_oracle_reduce(ref.data(), bp.data(), (int)bp.size(), L[p], 1);
+        check(ipls_agg_read(ipls.handle(), p, IPLS_TGT_AGG, got.data(), L[p], IPLS_HOST_F64), ipls.handle());
+        CHECK(bits_equal(got.data(), ref.data(), (size_t)L[p]), "partition folded in its producer's order");
+      }
     });
 
     run("partial updates (-i 1): commit, replica fold, storage merge", [&] {

@@ -27,7 +27,7 @@ def test_host_mirror_on_gpu():
     _build()
     r = subprocess.run([str(BIN), "--gpu", str(GOLDEN)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "7 passed, 0 failed" in r.stdout, r.stdout
+    assert "8 passed, 0 failed" in r.stdout, r.stdout
 
 
 def test_partial_update_parser_under_asan():
