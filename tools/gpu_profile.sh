@@ -16,9 +16,9 @@ fi
 timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || exit 12
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/trace -o run -- \
-  python3 $R/bench.py --no-cpu-baseline --no-e2e "$@" > $O/bench_trace.json 2> $O/bench_trace.err || exit 13
+  python3 $R/bench.py --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival "$@" > $O/bench_trace.json 2> $O/bench_trace.err || exit 13
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch -o run -- \
-  python3 $R/bench.py --no-cpu-baseline --no-e2e --no-verify "$@" --steps 3 --warmup 1 > $O/pmc_fetch.log 2>&1 || exit 14
+  python3 $R/bench.py --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify "$@" --steps 3 --warmup 1 > $O/pmc_fetch.log 2>&1 || exit 14
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/pmc_write -o run -- \
-  python3 $R/bench.py --no-cpu-baseline --no-e2e --no-verify "$@" --steps 3 --warmup 1 > $O/pmc_write.log 2>&1 || exit 15
+  python3 $R/bench.py --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify "$@" --steps 3 --warmup 1 > $O/pmc_write.log 2>&1 || exit 15
 echo done > $O/done
