@@ -763,6 +763,7 @@ int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
 }
 
 int ipls_agg_set_coalesce(ipls_agg* h, int max_group) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   h->coalesce = std::max(1, max_group);
   return IPLS_OK;

@@ -94,3 +94,25 @@ def test_jni_shim_matches_java_natives():
     declared = set(re.findall(r"\b(ipls_\w+)\s*\(", header))
     called = set(re.findall(r"\b(ipls_\w+)\s*\(", jni))
     assert called <= declared, called - declared
+
+
+def test_null_handle_fails_cleanly():
+    """Every entry point that takes a handle returns a negative code for a
+    NULL one (the Java caller's closed/never-opened aggregator), without
+    touching a GPU or crashing."""
+    import ipls
+    from ipls import _native as N
+    L = ipls.lib()
+    skipped = {"ipls_agg_open", "ipls_agg_abi_version", "ipls_agg_close", "ipls_agg_last_error", "ipls_agg_stream",
+               "ipls_host_alloc", "ipls_host_free", "ipls_synth_fill", "ipls_checksum_dev", "ipls_encode_secure",
+               "ipls_frame_parse", "ipls_frame_encode", "ipls_pair_parse", "ipls_pair_encode"}
+    checked = 0
+    for name, (res, args) in N.SIGNATURES.items():
+        if name in skipped or not args or args[0] is not ctypes.c_void_p:
+            continue
+        vals = [None] + [t() if isinstance(t, type) and issubclass(t, ctypes._SimpleCData) else None for t in args[1:]]
+        rc = getattr(L, name)(*vals)
+        assert rc < 0, f"{name}(NULL, ...) returned {rc}"
+        checked += 1
+    assert checked >= 25
+    assert L.ipls_agg_close(None) == 0                     # closing nothing is a no-op
