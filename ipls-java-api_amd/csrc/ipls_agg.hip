@@ -154,12 +154,16 @@ int flush_pending(ipls_agg* h);
   std::lock_guard<std::mutex> lk_(h->mu);       \
   if (int rc_ = flush_pending(h)) return rc_
 
+// A failed call also leaves HIP's per-thread last error set; it is cleared
+// here so that the next launch check (hipGetLastError) does not report it.
 #define HIP_TRY(h, expr)                                                                \
   do {                                                                                  \
     hipError_t e_ = (expr);                                                             \
-    if (e_ != hipSuccess)                                                               \
+    if (e_ != hipSuccess) {                                                             \
+      (void)hipGetLastError();                                                          \
       return fail((h), e_ == hipErrorOutOfMemory ? IPLS_E_NOMEM : IPLS_E_DEVICE,        \
                   "%s failed: %s", #expr, hipGetErrorString(e_));                       \
+    }                                                                                   \
   } while (0)
 
 int64_t ref_chunk(int64_t m, int p) { return (int64_t)(int32_t)(m / p) + 1; }  // IPLS.java:1019
@@ -665,6 +669,7 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
   // new double[(int)_MODEL_SIZE/_PARTITIONS + 2] (Updater.java:162)
   h->gbuf_len = h->model_size > 0 ? (int64_t)((int32_t)h->model_size / h->P) + 2 : cfg->bucket_len;
   auto cleanup = [&](int code) {
+    (void)hipGetLastError();   // the failed call's error must not reach a later launch check
     ipls_agg_close(h);
     return code;
   };
@@ -672,6 +677,7 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipStreamCreate failed"));
   if (hipMalloc(&h->arena, (size_t)h->arena_elems * 8) != hipSuccess) {
+    (void)hipGetLastError();   // not sticky: the next launch check must not see it
     h->arena = nullptr;
     return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc of %lld-byte arena failed", (long long)h->arena_elems * 8));
   }
@@ -1513,7 +1519,10 @@ int ipls_checksum_dev(const void* src, int64_t n, int src_kind, uint64_t* out, v
   }
   hipStream_t st = (hipStream_t)stream;
   unsigned long long* d = nullptr;
-  if (hipMallocAsync((void**)&d, 8, st) != hipSuccess) return fail(nullptr, IPLS_E_NOMEM, "hipMallocAsync failed");
+  if (hipMallocAsync((void**)&d, 8, st) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(nullptr, IPLS_E_NOMEM, "hipMallocAsync failed");
+  }
   hipMemsetAsync(d, 0, 8, st);
   const dim3 g(std::max(1u, std::min<unsigned>(blocks_for(n, kBlock * 8), 2048)));
   if (src_kind == IPLS_DEV_BE)
@@ -1875,6 +1884,7 @@ int ipls_host_alloc(size_t bytes, void** ptr) {
   hipError_t e = hipHostMalloc(ptr, bytes, hipHostMallocDefault);
   if (e != hipSuccess) {
     *ptr = nullptr;
+    (void)hipGetLastError();
     return fail(nullptr, e == hipErrorNoDevice ? IPLS_E_NODEV : IPLS_E_NOMEM, "hipHostMalloc(%zu): %s", bytes,
                 hipGetErrorString(e));
   }
@@ -1884,7 +1894,10 @@ int ipls_host_alloc(size_t bytes, void** ptr) {
 int ipls_host_free(void* ptr) {
   if (!ptr) return IPLS_OK;
   hipError_t e = hipHostFree(ptr);
-  if (e != hipSuccess) return fail(nullptr, IPLS_E_INVAL, "hipHostFree: %s", hipGetErrorString(e));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(nullptr, IPLS_E_INVAL, "hipHostFree: %s", hipGetErrorString(e));
+  }
   return IPLS_OK;
 }
 

@@ -319,6 +319,73 @@ def test_errors(ipls, O):
     agg.close()
 
 
+def test_invalid_arguments_rejected_before_launch(ipls, O):
+    """Bad arguments at every C-ABI entry come back as negative codes before
+    any device work (so no kernel ever sees them), and the handle keeps its
+    state: the reference's exceptions leave PeerData intact too."""
+    import ctypes
+    from ipls import _native as N
+    lib = ipls.lib()
+    L = 1000
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    h = agg.handle
+    g = O.synth_bucket(L, 0, 1)
+    agg.Update(g, 0)
+    t = torch.from_numpy(np.asarray(g)).to("cuda")
+    torch.cuda.synchronize()
+    d = int(t.data_ptr())
+    P = ctypes.c_void_p
+    tab = (P * 2)(d, d)
+    nul = (P * 2)(d, None)
+    mis = (P * 2)(d, d + 4)
+    tk = ctypes.c_uint64()
+    out = np.zeros(2 * L)
+    msg = np.frombuffer(O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"Qm")), dtype=np.uint8)
+    mp = (P * 1)(msg.ctypes.data)
+    ml = (ctypes.c_int64 * 1)(msg.size)
+    cases = {
+        "reduce_batch p_first -1": lambda: lib.ipls_agg_reduce_batch(h, -1, 1, tab, 2, N.DEV_F64, N.START_ACCUM, N.TGT_AGG),
+        "reduce_batch past P": lambda: lib.ipls_agg_reduce_batch(h, 1, 2, tab, 1, N.DEV_F64, N.START_ACCUM, N.TGT_AGG),
+        "reduce_batch host kind": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, tab, 2, N.HOST_F64, N.START_ACCUM, N.TGT_AGG),
+        "reduce_batch start 7": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, tab, 2, N.DEV_F64, 7, N.TGT_AGG),
+        "reduce_batch target 9": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, tab, 2, N.DEV_F64, N.START_ACCUM, 9),
+        "reduce_batch k -1": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, tab, -1, N.DEV_F64, N.START_ACCUM, N.TGT_AGG),
+        "reduce_batch NULL table": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, None, 2, N.DEV_F64, N.START_ACCUM, N.TGT_AGG),
+        "reduce_batch NULL bucket": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, nul, 2, N.DEV_F64, N.START_ACCUM, N.TGT_AGG),
+        "reduce_batch 4-B aligned": lambda: lib.ipls_agg_reduce_batch(h, 0, 1, mis, 2, N.DEV_F64, N.START_ACCUM, N.TGT_AGG),
+        "accumulate p 2": lambda: lib.ipls_agg_accumulate(h, 2, N.TGT_AGG, d, L, N.DEV_F64),
+        "accumulate target 9": lambda: lib.ipls_agg_accumulate(h, 0, 9, d, L, N.DEV_F64),
+        "accumulate kind 99": lambda: lib.ipls_agg_accumulate(h, 0, N.TGT_AGG, d, L, 99),
+        "accumulate short": lambda: lib.ipls_agg_accumulate(h, 0, N.TGT_AGG, d, L - 1, N.DEV_F64),
+        "async 4-B aligned": lambda: lib.ipls_agg_accumulate_async(h, 0, N.TGT_AGG, d + 4, L, N.DEV_F64, ctypes.byref(tk)),
+        "async short": lambda: lib.ipls_agg_accumulate_async(h, 0, N.TGT_AGG, d, L - 1, N.DEV_F64, ctypes.byref(tk)),
+        "async NULL ticket": lambda: lib.ipls_agg_accumulate_async(h, 0, N.TGT_AGG, d, L, N.DEV_F64, None),
+        "async p -1": lambda: lib.ipls_agg_accumulate_async(h, -1, N.TGT_AGG, d, L, N.DEV_F64, ctypes.byref(tk)),
+        "wait unissued": lambda: lib.ipls_agg_wait(h, 1 << 40),
+        "finalize p 5": lambda: lib.ipls_agg_finalize(h, 5, None, N.HOST_BE, None),
+        "read kind 99": lambda: lib.ipls_agg_read(h, 0, N.TGT_AGG, out.ctypes.data, L, 99),
+        "read p 2": lambda: lib.ipls_agg_read(h, 2, N.TGT_AGG, out.ctypes.data, L, N.HOST_F64),
+        "ingest layers 3": lambda: lib.ipls_agg_ingest_pubsub(h, N.TGT_AGG, mp, ml, 1, 3, None, None),
+        "ingest n -1": lambda: lib.ipls_agg_ingest_pubsub(h, N.TGT_AGG, mp, ml, -1, 2, None, None),
+        "ingest target 9": lambda: lib.ipls_agg_ingest_pubsub(h, 9, mp, ml, 1, 2, None, None),
+        "blend target 9": lambda: lib.ipls_agg_blend(h, 0, 9, d, L, N.DEV_F64, 0.5, 0.5),
+        "promote p 4": lambda: lib.ipls_agg_promote_future(h, (ctypes.c_int32 * 1)(4), 1),
+        "reset p 3": lambda: lib.ipls_agg_reset(h, 3),
+    }
+    for name, call in cases.items():
+        rc = call()
+        assert rc < 0, f"{name}: rc {rc}"
+    for bad in (dict(n_partitions=0, bucket_len=10), dict(n_partitions=2, bucket_len=-5)):
+        with pytest.raises(ipls.IplsError):
+            ipls.Aggregator(**bad)
+    with pytest.raises(ipls.IplsError) as e:
+        ipls.Aggregator(n_partitions=1, bucket_len=1 << 46)    # 512 TiB arena
+    assert e.value.code == N.IPLS_E_NOMEM
+    agg.Update(g, 0)                          # state intact: exactly the two good folds
+    assert_bits_equal(agg.read(0), O.reduce([g, g], L), "after rejected calls")
+    agg.close()
+
+
 # ---------------------------------------------------------------------------
 # full-size configs: size-independent property (checksum of the fixed-order
 # sum, computed by the C oracle from the counter formula at build time)
