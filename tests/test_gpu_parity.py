@@ -1341,3 +1341,120 @@ def test_full_ipls_round_four_peers(ipls, O):
         assert_bits_equal(models[k], ref, f"model on peer {k}")
     for agg in peers:
         agg.close()
+
+
+@pytest.mark.parametrize("seed,group", [(1, 1), (2, 4), (3, 32), (4, 2), (5, 8)])
+def test_stateful_random_sequence(ipls, O, seed, group):
+    """A random sequence over the whole accumulator surface, checked step by
+    step against a numpy model of the Java state (Aggregated_Gradients,
+    Replicas_Gradients, Aggregated_Gradients_from_future, Weights): host and
+    device folds, queued folds (coalescing group 1/4/32), batched folds with
+    every start mode and byte order, AggregatePartition, resets, promotion of
+    future gradients, the async blend, cache_partition, the fused round and
+    GetPartitions.  Buckets include -0.0, subnormals and huge values so the
+    start-value and grouping rules show in the bits."""
+    rng = np.random.default_rng(seed)
+    P, L = 4, 5003
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg.set_coalesce(group)
+    pool = []
+    for k in range(10):
+        g = O.synth_bucket(L, 9, k) * (10.0 ** rng.integers(-3, 4))
+        g[rng.integers(0, L, 40)] = -0.0
+        g[rng.integers(0, L, 10)] = 5e-324
+        g[rng.integers(0, L, 5)] = rng.choice([1e300, -1e300, 1e16])
+        g[-1] = 1.0
+        pool.append(g)
+    dev = [torch.from_numpy(g).to("cuda") for g in pool]
+    dev_be = [torch.from_numpy(np.frombuffer(O.be_encode(g), dtype=np.uint8).copy()).to("cuda") for g in pool]
+    torch.cuda.synchronize()
+    D = [ipls.DeviceBuffer.from_tensor(t) for t in dev]
+    DB = [ipls.DeviceBuffer(int(t.data_ptr()), L, big_endian=True) for t in dev_be]
+    T = {ipls.TGT_AGG: "agg", ipls.TGT_REP: "rep", ipls.TGT_FUTURE: "fut", ipls.TGT_WEIGHTS: "w"}
+    M = {name: [np.zeros(L) for _ in range(P)] for name in T.values()}
+
+    def check(p, tg, what):
+        assert_bits_equal(agg.read(p, tg), M[T[tg]][p], f"step {what}: p{p} {T[tg]}")
+
+    for step in range(300):
+        op = int(rng.integers(0, 12))
+        p = int(rng.integers(0, P))
+        k = int(rng.integers(0, len(pool)))
+        g = pool[k]
+        if op == 0:                                         # Updater._Update from host bytes/doubles
+            tg = [ipls.TGT_AGG, ipls.TGT_REP][int(rng.integers(0, 2))]
+            if rng.integers(0, 2):
+                agg.Update(g, p, from_clients=tg == ipls.TGT_AGG)
+            else:
+                agg.Update(O.be_encode(g), p, from_clients=tg == ipls.TGT_AGG)
+            M[T[tg]][p] = M[T[tg]][p] + g
+        elif op == 1:                                       # from the future
+            agg.Update(g, p, from_future=True)
+            M["fut"][p] = M["fut"][p] + g
+        elif op in (2, 3):                                  # queued device folds
+            tg = [ipls.TGT_AGG, ipls.TGT_REP][op - 2]
+            agg.UpdateAsync(DB[k] if rng.integers(0, 3) == 0 else D[k], p, from_clients=tg == ipls.TGT_AGG)
+            M[T[tg]][p] = M[T[tg]][p] + g
+        elif op == 4:                                       # batched folds, any start mode
+            n = int(rng.integers(1, P - p + 1))
+            kk = int(rng.integers(1, 4))
+            ks = [[int(x) for x in rng.integers(0, len(pool), kk)] for _ in range(n)]
+            mode = [ipls.START_ZERO, ipls.START_ACCUM, ipls.START_FIRST][int(rng.integers(0, 3))]
+            be = bool(rng.integers(0, 2))
+            tg = [ipls.TGT_AGG, ipls.TGT_REP][int(rng.integers(0, 2))]
+            agg.reduce_batch(p, [[(DB if be else D)[j] for j in row] for row in ks], start_mode=mode, target=tg,
+                             big_endian=be)
+            for q, row in enumerate(ks):
+                bufs = [pool[j] for j in row]
+                M[T[tg]][p + q] = O.reduce(bufs, L, mode, acc=M[T[tg]][p + q])
+        elif op == 5:                                       # AggregatePartition
+            agg.AggregatePartition(p)
+            M["w"][p] = M["agg"][p] + M["rep"][p]
+            M["agg"][p] = np.zeros(L)
+            M["rep"][p] = np.zeros(L)
+        elif op == 6:                                       # reset one / all
+            if rng.integers(0, 3) == 0:
+                agg.reset()
+                qs = range(P)
+            else:
+                agg.reset(p)
+                qs = [p]
+            for q in qs:
+                M["agg"][q] = np.zeros(L)
+                M["rep"][q] = np.zeros(L)
+        elif op == 7:                                       # Update_Client_WaitAck_List
+            qs = sorted({int(x) for x in rng.integers(0, P, 2)})
+            agg.PromoteFuture(qs)
+            for q in qs:
+                M["agg"][q] = M["fut"][q]
+                M["fut"][q] = np.zeros(L)
+        elif op == 8:                                       # -async replica fold W = 0.75 W + g
+            agg.UpdateAsyncReplica(g, p)
+            M["w"][p] = O.blend(M["w"][p], g, 0.75, 1.0)
+        elif op == 9:                                       # cache_partition: GetParameters into W
+            n = int(rng.integers(1, L + 1))
+            agg.cache_partition(p, O.be_encode(g[:n]))
+            M["w"][p][:n] = g[:n]
+        elif op == 10:                                      # fused round over a range
+            n = int(rng.integers(1, P - p + 1))
+            kk = int(rng.integers(0, 3))
+            ks = [[int(x) for x in rng.integers(0, len(pool), kk)] for _ in range(n)]
+            avg = agg.aggregate_round(p, [[D[j] for j in row] for row in ks])
+            exp = []
+            for q, row in enumerate(ks):
+                a = O.reduce([pool[j] for j in row], L, ipls.START_ACCUM, acc=M["agg"][p + q]) if row \
+                    else M["agg"][p + q]
+                M["w"][p + q] = a + M["rep"][p + q]
+                M["agg"][p + q] = np.zeros(L)
+                M["rep"][p + q] = np.zeros(L)
+                exp.append(O.divide(M["w"][p + q]))
+            assert_bits_equal(avg, np.concatenate(exp), f"step {step}: fused round")
+        else:                                               # reads
+            for tg in T:
+                check(p, tg, step)
+        if step % 40 == 39:
+            assert_bits_equal(agg.GetPartitions(), O.get_partitions(M["w"]), f"step {step}: GetPartitions")
+    for p in range(P):
+        for tg in T:
+            check(p, tg, "end")
+    agg.close()
