@@ -182,6 +182,46 @@ int main(int argc, char** argv) {
                      alg, {}})
   const bool be_out = getenv("SWEEP_BE_OUT") != nullptr;
   const bool quick = getenv("SWEEP_QUICK") != nullptr;   // the shipped big shape and its neighbours only
+  // SWEEP_LAYOUTS=1: the shipped big kernel over other bucket layouts carved
+  // from the SAME arena (same physical pages), so only the virtual placement
+  // differs: pads of 0 / 32 / 64 / 512 / 4096 / 32768 doubles between buckets,
+  // peer-major slot order, and a random slot permutation (pad 32).
+  if (getenv("SWEEP_LAYOUTS") && !separate) {
+    const int64_t max_pad = (PAD - 32) > 0 ? PAD - 32 : 0;   // run with PAD >= the largest pad + 32
+    struct Lay { const char* name; int64_t pad; int order; };
+    static const Lay lays[] = {{"layout pad 0", 0, 0},      {"layout pad 32 (shipped)", 32, 0},
+                               {"layout pad 64", 64, 0},    {"layout pad 512", 512, 0},
+                               {"layout pad 4096", 4096, 0}, {"layout pad 32768", 32768, 0},
+                               {"layout pad 32 peer-major", 32, 1}, {"layout pad 32 shuffled", 32, 2}};
+    std::vector<int> perm(P * K);
+    for (int i = 0; i < P * K; ++i) perm[i] = i;
+    unsigned long long x = 88172645463325252ULL;
+    for (int i = P * K - 1; i > 0; --i) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      std::swap(perm[i], perm[(int)(x % (unsigned long long)(i + 1))]);
+    }
+    for (const Lay& ly : lays) {
+      if (ly.pad > max_pad) continue;
+      std::vector<const unsigned long long*> lp(P * K);
+      for (int p = 0; p < P; ++p)
+        for (int k = 0; k < K; ++k) {
+          const int i = p * K + k;
+          const int slot = ly.order == 0 ? i : ly.order == 1 ? k * P + p : perm[i];
+          lp[i] = base + (int64_t)slot * (L + ly.pad);
+        }
+      const unsigned long long** d_lp;
+      CK(hipMalloc(&d_lp, lp.size() * 8));
+      CK(hipMemcpy(d_lp, lp.data(), lp.size() * 8, hipMemcpyHostToDevice));
+      vars.push_back(Var{ly.name,
+                         [=](hipStream_t s) {
+                           const int64_t tile = (int64_t)1024 * 2 * 16;
+                           const int tpp = (int)((L + tile - 1) / tile);
+                           hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, 16, true, 0, 1024>), dim3(tpp * P),
+                                              dim3(1024), 0, s, (const unsigned long long* const*)d_lp, d_pd, K, tpp, P);
+                         },
+                         alg, {}});
+    }
+  }
   ADDC(1, 8, 0, 1024);
   ADDC(1, 16, 0, 1024);
   ADDC(1, 16, 2, 1024);
