@@ -161,6 +161,10 @@ int ipls_agg_accumulate_async(ipls_agg *h, int p, int target, const void *src, i
 /* Wait until fold `ticket` (and every fold queued before it) has finished. */
 int ipls_agg_wait(ipls_agg *h, uint64_t ticket);
 
+/* Launch the folds of every queued asynchronous device bucket now, without
+ * waiting for them (for example when the Updater's queue runs dry). */
+int ipls_agg_flush(ipls_agg *h);
+
 /* Coalescing group g (>= 1; 1 = fold each arrival at once) of asynchronous
  * device buckets: the queues are flushed when they average g buckets per
  * partition or one of them holds 2g.  Device traffic per element is

@@ -768,6 +768,12 @@ int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
   return IPLS_OK;
 }
 
+int ipls_agg_flush(ipls_agg* h) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  IPLS_LOCK(h);   // launches the queued folds; does not wait for them
+  return IPLS_OK;
+}
+
 int ipls_agg_set_coalesce(ipls_agg* h, int max_group) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);

@@ -19,6 +19,7 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -366,7 +367,10 @@ class UpdaterThread {
     bool device_big_endian = false;
   };
 
-  explicit UpdaterThread(IPLS& ipls) : ipls_(ipls), th_([this] { loop(); }) {}
+  // idle_flush: when no request arrives for this long, the queued device
+  // buckets are folded (ipls_agg_flush) instead of waiting for the queues to fill.
+  explicit UpdaterThread(IPLS& ipls, std::chrono::microseconds idle_flush = std::chrono::microseconds(200))
+      : ipls_(ipls), idle_flush_(idle_flush), th_([this] { loop(); }) {}
   ~UpdaterThread() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -406,7 +410,17 @@ class UpdaterThread {
       Request r;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+        auto ready = [this] { return stop_ || !q_.empty(); };
+        if (!cv_.wait_for(lk, idle_flush_, ready)) {
+          if (queued_) {   // the queue ran dry: start the queued folds
+            queued_ = false;
+            lk.unlock();
+            const int rc = ipls_agg_flush(ipls_.handle());
+            lk.lock();
+            if (rc < 0) failures_.push_back(ipls_agg_last_error(ipls_.handle()));
+          }
+          cv_.wait(lk, ready);
+        }
         if (q_.empty()) return;   // stop_ and nothing left
         r = std::move(q_.front());
         q_.pop_front();
@@ -417,6 +431,8 @@ class UpdaterThread {
           check(ipls_agg_accumulate_async(ipls_.handle(), r.partition, r.from_clients ? IPLS_TGT_AGG : IPLS_TGT_REP,
                                           r.device, r.device_n, r.device_big_endian ? IPLS_DEV_BE : IPLS_DEV_F64, &t),
                 ipls_.handle());
+          std::lock_guard<std::mutex> lk(mu_);
+          queued_ = true;
         } else if (!r.gradient.empty()) {
           u._Update(&r.gradient, r.partition, r.from_clients);
         } else if (!r.file.empty()) {
@@ -435,10 +451,11 @@ class UpdaterThread {
   }
 
   IPLS& ipls_;
+  std::chrono::microseconds idle_flush_;
   std::mutex mu_;
   std::condition_variable cv_, idle_;
   std::deque<Request> q_;
-  bool stop_ = false;
+  bool stop_ = false, queued_ = false;
   uint64_t put_n_ = 0, done_n_ = 0;
   std::vector<std::string> failures_;
   std::thread th_;   // last: starts after every member above exists

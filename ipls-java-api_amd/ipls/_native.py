@@ -81,6 +81,7 @@ SIGNATURES = {
     "ipls_agg_accumulate_async": (_i, [_vp, _i, _i, _vp, _i64, _i, _P(_u64)]),
     "ipls_agg_wait": (_i, [_vp, _u64]),
     "ipls_agg_set_coalesce": (_i, [_vp, _i]),
+    "ipls_agg_flush": (_i, [_vp]),
     "ipls_agg_other_replica": (_i, [_vp, _i, _i32, _vp, _i64, _i]),
     "ipls_agg_collect_replicas": (_i, [_vp, _P(_i32)]),
     "ipls_agg_ingest_pubsub": (_i, [_vp, _i, _P(_vp), _P(_i64), _i, _i, _P(_i32), _P(_i32)]),

@@ -218,6 +218,10 @@ class Aggregator:
                                                       N.HOST_BE if big_endian else N.HOST_F64, ctypes.byref(t)))
         return t.value
 
+    def flush(self):
+        """Launch the folds of every queued device bucket now (no wait)."""
+        self._chk(self._lib.ipls_agg_flush(self._h))
+
     def set_coalesce(self, max_group: int):
         """Largest group of queued device buckets folded per partition in one launch."""
         self._chk(self._lib.ipls_agg_set_coalesce(self._h, max_group))

@@ -8,6 +8,7 @@
 // ETHModel (config A) is read from tests/golden/ethmodel.f64be.gz via zlib.
 #include <zlib.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -253,6 +254,7 @@ int main(int argc, char** argv) {
             }
             seq[p].push_back(g);
             ut.put(std::move(r));
+            if (j % 7 == 6) std::this_thread::sleep_for(std::chrono::milliseconds(1));   // idle: queued folds start
             if (t == 0 && j == 11) {
               UpdaterThread::Request bad;
               bad.partition = 0;
