@@ -72,6 +72,11 @@ public final class NativeAggregator implements AutoCloseable {
         waitTicket(handle, ticket);
     }
 
+    /** Start the folds of queued device buckets now (Updater.run when queue.isEmpty()). */
+    public void flush() {
+        flushQueued(handle);
+    }
+
     /** Updater.java:99-101: a client's bucket for a later iteration. */
     public void updateFromFuture(double[] gradient, int p) {
         if (gradient != null) accumulate(handle, p, TGT_FUTURE, gradient);
@@ -170,6 +175,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
     private static native long accumulateAsyncDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
     private static native void waitTicket(long h, long ticket);
+    private static native void flushQueued(long h);
     private static native void accumulateFrame(long h, int p, int target, byte[] frame);
     private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, long nBytes);
     private static native void finalizePartition(long h, int p, byte[] sumOut);

@@ -118,6 +118,11 @@ JNIEXPORT void JNICALL Java_NativeAggregator_waitTicket(JNIEnv *env, jclass c, j
     CHECK(ipls_agg_wait(H(h), (uint64_t)ticket), H(h));
 }
 
+JNIEXPORT void JNICALL Java_NativeAggregator_flushQueued(JNIEnv *env, jclass c, jlong h) {
+    (void)c;
+    CHECK(ipls_agg_flush(H(h)), H(h));
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                               jobject buf, jlong nBytes) {
     (void)c;
