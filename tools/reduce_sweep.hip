@@ -240,6 +240,31 @@ int main(int argc, char** argv) {
                          hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, R, true, MAP, 1024, F>), grid, dim3(1024), 0, s, bp, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
+#define ADDSB(R, BS, F)                                                                           \
+  vars.push_back(Var{"reduce R=" #R " MAP=0 BS=" #BS " SEQF=" #F,                                  \
+                     [=](hipStream_t s) {                                                       \
+                       const int64_t tile = (int64_t)BS * 2 * R;                                \
+                       const int tpp = (int)((L + tile - 1) / tile);                            \
+                       const dim3 grid((unsigned)grid_blocks(0, (int64_t)tpp * P));             \
+                       auto bp = (const unsigned long long* const*)d_ptrs;                      \
+                       if (be && be_out)                                                        \
+                         hipLaunchKernelGGL((k_reduce<true, true, kZero, 1, R, true, 0, BS, F>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                       else if (be)                                                             \
+                         hipLaunchKernelGGL((k_reduce<true, false, kZero, 1, R, true, 0, BS, F>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                       else                                                                     \
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, R, true, 0, BS, F>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                     },                                                                         \
+                     alg, {}})
+  if (getenv("SWEEP_BS")) {   // block size / fence interval of the big-endian fold
+    ADDSB(16, 1024, 2);
+    ADDSB(16, 512, 2);
+    ADDSB(16, 256, 2);
+    ADDSB(16, 256, 0);
+    ADDSB(16, 512, 0);
+    ADDSB(32, 256, 2);
+    ADDSB(32, 256, 4);
+  }
+#undef ADDSB
   if (quick) {             // fence interval of the SEQ schedule (0 = hipcc's own)
     ADDS(16, 0, 0);
     ADDS(16, 0, 1);
