@@ -303,6 +303,61 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
             "verified_checksum_p0": verified}
 
 
+def config_a_leg(ipls, reps: int = 20) -> dict:
+    """BASELINE configs[0], the reference's own CPU-runnable case: ETHModel
+    (M = 443,610, tests/golden/ethmodel.f64be.gz), -pa 3 -n 3, three peers.
+    One round as the Java API runs it: UpdateGradient of this peer's
+    gradients (IPLS.java:1737), the two other peers' partitions arriving as
+    `ipfs cat` BE bytes (Updater._Update), AggregatePartition for the three
+    partitions and GetPartitions -- host memory in, host memory out.  Beside
+    it the CPU port of the reference's loop on the same bytes (BE decode +
+    fold per bucket, then the divide; 1 thread).  The averaged models must be
+    bit-identical.  A latency line (14 MB of buckets), never the value."""
+    import gzip
+    from oracle import oracle as O   # checker + the CPU port timed beside the GPU round
+    raw = gzip.decompress((Path(__file__).resolve().parent / "tests" / "golden" / "ethmodel.f64be.gz").read_bytes())
+    model = np.frombuffer(raw, dtype=">f8").astype(np.float64)
+    M, P = model.size, 3
+    peers = [model + O.synth_bucket(M + 1, 0, k)[:M] for k in range(3)]
+    parts = [O.organize_gradients(g, M, P) for g in peers]
+    be = [[np.frombuffer(O.be_encode(parts[k][p]), dtype=np.uint8) for p in range(P)] for k in range(3)]
+    agg = ipls.Aggregator(M, P, max_peers=3)
+
+    def gpu_round():
+        agg.UpdateGradient(peers[0], auth_list=[0, 1, 2])
+        for k in (1, 2):
+            for p in range(P):
+                agg.Update(be[k][p].tobytes(), p)
+        for p in range(P):
+            agg.AggregatePartition(p)
+        return agg.GetPartitions()
+
+    def cpu_round():
+        out = []
+        for p in range(P):
+            s = O.c_updater_loop([be[k][p] for k in range(3)], len(parts[0][p]))
+            out.append(O.c_divide(s))
+        return np.concatenate(out)
+
+    got, want = gpu_round(), cpu_round()
+    same = bool(np.array_equal(got.view(np.int64), want.view(np.int64)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gpu_round()
+    g_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        cpu_round()
+    c_ms = (time.perf_counter() - t0) / reps * 1e3
+    agg.close()
+    return {"workload": "A: ETHModel M=443,610, -pa 3 -n 3, 3 peers (host buffers in, averaged model out)",
+            "gpu_round_ms": round(g_ms, 3), "cpu_port_round_ms": round(c_ms, 3), "cpu_port_cores": 1,
+            "bit_identical": same,
+            "note": f"wall time per round, mean of {reps}; GPU = Python caller through the C-ABI (H2D of 9 BE "
+                    "buckets + own gradients, folds, AggregatePartition, divide, D2H of the model); CPU = the C "
+                    "port of the Updater BE decode + fold and the GetPartitions divide"}
+
+
 def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, verify: bool, reps: int = 3) -> dict:
     """The headline workload folded the way Updater._Update folds its queue
     (Updater.java:115-117): one call per arriving bucket, peers arriving in
@@ -551,6 +606,7 @@ def main():
             torch.cuda.empty_cache()
             out["other_configs"] = {nm: config_leg(ipls, torch, nm, be, local, verify=not args.no_verify)
                                     for nm, be in (("B", False), ("D", True))}
+            out["other_configs"]["A"] = config_a_leg(ipls)
     dog = None
     printed = []
     if world > 1 and not args.no_replica_leg and not args.be:
