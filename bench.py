@@ -258,7 +258,8 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
     """One more BASELINE config on the same box, N=1: B
     (16 x 1M x 8, native doubles) or D (64 x 4M x 32) with big-endian IPFS
     bytes in and the sum packed to big-endian bytes out, i.e. config D's
-    'double<->byte pack/unpack in the timed region'.  Same algorithmic-bytes
+    'double<->byte pack/unpack in the timed region', or F (one GPU's slice of
+    config F: 16 x 8M x 64, 69.8 GB of buckets resident).  Same algorithmic-bytes
     accounting as the headline; kernel time by HIP events on the handle's
     stream; partition 0 checked against the oracle's checksum."""
     P, L, K = CONFIGS[name]
@@ -605,7 +606,7 @@ def main():
             del arena, rows
             torch.cuda.empty_cache()
             out["other_configs"] = {nm: config_leg(ipls, torch, nm, be, local, verify=not args.no_verify)
-                                    for nm, be in (("B", False), ("D", True))}
+                                    for nm, be in (("B", False), ("D", True), ("F", False))}
             out["other_configs"]["A"] = config_a_leg(ipls)
     dog = None
     printed = []
