@@ -595,19 +595,25 @@ def main():
         }
         if round_info:
             out["round"] = round_info
+        def side(fn, *a, **kw):
+            # a side measurement never costs the headline line: its failure is reported in place
+            try:
+                return fn(*a, **kw)
+            except Exception as e:   # noqa: BLE001
+                return {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.be and not args.no_per_arrival:
-            out["per_arrival"] = per_arrival_leg(ipls, torch, agg, rows, P, L, K, stream, not args.no_verify)
+            out["per_arrival"] = side(per_arrival_leg, ipls, torch, agg, rows, P, L, K, stream, not args.no_verify)
         if world == 1 and not args.no_e2e:
-            out["host_inclusive"] = host_inclusive(ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
+            out["host_inclusive"] = side(host_inclusive, ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(L, K, args.cpu_passes)
+            out["cpu_baseline"] = side(cpu_baseline, L, K, args.cpu_passes)
         if world == 1 and not args.no_other_configs and args.config == "C" and not args.be:
             # the other single-GPU BASELINE configs, measured in the same run (never the value)
             del arena, rows
             torch.cuda.empty_cache()
-            out["other_configs"] = {nm: config_leg(ipls, torch, nm, be, local, verify=not args.no_verify)
+            out["other_configs"] = {nm: side(config_leg, ipls, torch, nm, be, local, verify=not args.no_verify)
                                     for nm, be in (("B", False), ("D", True), ("F", False))}
-            out["other_configs"]["A"] = config_a_leg(ipls)
+            out["other_configs"]["A"] = side(config_a_leg, ipls)
     dog = None
     printed = []
     if world > 1 and not args.no_replica_leg and not args.be:
