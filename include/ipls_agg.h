@@ -294,10 +294,15 @@ int ipls_agg_promote_future(ipls_agg *h, const int32_t *parts, int n_parts);
 /* Zero AGG[p] and REP[p] (IPLS.java:1268-1269); p may be IPLS_ALL_PARTITIONS. */
 int ipls_agg_reset(ipls_agg *h, int p);
 
-/* Device address of an accumulator (for RCCL send/recv of replica partials). */
+/* Device address of an accumulator (for RCCL send/recv of replica partials).
+ * Work the caller orders on the handle's stream sees the folds of every call
+ * made so far -- except device buckets still queued by
+ * ipls_agg_accumulate_async: call ipls_agg_flush (or any other entry point)
+ * before reading the accumulator through this address. */
 int ipls_agg_device_ptr(ipls_agg *h, int p, int target, void **ptr);
 
-/* The handle's HIP stream (hipStream_t as void*) and a host wait on it. */
+/* The handle's HIP stream (hipStream_t as void*) and a host wait on it
+ * (ipls_agg_sync also folds queued device buckets first). */
 void *ipls_agg_stream(ipls_agg *h);
 int ipls_agg_sync(ipls_agg *h);
 
