@@ -1376,8 +1376,11 @@ def test_stateful_random_sequence(ipls, O, seed, group):
     def check(p, tg, what):
         assert_bits_equal(agg.read(p, tg), M[T[tg]][p], f"step {what}: p{p} {T[tg]}")
 
+    gbuf = np.zeros(L)          # the Updater's one Gradient_Buff (synthetic geometry: L doubles)
+    store = {}                  # Other_Replica_Gradients
+    msgs = [O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmS")) for g in pool]
     for step in range(300):
-        op = int(rng.integers(0, 12))
+        op = int(rng.integers(0, 17))
         p = int(rng.integers(0, P))
         k = int(rng.integers(0, len(pool)))
         g = pool[k]
@@ -1449,7 +1452,32 @@ def test_stateful_random_sequence(ipls, O, seed, group):
                 M["rep"][p + q] = np.zeros(L)
                 exp.append(O.divide(M["w"][p + q]))
             assert_bits_equal(avg, np.concatenate(exp), f"step {step}: fused round")
-        else:                                               # reads
+        elif op == 12:                                      # ThreadReceiver: pubsub text -> frame -> fold
+            n, st = agg.ingest_pubsub([msgs[k]], partitions=[p])
+            assert n == 1 and st == [0]
+            M["agg"][p] = M["agg"][p] + g
+        elif op == 13:                                      # Updater.run, hash-only: GetParameters(hash, Gradient_Buff)
+            n = int(rng.integers(1, L + 1))
+            agg.UpdateIndirect(O.be_encode(g[:n]), p)
+            gbuf[:n] = g[:n]
+            M["agg"][p] = M["agg"][p] + gbuf
+        elif op == 14:                                      # Download_Scheduler: another aggregator's bucket
+            a = int(rng.integers(0, 3))
+            agg.OtherReplicaGradients(p, a, g)
+            O.other_replica_add(store, p, a, g)
+        elif op == 15:                                      # Collect_Replicas
+            n, part = agg.Collect_Replicas()
+            exp_part = [0] * P
+            assert n == O.collect_replicas(M["rep"], store, exp_part)
+            assert part == exp_part
+        else:                                               # -async publish / leaving peer
+            if rng.integers(0, 2):
+                agg.AsyncPublishScale(p)
+                M["agg"][p] = O.scale(M["w"][p], 0.25)
+            else:
+                agg.UpdateLeavingPeer(g, p)
+                M["w"][p] = O.blend(M["w"][p], g, 0.6, 1 - 0.6)
+        if op == 11 or step % 25 == 24:                     # reads
             for tg in T:
                 check(p, tg, step)
         if step % 40 == 39:
