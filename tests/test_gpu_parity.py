@@ -1344,7 +1344,7 @@ def test_full_ipls_round_four_peers(ipls, O):
 
 
 @pytest.mark.parametrize("seed,group", [(1, 1), (2, 4), (3, 32), (4, 2), (5, 8)])
-def test_stateful_random_sequence(ipls, O, seed, group):
+def test_stateful_random_sequence(ipls, O, seed, group, P=4, L=5003):
     """A random sequence over the whole accumulator surface, checked step by
     step against a numpy model of the Java state (Aggregated_Gradients,
     Replicas_Gradients, Aggregated_Gradients_from_future, Weights): host and
@@ -1354,7 +1354,6 @@ def test_stateful_random_sequence(ipls, O, seed, group):
     GetPartitions.  Buckets include -0.0, subnormals and huge values so the
     start-value and grouping rules show in the bits."""
     rng = np.random.default_rng(seed)
-    P, L = 4, 5003
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     agg.set_coalesce(group)
     pool = []
