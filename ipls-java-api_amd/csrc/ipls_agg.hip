@@ -418,7 +418,7 @@ void launch_reduce_fin(bool be_in, int start, int secure, int64_t maxL, int n_pa
                        const unsigned long long* const* bufs, const PartDesc* parts, int k, double* cnts) {
 #define FIN(BI, ST)                                                                                   \
   do {                                                                                                \
-    hipLaunchKernelGGL((k_round_counts<BI, ST>), dim3((n_parts + kBlock - 1) / kBlock), dim3(kBlock), 0, st, \
+    hipLaunchKernelGGL((k_round_counts<BI, ST>), dim3(n_parts), dim3(64), 0, st,                     \
                        bufs, parts, k, n_parts, cnts);                                                 \
     launch_reduce_v<BI, false, ST, true>(maxL, n_parts, st, bufs, parts, k, secure, cnts);           \
   } while (0)

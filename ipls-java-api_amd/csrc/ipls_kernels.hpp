@@ -390,21 +390,30 @@ __global__ __launch_bounds__(kBlock) void k_fold_n(unsigned long long* __restric
   }
 }
 
-// Count slot of a fused round, per partition (one lane each): the same fold
-// k_round applies to element L-1, i.e. W[L-1] =
+// Count slot of a fused round, one wave per partition: the same fold k_round
+// applies to element L-1, i.e. W[L-1] =
 // (init[L-1] | +0.0) + b_0[L-1] + ... + b_{k-1}[L-1] + (REP[L-1] | +0.0).
+// Lane j loads b_j[L-1] (64 independent loads in flight instead of a chain of
+// k pointer + value loads), then every lane adds the broadcast values in peer
+// order -- the identical expression, so the identical bits.
 template <bool BE_IN, int START>
-__global__ __launch_bounds__(kBlock) void k_round_counts(const unsigned long long* const* __restrict__ bufs,
-                                                         const PartDesc* __restrict__ parts, int k, int n_parts,
-                                                         double* __restrict__ cnts) {
-  const int q = blockIdx.x * kBlock + threadIdx.x;
+__global__ __launch_bounds__(64) void k_round_counts(const unsigned long long* const* __restrict__ bufs,
+                                                     const PartDesc* __restrict__ parts, int k, int n_parts,
+                                                     double* __restrict__ cnts) {
+  const int q = blockIdx.x;
   if (q >= n_parts) return;
+  const int lane = threadIdx.x;
   const PartDesc d = parts[q];
   const int64_t e = d.len - 1;
   const unsigned long long* const* pb = bufs + (size_t)q * k;
   double c = (START == kZero) ? 0.0 : __builtin_bit_cast(double, ld8(d.init + e));
-  for (int jj = 0; jj < k; ++jj) c = c + decode1<BE_IN>(ld8(pb[jj] + e));
-  cnts[q] = c + (d.rep ? __builtin_bit_cast(double, ld8(d.rep + e)) : 0.0);
+  for (int j0 = 0; j0 < k; j0 += 64) {
+    const int j = j0 + lane;
+    const double v = j < k ? decode1<BE_IN>(ld8(pb[j] + e)) : 0.0;
+    const int m = k - j0 < 64 ? k - j0 : 64;
+    for (int t = 0; t < m; ++t) c = c + __shfl(v, t);
+  }
+  if (lane == 0) cnts[q] = c + (d.rep ? __builtin_bit_cast(double, ld8(d.rep + e)) : 0.0);
 }
 
 // Same fold for buckets that are only 8-byte aligned (e.g. a device view into
