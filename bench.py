@@ -614,6 +614,11 @@ def main():
             out["other_configs"] = {nm: side(config_leg, ipls, torch, nm, be, local, verify=not args.no_verify)
                                     for nm, be in (("B", False), ("D", True), ("F", False))}
             out["other_configs"]["A"] = side(config_a_leg, ipls)
+            if isinstance(out["other_configs"]["F"], dict) and not args.no_e2e:
+                # config F is the end-to-end case: its buckets start as host IPFS bytes
+                _, LF, KF = CONFIGS["F"]
+                out["other_configs"]["F"]["host_inclusive"] = side(host_inclusive, ipls, ipls.Aggregator, LF, KF, 2,
+                                                                   local)
     dog = None
     printed = []
     if world > 1 and not args.no_replica_leg and not args.be:
