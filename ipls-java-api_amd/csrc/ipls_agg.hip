@@ -92,6 +92,16 @@ struct ipls_agg {
   hipStream_t copy_stream[kCopyThreads] = {};
   hipEvent_t ingest_ev = nullptr;
   std::vector<hipEvent_t> msg_ev;
+  // Per-arrival staging of pageable buckets, double-buffered: bucket k+1 is
+  // copied into one slot while the fold of bucket k still reads the other.
+  struct StageSlot {
+    void* d = nullptr;
+    size_t cap = 0;
+    hipEvent_t free_ev = nullptr;   // recorded after the fold that reads the slot
+    bool pending = false;
+  };
+  StageSlot stage[2];
+  int stage_next = 0;
   // Asynchronous folds (ipls_agg_accumulate_async).  Device buckets are not
   // folded on arrival: per (target, partition) their pointers queue up and the
   // next flush folds each queue in one launch, in call order -- the same
@@ -297,6 +307,47 @@ int stage_h2d(ipls_agg* h, void* dst, const void* src, size_t bytes) {
   HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(h, hipEventRecord(h->copy_ev, h->stream));
   HIP_TRY(h, hipEventSynchronize(h->copy_ev));
+  return IPLS_OK;
+}
+
+// Host-synchronous H2D copy of a pageable buffer on a copy stream: no
+// ordering against `stream` (the caller owns `dst`), so it overlaps the fold
+// of the previous arrival.  (Splitting it over two threads measured within
+// noise at 32 MiB and +1.6 % at 64 MiB, profiles/r01/host_e2e_pageable_split.txt.)
+int copy_pageable(ipls_agg* h, void* dst, const void* src, size_t bytes) {
+  if (!h->copy_stream[0]) HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream[0], hipStreamNonBlocking));
+  HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->copy_stream[0]));
+  HIP_TRY(h, hipStreamSynchronize(h->copy_stream[0]));
+  return IPLS_OK;
+}
+
+// Stage one pageable per-arrival bucket into the next of the two staging
+// slots; release_stage() marks the slot busy until the fold queued after it.
+int stage_bucket(ipls_agg* h, const void* src, size_t bytes, const void** dptr) {
+  ipls_agg::StageSlot& sl = h->stage[h->stage_next];
+  if (sl.pending) {   // the fold that read this slot two arrivals ago
+    HIP_TRY(h, hipEventSynchronize(sl.free_ev));
+    sl.pending = false;
+  }
+  if (sl.cap < bytes) {
+    if (sl.d) HIP_TRY(h, hipFree(sl.d));
+    sl.d = nullptr;
+    sl.cap = 0;
+    const size_t cap = (size_t)align_up((int64_t)bytes, 1 << 20);
+    HIP_TRY(h, hipMalloc(&sl.d, cap));
+    sl.cap = cap;
+  }
+  if (!sl.free_ev) HIP_TRY(h, hipEventCreateWithFlags(&sl.free_ev, hipEventDisableTiming));
+  if (int rc = copy_pageable(h, sl.d, src, bytes)) return rc;
+  *dptr = sl.d;
+  return IPLS_OK;
+}
+
+int release_stage(ipls_agg* h) {
+  ipls_agg::StageSlot& sl = h->stage[h->stage_next];
+  HIP_TRY(h, hipEventRecord(sl.free_ev, h->stream));
+  sl.pending = true;
+  h->stage_next ^= 1;
   return IPLS_OK;
 }
 
@@ -706,6 +757,10 @@ int ipls_agg_close(ipls_agg* h) {
       hipStreamSynchronize(cs);
       hipStreamDestroy(cs);
     }
+  for (auto& sl : h->stage) {
+    if (sl.d) hipFree(sl.d);
+    if (sl.free_ev) hipEventDestroy(sl.free_ev);
+  }
   if (h->ingest_ev) hipEventDestroy(h->ingest_ev);
   for (hipEvent_t e : h->msg_ev) hipEventDestroy(e);
   for (auto& b : h->batches) hipEventDestroy(b.ev);
@@ -862,7 +917,7 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
   HIP_TRY(h, hipSetDevice(h->device));
   const int64_t L = h->len[p];
   const void* dptr = nullptr;
-  bool be = false;
+  bool be = false, staged = false;
   switch (src_kind) {
     case IPLS_DEV_F64:
     case IPLS_DEV_BE:
@@ -885,9 +940,8 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
         HIP_TRY(h, hipStreamSynchronize(h->stream));
         return IPLS_OK;
       }
-      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
-      if (int rc = stage_h2d(h, h->d_scratch, src, (size_t)L * 8)) return rc;
-      dptr = h->d_scratch;
+      if (int rc = stage_bucket(h, src, (size_t)L * 8, &dptr)) return rc;
+      staged = true;
       break;
     }
     case IPLS_HOST_FRAME: {
@@ -898,10 +952,9 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
       if (nd < 0) return fail(h, IPLS_E_FORMAT, "malformed frame (BufferUnderflowException)");
       if (nd == 0) return IPLS_OK;  // arr_len == 0 -> Gradients = null (MyIPFSClass.java:1449-1451)
       if (int rc = host_decode_count(src_kind, nd, L, h)) return rc;
-      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
       // The payload starts at byte 14 (unaligned); staging realigns it.
-      if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
-      dptr = h->d_scratch;
+      if (int rc = stage_bucket(h, (const char*)src + poff, (size_t)L * 8, &dptr)) return rc;
+      staged = true;
       be = true;
       break;
     }
@@ -913,9 +966,8 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
       const int64_t nd = javaser::parse_pair((const uint8_t*)src, n, &workers, &poff, &why);
       if (nd < 0) return fail(h, IPLS_E_FORMAT, "partial update: %s (ObjectInputStream)", why ? why : "malformed");
       if (int rc = host_decode_count(src_kind, nd, L, h)) return rc;
-      if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
-      if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
-      dptr = h->d_scratch;
+      if (int rc = stage_bucket(h, (const char*)src + poff, (size_t)L * 8, &dptr)) return rc;
+      staged = true;
       be = true;
       break;
     }
@@ -923,7 +975,8 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
       return fail(h, IPLS_E_INVAL, "bad src_kind %d", src_kind);
   }
   const void* bl[1] = {dptr};
-  return reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target);
+  if (int rc = reduce_dev(h, p, 1, bl, 1, be, IPLS_START_ACCUM, target)) return rc;
+  return staged ? release_stage(h) : IPLS_OK;
 }
 
 int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind,
