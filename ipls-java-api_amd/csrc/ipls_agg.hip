@@ -1053,13 +1053,14 @@ int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, 
       dsrc = alias;
       zero_copy = true;
     } else {
-      if (int rc = ensure_scratch(h, (size_t)nw * 8)) return rc;
-      if (int rc = stage_h2d(h, h->d_scratch, bytes, (size_t)nw * 8)) return rc;
-      dsrc = h->d_scratch;
+      // double-buffered like the per-arrival buckets (stage_bucket)
+      if (int rc = stage_bucket(h, bytes, (size_t)nw * 8, &dsrc)) return rc;
     }
     hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(nw, kBlock), 4096)), dim3(kBlock), 0,
                        h->stream, (const unsigned long long*)dsrc, h->d_gbuf, nw);
     HIP_TRY(h, hipGetLastError());
+    if (!zero_copy)
+      if (int rc = release_stage(h)) return rc;
   }
   if (nd > G) {
     if (zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
