@@ -255,6 +255,16 @@ int main(int argc, char** argv) {
                          hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, R, true, 0, BS, F>), grid, dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
                      },                                                                         \
                      alg, {}})
+  if (be) {   // the native-double kernel on the same bytes (values do not change the timing)
+    vars.push_back(Var{"f64 kernel on the same buckets R=16",
+                       [=](hipStream_t s) {
+                         const int64_t tile = (int64_t)1024 * 2 * 16;
+                         const int tpp = (int)((L + tile - 1) / tile);
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, 16, true, 0, 1024>), dim3(tpp * P),
+                                            dim3(1024), 0, s, (const unsigned long long* const*)d_ptrs, d_pd, K, tpp, P);
+                       },
+                       alg, {}});
+  }
   if (getenv("SWEEP_BS")) {   // block size / fence interval of the big-endian fold
     ADDSB(16, 1024, 2);
     ADDSB(16, 512, 2);
