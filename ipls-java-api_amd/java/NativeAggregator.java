@@ -119,6 +119,15 @@ public final class NativeAggregator implements AutoCloseable {
         accumulateFrame(handle, p, fromClients ? TGT_AGG : TGT_REP, frame);
     }
 
+    /** ThreadReceiver.run/process (IPLS.java:851-866, 453-465): pubsub 'data' texts
+     *  (base64url x layers of Marshall_Packet frames) decoded, parsed and folded on the
+     *  GPU in message order; partitions may be null (the frame's own field is used).
+     *  status[i]: 0 folded, 1 null gradient, negative = the dropped message's exception
+     *  (include/ipls_agg.h).  Returns the number of messages folded. */
+    public int ingestPubsub(byte[][] texts, int layers, int[] partitions, boolean fromClients, int[] status) {
+        return ingestTexts(handle, fromClients ? TGT_AGG : TGT_REP, texts, layers, partitions, status);
+    }
+
     /** AggregatePartition (IPLS.java:1248-1274); returns the commit_update file bytes. */
     public byte[] aggregatePartition(int p) {
         byte[] sum = new byte[8 * partitionLength(p)];
@@ -176,6 +185,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native long accumulateAsyncDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
     private static native void waitTicket(long h, long ticket);
     private static native void flushQueued(long h);
+    private static native int ingestTexts(long h, int target, byte[][] msgs, int layers, int[] parts, int[] status);
     private static native void accumulateFrame(long h, int p, int target, byte[] frame);
     private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, long nBytes);
     private static native void finalizePartition(long h, int p, byte[] sumOut);

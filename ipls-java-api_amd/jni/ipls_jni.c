@@ -140,6 +140,45 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulateFrame(JNIEnv *env, jclass
     CHECK(rc, H(h));
 }
 
+/* ThreadReceiver: a batch of pubsub texts.  The local refs are taken before
+ * any critical region opens (no other JNI call is allowed inside one); the
+ * texts stay pinned by the JVM for the call (the library copies them to the
+ * GPU before returning). */
+JNIEXPORT jint JNICALL Java_NativeAggregator_ingestTexts(JNIEnv *env, jclass c, jlong h, jint tgt,
+                                                         jobjectArray msgs, jint layers, jintArray parts,
+                                                         jintArray status) {
+    (void)c;
+    const jsize n = msgs ? (*env)->GetArrayLength(env, msgs) : 0;
+    jbyteArray *arr = calloc((size_t)n + 1, sizeof *arr);
+    const uint8_t **ptr = calloc((size_t)n + 1, sizeof *ptr);
+    int64_t *len = calloc((size_t)n + 1, sizeof *len);
+    int32_t *st = calloc((size_t)n + 1, sizeof *st);
+    jint *pp = NULL;
+    int rc = IPLS_E_NOMEM;
+    if (!arr || !ptr || !len || !st) goto out;
+    for (jsize i = 0; i < n; ++i) {
+        arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, msgs, i);
+        len[i] = arr[i] ? (*env)->GetArrayLength(env, arr[i]) : 0;
+    }
+    if (parts) pp = (*env)->GetIntArrayElements(env, parts, NULL);
+    for (jsize i = 0; i < n; ++i)
+        ptr[i] = arr[i] ? (*env)->GetPrimitiveArrayCritical(env, arr[i], NULL) : NULL;
+    rc = ipls_agg_ingest_pubsub(H(h), tgt, ptr, len, n, layers, (const int32_t *)pp, st);
+    for (jsize i = n; i-- > 0;)
+        if (ptr[i]) (*env)->ReleasePrimitiveArrayCritical(env, arr[i], (void *)ptr[i], JNI_ABORT);
+    if (pp) (*env)->ReleaseIntArrayElements(env, parts, pp, JNI_ABORT);
+    if (status && rc >= 0) (*env)->SetIntArrayRegion(env, status, 0, n, (const jint *)st);
+    for (jsize i = 0; i < n; ++i)
+        if (arr[i]) (*env)->DeleteLocalRef(env, arr[i]);
+out:
+    free(arr);
+    free(ptr);
+    free(len);
+    free(st);
+    CHECK(rc, H(h));
+    return rc;
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jclass c, jlong h, jint p,
                                                                  jbyteArray sum) {
     (void)c;
