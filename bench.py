@@ -402,6 +402,50 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
     return out
 
 
+def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: float) -> dict:
+    """The rest of an aggregation round on the same handle, one launch each:
+    AggregatePartition for all partitions (k_finalize: read AGG, write W ->
+    16 B/element) and GetPartitions into a device buffer (k_divide: read W,
+    write the flat model -> 16 B/element); then the same round fused into one
+    launch (ipls_agg_aggregate_round), checked bit-identical."""
+    flat = torch.empty(P * (L - 1), dtype=torch.float64, device="cuda")
+    fb = ipls.DeviceBuffer.from_tensor(flat)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    e[0].record(stream)
+    agg.AggregatePartition(ipls.ALL_PARTITIONS)
+    e[1].record(stream)
+    agg.GetPartitions(out=fb)
+    e[2].record(stream)
+    agg.sync()
+    fin_ms, div_ms = e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2])
+    n_el = P * L
+    ref_flat = flat.clone()
+    # the same round as ONE launch (ipls_agg_aggregate_round): folds + W + averages
+    reps = 5
+    fe = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    for i in range(reps):
+        fe[i].record(stream)
+        agg.aggregate_round(0, rows, out=fb)
+    fe[reps].record(stream)
+    agg.sync()
+    fused_ms = fe[0].elapsed_time(fe[reps]) / reps
+    fused_same = bool(torch.equal(flat.view(torch.int64), ref_flat.view(torch.int64)))
+    fused_bytes = P * (K + 1) * L * 8 + 8 * (n_el - P)   # K buckets in, W out, averages out
+    info = {
+        "finalize_ms": round(fin_ms, 4), "finalize_GBps": round(16 * n_el / fin_ms / 1e6, 1),
+        "divide_ms": round(div_ms, 4), "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
+        "round_ms": round(kern_ms + fin_ms + div_ms, 4),
+        "fused_round_ms": round(fused_ms, 4),
+        "fused_round_GBps": round(fused_bytes / fused_ms / 1e6, 1),
+        "fused_round_bit_identical": fused_same,
+        "note": "one aggregation round on device: reduce (K buckets) + AggregatePartition(all) + GetPartitions "
+                "as three launches (round_ms), and fused into one (fused_round_ms)",
+    }
+    del flat, ref_flat
+    return info
+
+
 def pmc_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass for this
     workload (profiles/pmc_traffic.json), or None."""
@@ -513,47 +557,13 @@ def main():
             got = agg.checksum(0)
         verified = got == O.c_synth_sum_checksum(L, p0, K)
 
-    # the rest of an aggregation round on the same handle, one launch each:
-    # AggregatePartition for all partitions (k_finalize: read AGG, write W ->
-    # 16 B/element) and GetPartitions into a device buffer (k_divide: read W,
-    # write the flat model -> 16 B/element)
+    # the rest of an aggregation round on the same handle (round_leg)
     round_info = None
     if not args.be:
-        flat = torch.empty(P * (L - 1), dtype=torch.float64, device="cuda")
-        fb = ipls.DeviceBuffer.from_tensor(flat)
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
-        e[0].record(stream)
-        agg.AggregatePartition(ipls.ALL_PARTITIONS)
-        e[1].record(stream)
-        agg.GetPartitions(out=fb)
-        e[2].record(stream)
-        agg.sync()
-        fin_ms, div_ms = e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2])
-        n_el = P * L
-        ref_flat = flat.clone()
-        # the same round as ONE launch (ipls_agg_aggregate_round): folds + W + averages
-        reps = 5
-        fe = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
-        for i in range(reps):
-            fe[i].record(stream)
-            agg.aggregate_round(0, rows, out=fb)
-        fe[reps].record(stream)
-        agg.sync()
-        fused_ms = fe[0].elapsed_time(fe[reps]) / reps
-        fused_same = bool(torch.equal(flat.view(torch.int64), ref_flat.view(torch.int64)))
-        fused_bytes = P * (K + 1) * L * 8 + 8 * (n_el - P)   # K buckets in, W out, averages out
-        round_info = {
-            "finalize_ms": round(fin_ms, 4), "finalize_GBps": round(16 * n_el / fin_ms / 1e6, 1),
-            "divide_ms": round(div_ms, 4), "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
-            "round_ms": round(kern_ms + fin_ms + div_ms, 4),
-            "fused_round_ms": round(fused_ms, 4),
-            "fused_round_GBps": round(fused_bytes / fused_ms / 1e6, 1),
-            "fused_round_bit_identical": fused_same,
-            "note": "one aggregation round on device: reduce (K buckets) + AggregatePartition(all) + GetPartitions "
-                    "as three launches (round_ms), and fused into one (fused_round_ms)",
-        }
-        del flat, ref_flat
+        try:
+            round_info = round_leg(ipls, torch, agg, rows, P, L, K, stream, kern_ms)
+        except Exception as e:   # a side measurement never costs the headline line
+            round_info = {"error": f"{type(e).__name__}: {e}"}
 
     out = None
     if rank == 0:
