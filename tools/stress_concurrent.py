@@ -1,0 +1,14 @@
+"""Stress: tests/test_gpu_parity.py::test_concurrent_callers_one_handle repeated N times in one process (dev tool)."""
+import sys, time
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "ipls-java-api_amd"), str(ROOT / "tests")]
+import ipls
+from oracle import oracle as O
+import test_gpu_parity as T
+t0 = time.time()
+for i in range(int(sys.argv[1])):
+    T.test_concurrent_callers_one_handle(ipls, O)
+    if i % 20 == 19:
+        print(f"{i+1} runs ok ({time.time()-t0:.0f} s)", flush=True)
+print("stress ok")
