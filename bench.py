@@ -71,6 +71,8 @@ def parse():
                     help="N=1: skip the per-arrival (one call per bucket) leg measured after the headline")
     ap.add_argument("--no-replica-leg", action="store_true",
                     help="N>1: skip the cross-GPU replica exchange measurement (config E)")
+    ap.add_argument("--no-strong-leg", action="store_true",
+                    help="N>1: skip the fixed-total-work leg (config D split over the ranks)")
     ap.add_argument("--replica-reps", type=int, default=5)
     ap.add_argument("--replica-timeout", type=float, default=120.0)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -446,6 +448,53 @@ def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: f
     return info
 
 
+def strong_leg(ipls, torch, dist, rank: int, world: int, local: int, steps: int = 5, verify: bool = True) -> dict:
+    """Fixed total work ('at fixed total work (config D)'):
+    config D's 64 partitions x 4M doubles x 32 peers split over the ranks in
+    contiguous blocks, native doubles, no data-path collective.  Timed like the
+    headline: barrier + sync on both sides, max over ranks; bytes = the whole
+    config's algorithmic bytes.  Never the value."""
+    P_all, L, K = CONFIGS["D"]
+    if P_all % world:
+        return {"error": f"{P_all} partitions do not split over {world} ranks"}
+    P = P_all // world
+    p0 = rank * P
+    elem = L + 32
+    arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
+    base = (int(arena.data_ptr()) + 255) // 256 * 256
+    rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L) for k in range(K)] for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[q][k], p0 + q, k, ipls.SEED)
+    torch.cuda.synchronize()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=local)
+    agg.reduce_batch(0, rows)
+    agg.sync()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agg.reduce_batch(0, rows)
+    agg.sync()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ok = None
+    if verify and rank == 0:
+        from oracle import oracle as O   # checker only
+        ok = agg.checksum(0) == O.c_synth_sum_checksum(L, 0, K)
+    agg.close()
+    del arena, rows
+    torch.cuda.empty_cache()
+    total = P_all * (K + 1) * L * 8 * steps
+    return {"workload": f"D: {P_all} partitions x {L} doubles x {K} peers in total, {P} per rank",
+            "ms_per_step": round(dt / steps * 1e3, 4), "GBps_total": round(total / dt / 1e9, 1),
+            "GBps_per_gpu": round(total / dt / 1e9 / world, 1), "verified_checksum_p0": ok}
+
+
 def pmc_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass for this
     workload (profiles/pmc_traffic.json), or None."""
@@ -631,27 +680,40 @@ def main():
                                                                    local)
     dog = None
     printed = []
-    if world > 1 and not args.no_replica_leg and not args.be:
-        # the cross-GPU exchange is an extra measurement: a watchdog makes sure
+    stage = ["replica_exchange"]
+    if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg):
+        # the multi-rank side legs are extra measurements: a watchdog makes sure
         # a stuck exchange (or a teardown stuck behind a peer that failed in
         # it) can never cost the main line -- every rank exits
         import threading
 
         def expire():
             if out is not None and not printed:
-                out["replica_exchange"] = {"error": f"timed out after {args.replica_timeout} s"}
+                out[stage[0]] = {"error": f"timed out after {args.replica_timeout} s"}
                 print(json.dumps(out), flush=True)
             os._exit(0)
         dog = threading.Timer(args.replica_timeout, expire)
         dog.daemon = True
         dog.start()
-        try:
-            leg = replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, args.replica_reps,
-                                   not args.no_verify, args.dist_backend)
-        except Exception as e:                       # reported, never fatal to the main line
-            leg = {"error": f"{type(e).__name__}: {e}"}
-        if out is not None:
-            out["replica_exchange"] = leg
+        if not args.no_replica_leg:
+            stage[0] = "replica_exchange"
+            try:
+                leg = replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, args.replica_reps,
+                                       not args.no_verify, args.dist_backend)
+            except Exception as e:                   # reported, never fatal to the main line
+                leg = {"error": f"{type(e).__name__}: {e}"}
+            if out is not None:
+                out["replica_exchange"] = leg
+        if not args.no_strong_leg and not args.strong:
+            stage[0] = "strong_scaling_D"
+            del arena, rows
+            torch.cuda.empty_cache()
+            try:
+                sl = strong_leg(ipls, torch, dist, rank, world, local, verify=not args.no_verify)
+            except Exception as e:                   # reported, never fatal to the main line
+                sl = {"error": f"{type(e).__name__}: {e}"}
+            if out is not None:
+                out["strong_scaling_D"] = sl
     if out is not None:
         printed.append(True)
         print(json.dumps(out), flush=True)
