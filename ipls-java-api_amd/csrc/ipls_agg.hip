@@ -798,28 +798,54 @@ int ipls_agg_partition_offset(const ipls_agg* hc, int p, int64_t* off) {
 
 void* ipls_agg_stream(ipls_agg* h) { return h ? (void*)h->stream : nullptr; }
 
+// sync and wait hold the handle's lock only to flush and to book-keep: the
+// host waits with it released, so the Updater and daemon threads (or any
+// other caller) keep queueing folds meanwhile.
 int ipls_agg_sync(ipls_agg* h) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  IPLS_LOCK(h);
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  std::unique_lock<std::mutex> lk(h->mu);
+  if (int rc = flush_pending(h)) return rc;
+  lk.unlock();
+  const hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    lk.lock();
+    return fail(h, IPLS_E_DEVICE, "hipStreamSynchronize failed: %s", hipGetErrorString(e));
+  }
   return IPLS_OK;
 }
 
 int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  std::lock_guard<std::mutex> lk(h->mu);
+  std::unique_lock<std::mutex> lk(h->mu);
   if (ticket >= h->ticket_next) return fail(h, IPLS_E_INVAL, "ticket %llu was never issued", (unsigned long long)ticket);
   if (ticket <= h->ticket_done) return IPLS_OK;
   if (ticket > h->launched_upto)
     if (int rc = flush_pending(h)) return rc;
-  while (!h->batches.empty()) {
-    const ipls_agg::Batch b = h->batches.front();
-    HIP_TRY(h, hipEventSynchronize(b.ev));
-    h->batches.pop_front();
-    h->ev_free.push_back(b.ev);
-    h->ticket_done = std::max(h->ticket_done, b.max_ticket);
-    if (b.max_ticket >= ticket) break;
+  // the first launch group that covers `ticket` (groups complete in order)
+  hipEvent_t ev = nullptr;
+  uint64_t covered = 0;
+  for (const auto& b : h->batches)
+    if (b.max_ticket >= ticket) {
+      ev = b.ev;
+      covered = b.max_ticket;
+      break;
+    }
+  if (!ev) return IPLS_OK;   // already retired by another waiter
+  lk.unlock();
+  // If another thread retires and re-records this event meanwhile, the wait
+  // only gets longer: the re-recorded work was queued after ours.
+  const hipError_t e = hipEventSynchronize(ev);
+  lk.lock();
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(h, IPLS_E_DEVICE, "hipEventSynchronize failed: %s", hipGetErrorString(e));
   }
+  while (!h->batches.empty() && h->batches.front().max_ticket <= covered) {
+    h->ev_free.push_back(h->batches.front().ev);
+    h->batches.pop_front();
+  }
+  h->ticket_done = std::max(h->ticket_done, covered);
   return IPLS_OK;
 }
 

@@ -1210,13 +1210,17 @@ def test_concurrent_callers_one_handle(ipls, O):
                 elif how == 1:
                     agg.Update(dev[k][1], p)
                 elif how == 2:
-                    agg.UpdateAsync(dev[k][1], p)
+                    t = agg.UpdateAsync(dev[k][1], p)
+                    if j % 5 == 0:
+                        agg.Wait(t)            # host waits run with the handle's lock released
                 else:
                     n, st = agg.ingest_pubsub([msgs[k]], partitions=[p])
                     assert n == 1 and st == [0]
                 seq.append((p, k))
                 if j % 17 == 0:
                     agg.read(p)
+                if j % 23 == 0:
+                    agg.sync()
             plans[w] = seq
         except Exception as e:   # surfaced below
             errors.append(e)
