@@ -1,7 +1,7 @@
 // host_e2e.cpp -- dev tool: host-inclusive aggregation rate through the C-ABI
 // alone (what a JNI caller sees), without the Python/ctypes layer of bench.py.
 //
-// Usage: host_e2e L K REPS
+// Usage: host_e2e L K REPS [P]   (P: also the device-resident per-arrival legs)
 // K big-endian buckets of L doubles (update_file bytes) start in host memory;
 // one round = K arrivals folded into AGG[0] + AggregatePartition with the BE
 // sum written back to host memory (commit_update's update_file image).
@@ -102,5 +102,70 @@ int main(int argc, char** argv) {
   }
   ipls_host_free(sum);
   CK(ipls_agg_close(h));
+
+  // Device-resident buckets, one call per arrival as a native (JNI-like)
+  // caller makes them: P partitions x K peers, peers arriving in turn.  The
+  // K buckets live in a second handle's AGG arrays (filled by ipls_synth_fill)
+  // and are reused for every partition (the timing does not depend on values).
+  // Time = wall clock around the P*K calls + the final wait; bytes = the
+  // batch's P*(K+1)*L*8.
+  if (argc > 4) {
+    const int P = atoi(argv[4]);
+    ipls_agg* src = nullptr;
+    ipls_agg_cfg sc{};
+    sc.n_partitions = K;
+    sc.bucket_len = L;
+    h = nullptr;
+    CK(ipls_agg_open(&sc, &src));
+    std::vector<const void*> dev(K);
+    for (int k = 0; k < K; ++k) {
+      void* d = nullptr;
+      CK(ipls_agg_device_ptr(src, k, IPLS_TGT_AGG, &d));
+      CK(ipls_synth_fill(d, L, 0x1B52026ULL, 0, k, IPLS_DEV_F64, ipls_agg_stream(src)));
+      dev[k] = d;
+    }
+    CK(ipls_agg_sync(src));
+    ipls_agg_cfg dc{};
+    dc.n_partitions = P;
+    dc.bucket_len = L;
+    CK(ipls_agg_open(&dc, &h));
+    const double algd = (double)P * (K + 1) * bytes;
+    printf("# device-resident, one call per arrival: P=%d x K=%d x L=%lld, algorithmic bytes=%.0f\n", P, K,
+           (long long)L, algd);
+    auto drun = [&](const char* name, const std::function<void()>& round) {
+      round();
+      double best = 1e30;
+      for (int r = 0; r < REPS; ++r) {
+        CK(ipls_agg_reset(h, IPLS_ALL_PARTITIONS));
+        CK(ipls_agg_sync(h));
+        const double t0 = now();
+        round();
+        best = std::min(best, now() - t0);
+      }
+      printf("%-40s best %8.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s\n", name, best * 1e3, algd / best / 1e9,
+             algd / best / 1e9 / 80.0);
+    };
+    drun("device, one launch per arrival", [&] {
+      for (int k = 0; k < K; ++k)
+        for (int p = 0; p < P; ++p) CK(ipls_agg_accumulate(h, p, IPLS_TGT_AGG, dev[k], L, IPLS_DEV_F64));
+      CK(ipls_agg_sync(h));
+    });
+    drun("device, queued (accumulate_async)", [&] {
+      uint64_t t = 0;
+      for (int k = 0; k < K; ++k)
+        for (int p = 0; p < P; ++p) CK(ipls_agg_accumulate_async(h, p, IPLS_TGT_AGG, dev[k], L, IPLS_DEV_F64, &t));
+      CK(ipls_agg_wait(h, t));
+    });
+    std::vector<const void*> tab((size_t)P * K);
+    for (int p = 0; p < P; ++p)
+      for (int k = 0; k < K; ++k) tab[(size_t)p * K + k] = dev[k];
+    drun("device, one reduce_batch", [&] {
+      CK(ipls_agg_reduce_batch(h, 0, P, tab.data(), K, IPLS_DEV_F64, IPLS_START_ZERO, IPLS_TGT_AGG));
+      CK(ipls_agg_sync(h));
+    });
+    CK(ipls_agg_close(h));
+    h = src;
+    CK(ipls_agg_close(src));
+  }
   return 0;
 }
