@@ -400,7 +400,23 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
                      "verified_checksum_p0": (agg.checksum(0) == want) if verify else None}
     out["note"] = ("one call per arriving bucket (peer-major); each = a fold launch per arrival, "
                    "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), best of "
-                   f"{reps}; algorithmic bytes P*(K+1)*L*8")
+                   f"{reps}; algorithmic bytes P*(K+1)*L*8; Python/ctypes caller")
+    # the same calls from a native caller (what a JNI shim sees): tools/host_e2e.cpp, a child process
+    exe = Path(__file__).resolve().parent / "ipls-java-api_amd" / "lib" / "host_e2e"
+    if exe.exists():
+        import subprocess
+        r = subprocess.run([str(exe), str(L), str(K), "3", str(P), "--device-only"], capture_output=True,
+                           text=True, timeout=180)
+        native = {}
+        for line in r.stdout.splitlines():
+            for key, tag in (("each", "one launch per arrival"), ("coalesced", "queued"), ("batch", "reduce_batch")):
+                if line.startswith("device,") and tag in line:
+                    f = line.split()
+                    ms = float(f[f.index("best") + 1])
+                    native[key] = {"ms": ms, "GBps": round(nbytes / ms / 1e6, 1),
+                                   "frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4)}
+        native["source"] = "tools/host_e2e.cpp --device-only (C-ABI calls, no Python), wall clock, best of 3"
+        out["native_c_abi"] = native if r.returncode == 0 else {"error": r.stderr[-300:]}
     return out
 
 

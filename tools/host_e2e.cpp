@@ -1,7 +1,7 @@
 // host_e2e.cpp -- dev tool: host-inclusive aggregation rate through the C-ABI
 // alone (what a JNI caller sees), without the Python/ctypes layer of bench.py.
 //
-// Usage: host_e2e L K REPS [P]   (P: also the device-resident per-arrival legs)
+// Usage: host_e2e L K REPS [P [--device-only]]   (P: also the device-resident per-arrival legs)
 // K big-endian buckets of L doubles (update_file bytes) start in host memory;
 // one round = K arrivals folded into AGG[0] + AggregatePartition with the BE
 // sum written back to host memory (commit_update's update_file image).
@@ -53,6 +53,9 @@ int main(int argc, char** argv) {
   cfg.n_partitions = 1;
   cfg.bucket_len = L;
   CK(ipls_agg_open(&cfg, &h));
+  const bool device_only = argc > 5 && std::strcmp(argv[5], "--device-only") == 0;
+  if (device_only) goto device_legs;
+  {
   std::vector<void*> pinned(K);
   std::vector<uint8_t*> pageable(K);
   for (int k = 0; k < K; ++k) {
@@ -101,6 +104,8 @@ int main(int argc, char** argv) {
     free(pageable[k]);
   }
   ipls_host_free(sum);
+  }
+device_legs:
   CK(ipls_agg_close(h));
 
   // Device-resident buckets, one call per arrival as a native (JNI-like)
