@@ -389,10 +389,13 @@ inline bool fill(int64_t tiles) {
 // the loop -- checked with -Rpass-analysis=kernel-resource-usage).
 template <bool BE_IN, int START, bool FIN = false>
 constexpr int big_r() { return START != kAccum ? 16 : 8; }
-// SEQ fence interval of the big shape (0 = hipcc's own schedule): big-endian
-// input at R = 16 fences every 2 loads (profiles/r01/sweep_be_seqf*.txt).
+// SEQ schedule of the big shape (0 = hipcc's own): big-endian input at R = 16
+// fences every 2 loads except among a peer's last 4 vectors (SEQF = 2 + 10*4),
+// which lets hipcc overlap the next peer's first loads with that tail:
+// +0.5 to +1.7 points over fencing all 16 in the same process, no spills
+// (profiles/r01/sweep_be_seqf*.txt, sweep_be_tail.txt).
 template <bool BE_IN, int START>
-constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 2 : 0; }
+constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 42 : 0; }
 
 template <bool BE_IN, bool BE_OUT, int START, bool FIN = false>
 void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,

@@ -228,7 +228,9 @@ __device__ __forceinline__ void reduce_tiles(
           const d2 x = decode2<BE_IN>(ld16<NT>(src + off[r]));
           acc[r].x = acc[r].x + x.x;
           acc[r].y = acc[r].y + x.y;
-          if constexpr (SEQF > 0) if ((r + 1) % SEQF == 0) __builtin_amdgcn_sched_barrier(0);
+          // SEQF = F + 10*T: a fence after every F vectors, none among the last T
+          if constexpr (SEQF > 0)
+            if ((r + 1) % (SEQF % 10) == 0 && r + 1 < R - SEQF / 10) __builtin_amdgcn_sched_barrier(0);
         }
       }
     } else {

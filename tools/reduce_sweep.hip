@@ -275,6 +275,13 @@ int main(int argc, char** argv) {
     ADDSB(32, 256, 4);
   }
 #undef ADDSB
+  if (getenv("SWEEP_TAIL")) {   // fence every 2, the last T vectors of a peer unfenced (SEQF = 2 + 10*T)
+    ADDS(16, 0, 2);
+    ADDS(16, 0, 22);
+    ADDS(16, 0, 42);
+    ADDS(16, 0, 62);
+    ADDS(16, 0, 82);
+  }
   if (quick) {             // fence interval of the SEQ schedule (0 = hipcc's own)
     ADDS(16, 0, 0);
     ADDS(16, 0, 1);
