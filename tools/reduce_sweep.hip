@@ -281,6 +281,10 @@ int main(int argc, char** argv) {
     ADDS(16, 0, 42);
     ADDS(16, 0, 62);
     ADDS(16, 0, 82);
+    ADDS(16, 0, 32);
+    ADDS(16, 0, 52);
+    ADDS(16, 0, 44);
+    ADDS(16, 0, 84);
   }
   if (quick) {             // fence interval of the SEQ schedule (0 = hipcc's own)
     ADDS(16, 0, 0);
