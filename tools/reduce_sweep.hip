@@ -275,6 +275,26 @@ int main(int argc, char** argv) {
     ADDSB(32, 256, 4);
   }
 #undef ADDSB
+#define ADDACC(R, BS, F)                                                                          \
+  vars.push_back(Var{"ACCUM R=" #R " BS=" #BS " SEQF=" #F,                                          \
+                     [=](hipStream_t s) {                                                       \
+                       const int64_t tile = (int64_t)BS * 2 * R;                                \
+                       const int tpp = (int)((L + tile - 1) / tile);                            \
+                       auto bp = (const unsigned long long* const*)d_ptrs;                      \
+                       if (be)                                                                  \
+                         hipLaunchKernelGGL((k_reduce<true, false, kAccum, 1, R, true, 0, BS, F>), dim3(tpp * P), dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                       else                                                                     \
+                         hipLaunchKernelGGL((k_reduce<false, false, kAccum, 1, R, true, 0, BS, F>), dim3(tpp * P), dim3(BS), 0, s, bp, d_pd, K, tpp, P); \
+                     },                                                                         \
+                     (double)P * (K + 2) * L * 8, {}})
+  if (getenv("SWEEP_ACCUM")) {   // ACCUM start (reads the target): shipped R=8 x 1024 lanes vs R=16 at fewer lanes
+    ADDACC(8, 1024, 0);
+    ADDACC(16, 512, 0);
+    ADDACC(16, 256, 0);
+    ADDACC(8, 1024, 42);
+    ADDACC(16, 512, 42);
+  }
+#undef ADDACC
   if (getenv("SWEEP_TAIL")) {   // fence every 2, the last T vectors of a peer unfenced (SEQF = 2 + 10*T)
     ADDS(16, 0, 2);
     ADDS(16, 0, 22);
