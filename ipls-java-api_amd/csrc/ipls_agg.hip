@@ -1693,9 +1693,12 @@ namespace {
 
 // Strip and validate the '=' tail of a java.util.Base64 URL text (the rules
 // Decoder.decode0 enforces) -> data chars, or -1 (IllegalArgumentException).
-int64_t b64_data_chars(const uint8_t* t, int64_t n) {
+// `tail` holds the last k >= min(n, 3) chars of an n-char text, so the inner
+// layer's ends can be checked from a few host-decoded bytes: the '=' rules
+// hang on the data-char count of the WHOLE text, not of the window.
+int64_t b64_data_chars(const uint8_t* tail, int64_t k, int64_t n) {
   int64_t pad = 0;
-  while (pad < n && pad < 3 && t[n - 1 - pad] == '=') ++pad;
+  while (pad < k && pad < 3 && tail[k - 1 - pad] == '=') ++pad;
   const int64_t d = n - pad;
   const int64_t r = d % 4;
   if (r == 1) return -1;                       // dangling single char
@@ -1765,7 +1768,7 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
   std::vector<int64_t> dc(n_msgs, 0), dc2(n_msgs, 0);
   std::vector<uint8_t> decode(n_msgs, 0);
   for (int i = 0; i < n_msgs; ++i) {
-    const int64_t d = lens[i] >= 0 ? b64_data_chars(msgs[i], lens[i]) : -1;
+    const int64_t d = lens[i] >= 0 ? b64_data_chars(msgs[i], lens[i], lens[i]) : -1;
     if (d < 0) { st[i] = IPLS_E_FORMAT; continue; }
     dc[i] = d;
     bool ok = true;
@@ -1775,9 +1778,9 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
       const int64_t n = b64_out_len(d), k = std::min<int64_t>(4, n);
       uint8_t tail[4];
       ok = b64_host_bytes(msgs[i], d, n - k, n, tail);
-      const int64_t t = ok ? b64_data_chars(tail, k) : -1;
-      if (t < 0 || (n - k + t) % 4 == 1) { st[i] = IPLS_E_FORMAT; continue; }
-      dc2[i] = n - k + t;
+      const int64_t t = ok ? b64_data_chars(tail, k, n) : -1;
+      if (t < 0) { st[i] = IPLS_E_FORMAT; continue; }
+      dc2[i] = t;
       fl = b64_out_len(dc2[i]);
       if (fl >= 14) {
         uint8_t mid[20];
