@@ -50,8 +50,8 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="C", choices=sorted(CONFIGS))
     ap.add_argument("--strong", action="store_true",
                     help="fixed total work: the config's partitions are split over the ranks "
