@@ -720,8 +720,8 @@ def test_ingest_pubsub_inner_padding(ipls, O):
     agg.close()
 
 
-@pytest.mark.parametrize("layers", [1, 2])
-def test_ingest_pubsub_mutations(ipls, O, layers, seed=None, n_msgs=120):
+@pytest.mark.parametrize("layers,override", [(1, False), (2, False), (2, True)])
+def test_ingest_pubsub_mutations(ipls, O, layers, override, seed=None, n_msgs=120):
     """Every status the pipelined ingest reports (host-read text ends, device-
     checked bodies) against the oracle: invalid chars in the header, body or
     tail of either base64 layer, '=' in the middle, truncations, wrong
@@ -767,15 +767,17 @@ def test_ingest_pubsub_mutations(ipls, O, layers, seed=None, n_msgs=120):
         if t % 11 == 0 and kind == 1 and len(m) > 40:
             m[len(m) // 2] = ord("*")                   # bad route AND bad body char -> -6
         msgs.append(bytes(m))
-    exp = [_ingest_expected(O, m, layers, P, L) for m in msgs]
-    n, st = agg.ingest_pubsub(msgs, layers=layers)
+    # override: the caller routes each text (Download_Scheduler's known partition), -1 and P out of range
+    parts = [int(x) for x in rng.integers(-1, P + 1, size=len(msgs))] if override else None
+    exp = [_ingest_expected(O, m, layers, P, L, None if parts is None else parts[i]) for i, m in enumerate(msgs)]
+    n, st = agg.ingest_pubsub(msgs, layers=layers, partitions=parts)
     bad = [(i, msgs[i][:48], len(msgs[i]), e[0], st[i]) for i, e in enumerate(exp) if st[i] != e[0]]
     assert not bad, f"(index, text head, text len, expected, got): {bad}"
     assert n == sum(1 for e in exp if e[0] == 0)
     assert len(set(st)) >= 4 or seed is not None, st
     for p in range(P):
         gs = [e[1][1] for e in exp if e[0] == 0 and e[1][0] == p]
-        assert gs or seed is not None, p       # the fixed-seed cases fold into every partition
+        assert gs or seed is not None or override, p       # the fixed-seed cases fold into every partition
         assert_bits_equal(agg.read(p), O.reduce(gs, L[p]), f"p{p}")
     agg.close()
 

@@ -1,5 +1,5 @@
 """Soak run of tests/test_gpu_parity.py::test_ingest_pubsub_mutations over
-many seeds and both base64 layer counts (dev tool; one process, stops at the
+many seeds, both base64 layer counts and caller-given routing (dev tool; one process, stops at the
 first status or bit mismatch).  Usage: fuzz_ingest.py FIRST_SEED N_SEEDS"""
 import sys
 import time
@@ -16,19 +16,19 @@ def main(first=100, n=100):
     t0 = time.time()
     fails = 0
     for seed in range(first, first + n):
-        for layers in (1, 2):
+        for layers, override in ((1, False), (2, False), (2, True)):
             try:
-                T.test_ingest_pubsub_mutations(ipls, O, layers, seed=seed, n_msgs=60)
+                T.test_ingest_pubsub_mutations(ipls, O, layers, override, seed=seed, n_msgs=60)
             except AssertionError as e:
                 fails += 1
-                print(f"MISMATCH seed {seed} layers {layers}: {e}", flush=True)
+                print(f"MISMATCH seed {seed} layers {layers} override {override}: {e}", flush=True)
                 if fails >= 12:
                     raise SystemExit(1)
         if (seed - first) % 20 == 19:
             print(f"seeds {first}..{seed} ok ({time.time() - t0:.0f} s)", flush=True)
     if fails:
         raise SystemExit(f"{fails} mismatching cases")
-    print(f"fuzz ok: {n} seeds x 2 layer counts x 60 mutated texts", flush=True)
+    print(f"fuzz ok: {n} seeds x 3 (layers, routing) cases x 60 mutated texts", flush=True)
 
 
 if __name__ == "__main__":
