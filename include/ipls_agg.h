@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define IPLS_AGG_ABI_VERSION 1
+#define IPLS_AGG_ABI_VERSION 2
 
 /* ---- error codes (Java exception the reference would raise) ---- */
 #define IPLS_OK           0
@@ -74,6 +74,9 @@ extern "C" {
 #define IPLS_HOST_PAIR    6  /* host byte[] of a Java-serialised org.javatuples.Pair<Integer,
                                 double[]> partial update (MyIPFSClass.java:160-166, read by
                                 Download_Partial_Updates :326-338); n = byte length         */
+#define IPLS_HOST_TEXT    7  /* output only: host bytes of a base64url pubsub text
+                                (Marshall_Packet's String, MyIPFSClass.java:1016)           */
+#define IPLS_DEV_TEXT     8  /* output only: the same text in device memory                  */
 
 /* ---- fold start modes ---- */
 #define IPLS_START_ACCUM  0  /* fold into the target's current value (Updater arrival fold)     */
@@ -95,6 +98,15 @@ typedef struct ipls_agg_cfg {
     int32_t flags;               /* reserved, must be 0                                          */
     int64_t bucket_len;          /* model_size == 0: every partition has this length incl. the
                                     count slot (synthetic configs, SURVEY.md §8 notation)        */
+    /* ABI 2: the devices of a multi-GPU handle (SURVEY.md §8(b) "device ids", §8(e)).
+     * n_devices == 0 (or devices == NULL): one device, `device`.  Otherwise the
+     * -pa partitions are sharded over devices[0..n_devices) in contiguous blocks,
+     * partition p on shard p / ceil(P / n_devices) (ipls_shard_plan), each shard
+     * with its own HIP stream and accumulator arena on its device; a device may
+     * appear more than once (shards sharing one GPU).  The list is copied. */
+    const int32_t *devices;
+    int32_t n_devices;
+    int32_t reserved;            /* must be 0 */
 } ipls_agg_cfg;
 
 /* ABI version of the loaded library (IPLS_AGG_ABI_VERSION). */
@@ -310,6 +322,79 @@ int ipls_agg_sync(ipls_agg *h);
  *   sum_i splitmix64(bits(x_i) + i*0x9E3779B97F4A7C15) mod 2^64
  * computed on the device (wave DPP + LDS reduction, exact integer sum). */
 int ipls_agg_checksum(ipls_agg *h, int p, int target, uint64_t *out);
+
+/* ---- multi-GPU (cfg.devices) ----
+ * A partition's accumulators live on its owner shard.  Its contributors may
+ * span GPUs the way the reference's replica aggregators of one partition do
+ * (IPLS.java:1402-1468: each aggregator folds the buckets it received, the
+ * partials are published at :1423-1431, the owner adds them in
+ * Collect_Replicas :1449 / the Updater replica branch, Updater.java:40-44,
+ * and AggregatePartition :1462-1468 forms W = AGG + REP).  Here a replica
+ * aggregator is a SLOT: a shard other than the owner folds the buckets
+ * resident on its GPU into the slot's partial sum of p
+ * (ipls_agg_reduce_partial), and ipls_agg_combine_partials pulls the partials
+ * of every other slot over xGMI (peer loads in the owner's fold kernel) and
+ * folds them into REP[p] in ascending slot order:
+ *     REP[p] = ((REP[p] + R_s1) + R_s2) + ...     (REP starts at +0.0)
+ * which is the reference's expression for aggregators s1 < s2 < ...  */
+
+/* Owner shard of partition p: its HIP device ordinal and stream (hipStream_t
+ * as void*; work on p's device pointers is ordered on that stream).  Either
+ * output may be NULL. */
+int ipls_agg_partition_device(ipls_agg *h, int p, int32_t *device, void **stream);
+
+/* The contiguous-block shard plan of cfg.devices, without a handle (no GPU
+ * needed): owner[p] = p / ceil(n_partitions / n_shards) for every p. */
+int ipls_shard_plan(int32_t n_partitions, int32_t n_shards, int32_t *owner);
+
+/* Replica slot `slot` (a shard index, not the owner of any partition in
+ * range) folds k device buckets per partition -- resident on that slot's
+ * device -- into its partial sums of partitions [p_first, p_first+n_parts):
+ *     R_slot[p] = fold(start_mode; bufs[q*k + 0..k-1])
+ * with the same kernels and order as ipls_agg_reduce_batch.  ACCUM folds on
+ * top of the slot's current partial (+0.0 after a combine). */
+int ipls_agg_reduce_partial(ipls_agg *h, int slot, int p_first, int n_parts, const void *const *bufs, int k,
+                            int src_kind, int start_mode);
+
+/* For every partition of [p_first, p_first+n_parts): REP[p] += the partial of
+ * every slot that folded into p since the last combine, slots ascending, in
+ * one launch per owner shard that reads the partials over xGMI; the partials
+ * are then logically +0.0 again.  Returns the number of partials folded. */
+int ipls_agg_combine_partials(ipls_agg *h, int p_first, int n_parts);
+
+/* ---- publish-side codec (a9) ----
+ * Marshall_Packet(target[p], origin, a, b, pid) (MyIPFSClass.java:990-1016),
+ * as the aggregator publishes its partial sum every round
+ * (IPLS.java:1429-1430: a = middleware_iteration, b = workers + 1, pid = 3):
+ * the frame [i16 pid][i32 L_p][i32 a][i32 b][L_p x f64 BE][origin] encoded
+ * with Base64.getUrlEncoder ('=' padding), produced on the device straight
+ * from the accumulator (k_b64url_encode_frame).  origin = the bytes of
+ * OriginPeer.getBytes() the frame carries (String.length() of them).
+ * out_kind IPLS_HOST_TEXT (copied back, call complete on return) or
+ * IPLS_DEV_TEXT (device buffer, stream-ordered).  Returns the text length
+ * 4*ceil((14 + 8*L_p + origin_len)/3); out == NULL: the length only. */
+int64_t ipls_agg_publish_partial(ipls_agg *h, int p, int target, int32_t a, int32_t b, int16_t pid,
+                                 const uint8_t *origin, int32_t origin_len, void *out, int64_t out_cap,
+                                 int out_kind);
+
+/* ---- observability ----
+ * What the last fold launch of a handle (of p's shard for multi-GPU handles:
+ * the shard of the last call) ran: the kernel, the tile shape chosen by the
+ * dispatch, lanes per workgroup, 16-B vectors per lane per
+ * tile, the SEQ schedule code, the block->tile map and the grid. */
+#define IPLS_KERNEL_REDUCE        1  /* k_reduce        */
+#define IPLS_KERNEL_ROUND         2  /* k_round (fused) */
+#define IPLS_KERNEL_FOLD1         3  /* k_fold1         */
+#define IPLS_KERNEL_REDUCE_SCALAR 4  /* k_reduce_scalar */
+#define IPLS_SHAPE_BIG    1
+#define IPLS_SHAPE_MID    2
+#define IPLS_SHAPE_SMALL  3
+typedef struct ipls_launch_info {
+    int32_t kernel, shape, block, vectors, seqf, map;
+    int64_t grid;
+    int32_t be_in, be_out, start, reserved;
+} ipls_launch_info;
+int ipls_agg_last_launch(ipls_agg *h, ipls_launch_info *out);
 
 /* ---- host memory ---- */
 

@@ -1,6 +1,8 @@
-// ipls_agg.hip -- C-ABI implementation (include/ipls_agg.h) of the MI355X
-// IPLS aggregator.  One handle = one aggregator's PeerData accumulator state
-// on one GPU, one HIP stream, one mutex.
+// engine.hip -- the single-device aggregation engine behind the C-ABI
+// (include/ipls_agg.h; the exported entry points are in ipls_agg.cpp, which
+// shards a handle's partitions over one engine per device).  One engine =
+// the PeerData accumulator state of a contiguous block of partitions on one
+// GPU, one HIP stream, one mutex.
 //
 // Device layout: one arena of doubles per handle holding, for
 // every partition p, three arrays of L_p doubles -- AGG (Aggregated_Gradients,
@@ -29,6 +31,8 @@
 #include "../../include/ipls_agg.h"
 #include "ipls_kernels.hpp"
 #include "javaser.hpp"
+#include "engine.hpp"
+#include "pubsub_host.hpp"
 
 using namespace ipls;
 
@@ -41,10 +45,6 @@ constexpr int kRingSlots = 4;
 
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
-uint32_t rd_be32_host(const uint8_t* b) {
-  return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
-}
-
 struct PinnedSlot {
   void* host = nullptr;
   size_t cap = 0;
@@ -54,7 +54,7 @@ struct PinnedSlot {
 
 }  // namespace
 
-struct ipls_agg {
+struct ipls_dev {
   std::mutex mu;
   std::string err;
   int device = 0;
@@ -66,7 +66,9 @@ struct ipls_agg {
   int64_t chunk = 0;  // flat stride between partitions
   int secure = 0;
   std::vector<int64_t> len, flat_off;
-  int64_t max_len = 0, flat_total = 0;
+  int64_t max_len = 0, flat_total = 0;   // flat_total: end of this engine's flat segment
+  int p_lo = 0;                           // first partition of the handle held here
+  int64_t flat_base = 0;                  // flat offset of partition p_lo
 
   // arena
   double* arena = nullptr;
@@ -141,11 +143,12 @@ struct ipls_agg {
   };
   std::map<std::pair<int, int32_t>, OtherRep> other;
   int64_t gbuf_len = 0;
+  ipls_launch_info last_launch{};   // the last fold launch (ipls_agg_last_launch)
 };
 
 namespace {
 
-int fail(ipls_agg* h, int code, const char* fmt, ...) {
+int fail(ipls_dev* h, int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -156,7 +159,7 @@ int fail(ipls_agg* h, int code, const char* fmt, ...) {
   return code;
 }
 
-int flush_pending(ipls_agg* h);
+int flush_pending(ipls_dev* h);
 
 // Take the handle's lock and fold any queued asynchronous device arrivals
 // first, so every entry point sees the accumulators in call order.
@@ -179,12 +182,12 @@ int flush_pending(ipls_agg* h);
 int64_t ref_chunk(int64_t m, int p) { return (int64_t)(int32_t)(m / p) + 1; }  // IPLS.java:1019
 
 
-int check_part(ipls_agg* h, int p) {
+int check_part(ipls_dev* h, int p) {
   if (p < 0 || p >= h->P) return fail(h, IPLS_E_RANGE, "partition %d out of range [0,%d)", p, h->P);
   return IPLS_OK;
 }
 
-int64_t target_off(ipls_agg* h, int p, int target) {
+int64_t target_off(ipls_dev* h, int p, int target) {
   switch (target) {
     case IPLS_TGT_AGG: return h->agg_off[p];
     case IPLS_TGT_REP: return h->rep_off[p];
@@ -195,7 +198,7 @@ int64_t target_off(ipls_agg* h, int p, int target) {
   }
 }
 
-uint8_t* zero_flag(ipls_agg* h, int p, int target) {
+uint8_t* zero_flag(ipls_dev* h, int p, int target) {
   if (target == IPLS_TGT_AGG) return &h->agg_zero[p];
   if (target == IPLS_TGT_REP) return &h->rep_zero[p];
   if (target == IPLS_TGT_FUTURE) return &h->fut_zero[p];
@@ -204,7 +207,7 @@ uint8_t* zero_flag(ipls_agg* h, int p, int target) {
 
 // Make a logically-zero accumulator physically zero (before anything reads it
 // with ACCUM semantics or hands its address out).
-int materialize(ipls_agg* h, int p, int target) {
+int materialize(ipls_dev* h, int p, int target) {
   uint8_t* f = zero_flag(h, p, target);
   if (f && *f) {
     HIP_TRY(h, hipMemsetAsync(h->arena + target_off(h, p, target), 0, (size_t)h->len[p] * 8, h->stream));
@@ -213,7 +216,7 @@ int materialize(ipls_agg* h, int p, int target) {
   return IPLS_OK;
 }
 
-int ensure_pinned(ipls_agg* h, PinnedSlot& s, size_t bytes) {
+int ensure_pinned(ipls_dev* h, PinnedSlot& s, size_t bytes) {
   if (s.pending) {
     HIP_TRY(h, hipEventSynchronize(s.ev));
     s.pending = false;
@@ -230,7 +233,7 @@ int ensure_pinned(ipls_agg* h, PinnedSlot& s, size_t bytes) {
   return IPLS_OK;
 }
 
-int ensure_scratch(ipls_agg* h, size_t bytes) {
+int ensure_scratch(ipls_dev* h, size_t bytes) {
   if (h->scratch_bytes >= bytes) return IPLS_OK;
   if (h->d_scratch) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -246,7 +249,7 @@ int ensure_scratch(ipls_agg* h, size_t bytes) {
 
 // Upload a table through the pinned ring; returns its device address.  An
 // identical table to the previous upload is not re-sent.
-int upload_table(ipls_agg* h, const void* data, size_t bytes, void** dev) {
+int upload_table(ipls_dev* h, const void* data, size_t bytes, void** dev) {
   if (h->last_slot >= 0 && h->last_table.size() == bytes &&
       std::memcmp(h->last_table.data(), data, bytes) == 0) {
     *dev = h->d_table[h->last_slot];
@@ -301,7 +304,7 @@ bool is_pinned_host(const void* p, void** dev_alias = nullptr) {
 // on return, kernels queued behind the copy keep running.  HIP's own path for
 // pageable sources runs at the PCIe rate (56 GB/s measured, tools/h2d_bench.hip),
 // where a memcpy into pinned staging was capped at ~31 GB/s by one CPU thread.
-int stage_h2d(ipls_agg* h, void* dst, const void* src, size_t bytes) {
+int stage_h2d(ipls_dev* h, void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return IPLS_OK;
   if (!h->copy_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->copy_ev, hipEventDisableTiming));
   HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream));
@@ -314,7 +317,7 @@ int stage_h2d(ipls_agg* h, void* dst, const void* src, size_t bytes) {
 // ordering against `stream` (the caller owns `dst`), so it overlaps the fold
 // of the previous arrival.  (Splitting it over two threads measured within
 // noise at 32 MiB and +1.6 % at 64 MiB, profiles/r01/host_e2e_pageable_split.txt.)
-int copy_pageable(ipls_agg* h, void* dst, const void* src, size_t bytes) {
+int copy_pageable(ipls_dev* h, void* dst, const void* src, size_t bytes) {
   if (!h->copy_stream[0]) HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream[0], hipStreamNonBlocking));
   HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->copy_stream[0]));
   HIP_TRY(h, hipStreamSynchronize(h->copy_stream[0]));
@@ -323,8 +326,8 @@ int copy_pageable(ipls_agg* h, void* dst, const void* src, size_t bytes) {
 
 // Stage one pageable per-arrival bucket into the next of the two staging
 // slots; release_stage() marks the slot busy until the fold queued after it.
-int stage_bucket(ipls_agg* h, const void* src, size_t bytes, const void** dptr) {
-  ipls_agg::StageSlot& sl = h->stage[h->stage_next];
+int stage_bucket(ipls_dev* h, const void* src, size_t bytes, const void** dptr) {
+  ipls_dev::StageSlot& sl = h->stage[h->stage_next];
   if (sl.pending) {   // the fold that read this slot two arrivals ago
     HIP_TRY(h, hipEventSynchronize(sl.free_ev));
     sl.pending = false;
@@ -343,15 +346,15 @@ int stage_bucket(ipls_agg* h, const void* src, size_t bytes, const void** dptr) 
   return IPLS_OK;
 }
 
-int release_stage(ipls_agg* h) {
-  ipls_agg::StageSlot& sl = h->stage[h->stage_next];
+int release_stage(ipls_dev* h) {
+  ipls_dev::StageSlot& sl = h->stage[h->stage_next];
   HIP_TRY(h, hipEventRecord(sl.free_ev, h->stream));
   sl.pending = true;
   h->stage_next ^= 1;
   return IPLS_OK;
 }
 
-int d2h(ipls_agg* h, void* dst, const void* src, size_t bytes) {
+int d2h(ipls_dev* h, void* dst, const void* src, size_t bytes) {
   HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return IPLS_OK;
@@ -397,10 +400,34 @@ constexpr int big_r() { return START != kAccum ? 16 : 8; }
 template <bool BE_IN, int START>
 constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 42 : 0; }
 
+// C-ABI start mode -> kernel template start
+int kstart(int start_mode) {
+  return start_mode == IPLS_START_ZERO ? kZero : start_mode == IPLS_START_FIRST ? kFirst : kAccum;
+}
+
+// What a fold launch ran (ipls_agg_last_launch): tests assert that a case
+// reaches the kernel shape it was written for.
+ipls_launch_info launch_info(int kernel, int shape, int block, int r, int seqf, int map, int64_t grid, bool be_in,
+                             bool be_out, int start) {
+  ipls_launch_info li{};
+  li.kernel = kernel;
+  li.shape = shape;
+  li.block = block;
+  li.vectors = r;
+  li.seqf = seqf;
+  li.map = map;
+  li.grid = grid;
+  li.be_in = be_in;
+  li.be_out = be_out;
+  li.start = start == kZero ? IPLS_START_ZERO : start == kFirst ? IPLS_START_FIRST : IPLS_START_ACCUM;
+  return li;
+}
+
 template <bool BE_IN, bool BE_OUT, int START, bool FIN = false>
-void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,
-                     const PartDesc* parts, int k, int secure = 0, const double* cnts = nullptr) {
+ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,
+                                 const PartDesc* parts, int k, int secure = 0, const double* cnts = nullptr) {
   constexpr int R = big_r<BE_IN, START, FIN>();
+  constexpr int KER = FIN ? IPLS_KERNEL_ROUND : IPLS_KERNEL_REDUCE;
   const int64_t big_tile = (int64_t)kBigBS * 2 * R;
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   const int64_t mid_tile = (int64_t)kMidBS * 2 * R;
@@ -422,6 +449,8 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
     if (partial) BIG(3);
     else BIG(kBigMap);
 #undef BIG
+    return launch_info(KER, IPLS_SHAPE_BIG, kBigBS, R, big_seqf<BE_IN, START>(), partial ? 3 : kBigMap, grid.x,
+                       BE_IN, BE_OUT, START);
   } else if (fill(mid_tpp * n_parts)) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, mid_tpp * n_parts));
     const bool partial = mid_tpp > 1 && maxL % mid_tile != 0;
@@ -438,6 +467,8 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
     if (partial) MID(3);
     else MID(kBigMap);
 #undef MID
+    return launch_info(KER, IPLS_SHAPE_MID, kMidBS, R, big_seqf<BE_IN, START>(), partial ? 3 : kBigMap, grid.x,
+                       BE_IN, BE_OUT, START);
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;
     const int64_t tpp = (maxL + tile - 1) / tile;
@@ -448,16 +479,17 @@ void launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned l
     else
       hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kSmallG, kSmallR, true, kSmallMap>), grid, dim3(kBlock), 0,
                          st, bufs, parts, k, (int)tpp, n_parts);
+    return launch_info(KER, IPLS_SHAPE_SMALL, kBlock, kSmallR, 0, kSmallMap, grid.x, BE_IN, BE_OUT, START);
   }
 }
 
-void launch_reduce(bool be_in, bool be_out, int start, int64_t maxL, int n_parts, hipStream_t st,
-                   const unsigned long long* const* bufs, const PartDesc* parts, int k) {
-#define LV(BI, BO)                                                                                  \
-  do {                                                                                              \
-    if (start == kZero) launch_reduce_v<BI, BO, kZero>(maxL, n_parts, st, bufs, parts, k);          \
-    else if (start == kFirst) launch_reduce_v<BI, BO, kFirst>(maxL, n_parts, st, bufs, parts, k);   \
-    else launch_reduce_v<BI, BO, kAccum>(maxL, n_parts, st, bufs, parts, k);                        \
+ipls_launch_info launch_reduce(bool be_in, bool be_out, int start, int64_t maxL, int n_parts, hipStream_t st,
+                               const unsigned long long* const* bufs, const PartDesc* parts, int k) {
+#define LV(BI, BO)                                                                                         \
+  do {                                                                                                     \
+    if (start == kZero) return launch_reduce_v<BI, BO, kZero>(maxL, n_parts, st, bufs, parts, k);          \
+    else if (start == kFirst) return launch_reduce_v<BI, BO, kFirst>(maxL, n_parts, st, bufs, parts, k);   \
+    else return launch_reduce_v<BI, BO, kAccum>(maxL, n_parts, st, bufs, parts, k);                        \
   } while (0)
   if (be_in) { if (be_out) LV(true, true); else LV(true, false); }
   else { if (be_out) LV(false, true); else LV(false, false); }
@@ -468,13 +500,14 @@ void launch_reduce(bool be_in, bool be_out, int start, int64_t maxL, int n_parts
 // FIRST-started).  A one-block pre-pass folds each partition's count slot
 // (k + 2 scalar loads per partition) so that the wide kernel reads one value
 // per block instead of a k-long chain of dependent loads.
-void launch_reduce_fin(bool be_in, int start, int secure, int64_t maxL, int n_parts, hipStream_t st,
-                       const unsigned long long* const* bufs, const PartDesc* parts, int k, double* cnts) {
+ipls_launch_info launch_reduce_fin(bool be_in, int start, int secure, int64_t maxL, int n_parts, hipStream_t st,
+                                   const unsigned long long* const* bufs, const PartDesc* parts, int k,
+                                   double* cnts) {
 #define FIN(BI, ST)                                                                                   \
   do {                                                                                                \
     hipLaunchKernelGGL((k_round_counts<BI, ST>), dim3(n_parts), dim3(64), 0, st,                     \
                        bufs, parts, k, n_parts, cnts);                                                 \
-    launch_reduce_v<BI, false, ST, true>(maxL, n_parts, st, bufs, parts, k, secure, cnts);           \
+    return launch_reduce_v<BI, false, ST, true>(maxL, n_parts, st, bufs, parts, k, secure, cnts);    \
   } while (0)
   if (be_in) { if (start == kZero) FIN(true, kZero); else FIN(true, kAccum); }
   else { if (start == kZero) FIN(false, kZero); else FIN(false, kAccum); }
@@ -505,9 +538,12 @@ struct FinOut {
 // host_src: the bucket is pinned host memory read over PCIe (zero copy); the
 // single-bucket fold then runs on 128 workgroups, which measured 1-2.5 GB/s
 // above 256..4096 (tools/h2d_bench.hip, profiles/r01/h2d_bench_fold1.txt).
-int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, bool be_in,
+int reduce_dev(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, bool be_in,
                int start_mode, int target, void* const* ext_dst = nullptr, bool be_out = false,
-               const FinOut* fin = nullptr, bool host_src = false) {
+               const FinOut* fin = nullptr, bool host_src = false, const int64_t* lens = nullptr) {
+  // lens: lengths of caller destinations that are not this engine's
+  // partitions (ext_dst only, e.g. a replica slot's partial sums)
+  auto len_of = [&](int q) -> int64_t { return lens ? lens[q] : h->len[p_first + q]; };
   auto dst_of = [&](int q) -> unsigned long long* {
     if (fin) return (unsigned long long*)(h->arena + h->w_off[p_first + q]);
     return ext_dst ? (unsigned long long*)ext_dst[q]
@@ -518,7 +554,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
       for (int q = 0; q < n_parts; ++q) {
         uint8_t* f = ext_dst ? nullptr : zero_flag(h, p_first + q, target);
         if (f) *f = 1;
-        else HIP_TRY(h, hipMemsetAsync(dst_of(q), 0, (size_t)h->len[p_first + q] * 8, h->stream));
+        else HIP_TRY(h, hipMemsetAsync(dst_of(q), 0, (size_t)len_of(q) * 8, h->stream));
       }
     }
     return IPLS_OK;  // ACCUM / FIRST with no bucket: nothing to fold
@@ -544,7 +580,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   // kernel arguments, no table upload
   if (!fin && n_parts == 1 && k == 1 && bufs[0]) {
     unsigned long long* d0 = dst_of(0);
-    const int64_t L = h->len[p_first];
+    const int64_t L = len_of(0);
     if (d0 && !((uintptr_t)bufs[0] & 15) && !((uintptr_t)d0 & 15) && L > 0) {
       const auto* s0 = (const unsigned long long*)bufs[0];
       const unsigned blocks =
@@ -556,6 +592,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
 #undef F1S
 #undef F1
       HIP_TRY(h, hipGetLastError());
+      h->last_launch = launch_info(IPLS_KERNEL_FOLD1, 0, kBlock, 4, 0, 0, blocks, be_in, be_out, kstart(start));
       if (!ext_dst)
         if (uint8_t* f = zero_flag(h, p_first, target)) *f = 0;
       return IPLS_OK;
@@ -563,7 +600,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   }
   bool aligned16 = true;
   int64_t maxL = 0;
-  for (int q = 0; q < n_parts; ++q) maxL = std::max(maxL, h->len[p_first + q]);
+  for (int q = 0; q < n_parts; ++q) maxL = std::max(maxL, len_of(q));
   for (int64_t i = 0; i < (int64_t)n_parts * k; ++i) {
     if (!bufs[i]) return fail(h, IPLS_E_INVAL, "bucket pointer %lld is NULL", (long long)i);
     uintptr_t a = (uintptr_t)bufs[i];
@@ -577,7 +614,7 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   PartDesc* pd = (PartDesc*)tbl.data();
   for (int q = 0; q < n_parts; ++q) {
     const int p = p_first + q;
-    pd[q].len = h->len[p];
+    pd[q].len = len_of(q);
     pd[q].dst = dst_of(q);
     pd[q].init = pd[q].dst;
     pd[q].rep = nullptr;
@@ -599,18 +636,20 @@ int reduce_dev(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, i
   auto dbufs = (const unsigned long long* const*)((char*)dtab + desc_bytes);
   if (fin) {
     if (!aligned16) return fail(h, IPLS_E_INVAL, "fused round needs 16-B aligned buckets");
-    launch_reduce_fin(be_in, start, h->secure, maxL, n_parts, h->stream, dbufs, dparts, k, h->d_cnt);
+    h->last_launch = launch_reduce_fin(be_in, start, h->secure, maxL, n_parts, h->stream, dbufs, dparts, k, h->d_cnt);
     HIP_TRY(h, hipGetLastError());
     for (int q = p_first; q < p_first + n_parts; ++q) h->agg_zero[q] = h->rep_zero[q] = 1;
     return IPLS_OK;
   }
   if (aligned16) {
-    launch_reduce(be_in, be_out, start, maxL, n_parts, h->stream, dbufs, dparts, k);
+    h->last_launch = launch_reduce(be_in, be_out, start, maxL, n_parts, h->stream, dbufs, dparts, k);
   } else {
     const int64_t tile = (int64_t)kBlock * 8;
     const int tpp = (int)((maxL + tile - 1) / tile);
     launch_reduce_scalar(be_in, be_out, start, dim3((unsigned)tpp * n_parts), h->stream, dbufs, dparts, k, tpp,
                          tile);
+    h->last_launch = launch_info(IPLS_KERNEL_REDUCE_SCALAR, 0, kBlock, 1, 0, 0, (int64_t)tpp * n_parts, be_in, be_out,
+                                 kstart(start));
   }
   HIP_TRY(h, hipGetLastError());
   if (!ext_dst)
@@ -659,7 +698,7 @@ int partition_geometry(const ipls_agg_cfg* c, std::vector<int64_t>& len, std::ve
   return IPLS_OK;
 }
 
-int host_decode_count(int kind, int64_t n, int64_t L, ipls_agg* h) {
+int host_decode_count(int kind, int64_t n, int64_t L, ipls_dev* h) {
   if (n < L) return fail(h, IPLS_E_RANGE, "bucket of %lld doubles shorter than partition length %lld", (long long)n, (long long)L);
   (void)kind;
   return IPLS_OK;
@@ -668,40 +707,48 @@ int host_decode_count(int kind, int64_t n, int64_t L, ipls_agg* h) {
 }  // namespace
 
 // ===========================================================================
-// C-ABI
+// Engine entry points (engine.hpp).  The handle-free ipls_* utilities further
+// down keep the C linkage of their declarations in include/ipls_agg.h.
 // ===========================================================================
-extern "C" {
-
-int ipls_agg_abi_version(void) { return IPLS_AGG_ABI_VERSION; }
-
-const char* ipls_agg_last_error(const ipls_agg* h) {
+const char* dev_last_error(const ipls_dev* h) {
   if (h) return h->err.c_str();
   return g_tls_err.c_str();
 }
 
-int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
-  if (!cfg || !out) return fail(nullptr, IPLS_E_INVAL, "null cfg/out");
-  *out = nullptr;
-  if (cfg->n_partitions <= 0) return fail(nullptr, IPLS_E_INVAL, "n_partitions must be > 0 (-pa)");
-  if (cfg->model_size < 0) return fail(nullptr, IPLS_E_INVAL, "model_size < 0");
-  if (cfg->flags != 0) return fail(nullptr, IPLS_E_INVAL, "cfg.flags must be 0");
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return fail(nullptr, IPLS_E_NODEV, "no HIP device available");
-  if (cfg->device < 0 || cfg->device >= ndev)
-    return fail(nullptr, IPLS_E_NODEV, "device %d not in [0,%d)", cfg->device, ndev);
+// The front's own failures land in the same per-thread message that
+// ipls_agg_last_error(NULL) reads.
+void dev_set_thread_error(const char* msg) { g_tls_err = msg ? msg : ""; }
 
-  ipls_agg* h = new (std::nothrow) ipls_agg();
+int dev_geometry(const ipls_agg_cfg* cfg, std::vector<int64_t>& len, std::vector<int64_t>& off, int64_t& chunk,
+                 std::string& why) {
+  return partition_geometry(cfg, len, off, chunk, why);
+}
+
+// One engine for the partitions [p_lo, p_hi) of the handle's geometry on
+// `device` (the front has validated cfg and the device ordinal).  Partition
+// q of the engine is partition p_lo + q of the handle; flat offsets stay the
+// handle's (flat model coordinates), flat_base is the first one.
+int dev_open(const ipls_agg_cfg* cfg, int device, int p_lo, int p_hi, ipls_dev** out) {
+  if (!cfg || !out || p_lo < 0 || p_hi < p_lo || p_hi > cfg->n_partitions)
+    return fail(nullptr, IPLS_E_INVAL, "bad engine range");
+  *out = nullptr;
+  ipls_dev* h = new (std::nothrow) ipls_dev();
   if (!h) return fail(nullptr, IPLS_E_NOMEM, "host allocation failed");
   std::string why;
-  int rc = partition_geometry(cfg, h->len, h->flat_off, h->chunk, why);
+  std::vector<int64_t> glen, goff;
+  int rc = partition_geometry(cfg, glen, goff, h->chunk, why);
   if (rc) {
     delete h;
     return fail(nullptr, rc, "%s", why.c_str());
   }
-  h->device = cfg->device;
+  h->len.assign(glen.begin() + p_lo, glen.begin() + p_hi);
+  h->flat_off.assign(goff.begin() + p_lo, goff.begin() + p_hi);
+  h->p_lo = p_lo;
+  // an empty engine (p_hi == p_lo) owns no partition: a replica slot only
+  h->flat_base = p_hi > p_lo ? h->flat_off[0] : 0;
+  h->P = p_hi - p_lo;
+  h->device = device;
   h->model_size = cfg->model_size;
-  h->P = cfg->n_partitions;
   h->secure = cfg->secure;
   h->agg_off.resize(h->P);
   h->rep_off.resize(h->P);
@@ -721,32 +768,32 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
   }
   h->arena_elems = cur;
   // new double[(int)_MODEL_SIZE/_PARTITIONS + 2] (Updater.java:162)
-  h->gbuf_len = h->model_size > 0 ? (int64_t)((int32_t)h->model_size / h->P) + 2 : cfg->bucket_len;
+  h->gbuf_len = h->model_size > 0 ? (int64_t)((int32_t)h->model_size / cfg->n_partitions) + 2 : cfg->bucket_len;
   auto cleanup = [&](int code) {
     (void)hipGetLastError();   // the failed call's error must not reach a later launch check
-    ipls_agg_close(h);
+    dev_close(h);
     return code;
   };
   if (hipSetDevice(h->device) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipSetDevice(%d) failed", h->device));
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipStreamCreate failed"));
-  if (hipMalloc(&h->arena, (size_t)h->arena_elems * 8) != hipSuccess) {
+  if (h->arena_elems > 0 && hipMalloc(&h->arena, (size_t)h->arena_elems * 8) != hipSuccess) {
     (void)hipGetLastError();   // not sticky: the next launch check must not see it
     h->arena = nullptr;
     return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc of %lld-byte arena failed", (long long)h->arena_elems * 8));
   }
   if (hipMalloc(&h->d_sum, 64) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc failed"));
-  if (hipMalloc(&h->d_cnt, sizeof(double) * h->P) != hipSuccess)
+  if (hipMalloc(&h->d_cnt, sizeof(double) * std::max(1, h->P)) != hipSuccess)
     return cleanup(fail(nullptr, IPLS_E_NOMEM, "hipMalloc failed"));
   // InitializeWeights(): new double[] -> all zero (IPLS.java:1860-1878).
-  if (hipMemsetAsync(h->arena, 0, (size_t)h->arena_elems * 8, h->stream) != hipSuccess ||
+  if ((h->arena && hipMemsetAsync(h->arena, 0, (size_t)h->arena_elems * 8, h->stream) != hipSuccess) ||
       hipStreamSynchronize(h->stream) != hipSuccess)
     return cleanup(fail(nullptr, IPLS_E_DEVICE, "arena clear failed"));
   *out = h;
   return IPLS_OK;
 }
 
-int ipls_agg_close(ipls_agg* h) {
+int dev_close(ipls_dev* h) {
   if (!h) return IPLS_OK;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
@@ -783,28 +830,12 @@ int ipls_agg_close(ipls_agg* h) {
   return IPLS_OK;
 }
 
-int ipls_agg_partition_len(const ipls_agg* hc, int p, int64_t* L) {
-  ipls_agg* h = const_cast<ipls_agg*>(hc);
-  if (!h || !L) return fail(h, IPLS_E_INVAL, "null argument");
-  if (int rc = check_part(h, p)) return rc;
-  *L = h->len[p];
-  return IPLS_OK;
-}
-
-int ipls_agg_partition_offset(const ipls_agg* hc, int p, int64_t* off) {
-  ipls_agg* h = const_cast<ipls_agg*>(hc);
-  if (!h || !off) return fail(h, IPLS_E_INVAL, "null argument");
-  if (int rc = check_part(h, p)) return rc;
-  *off = h->flat_off[p];
-  return IPLS_OK;
-}
-
-void* ipls_agg_stream(ipls_agg* h) { return h ? (void*)h->stream : nullptr; }
+void* dev_stream(ipls_dev* h) { return h ? (void*)h->stream : nullptr; }
 
 // sync and wait hold the handle's lock only to flush and to book-keep: the
 // host waits with it released, so the Updater and daemon threads (or any
 // other caller) keep queueing folds meanwhile.
-int ipls_agg_sync(ipls_agg* h) {
+int dev_sync(ipls_dev* h) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   std::unique_lock<std::mutex> lk(h->mu);
   if (int rc = flush_pending(h)) return rc;
@@ -818,7 +849,7 @@ int ipls_agg_sync(ipls_agg* h) {
   return IPLS_OK;
 }
 
-int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
+int dev_wait(ipls_dev* h, uint64_t ticket) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   std::unique_lock<std::mutex> lk(h->mu);
   if (ticket >= h->ticket_next) return fail(h, IPLS_E_INVAL, "ticket %llu was never issued", (unsigned long long)ticket);
@@ -852,13 +883,13 @@ int ipls_agg_wait(ipls_agg* h, uint64_t ticket) {
   return IPLS_OK;
 }
 
-int ipls_agg_flush(ipls_agg* h) {
+int dev_flush(ipls_dev* h) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);   // launches the queued folds; does not wait for them
   return IPLS_OK;
 }
 
-int ipls_agg_set_coalesce(ipls_agg* h, int max_group) {
+int dev_set_coalesce(ipls_dev* h, int max_group) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   h->coalesce = std::max(1, max_group);
@@ -869,7 +900,7 @@ namespace {
 
 // Close the launches queued since the last batch: tickets up to ticket_next-1
 // complete at the event recorded now.
-int end_batch(ipls_agg* h) {
+int end_batch(ipls_dev* h) {
   hipEvent_t ev;
   if (!h->ev_free.empty()) {
     ev = h->ev_free.back();
@@ -880,8 +911,8 @@ int end_batch(ipls_agg* h) {
   HIP_TRY(h, hipEventRecord(ev, h->stream));
   h->batches.push_back({h->ticket_next - 1, ev});
   h->launched_upto = h->ticket_next - 1;
-  while ((int)h->batches.size() > ipls_agg::kMaxBatches) {   // bound the events in flight
-    const ipls_agg::Batch b = h->batches.front();
+  while ((int)h->batches.size() > ipls_dev::kMaxBatches) {   // bound the events in flight
+    const ipls_dev::Batch b = h->batches.front();
     HIP_TRY(h, hipEventSynchronize(b.ev));
     h->batches.pop_front();
     h->ev_free.push_back(b.ev);
@@ -893,7 +924,7 @@ int end_batch(ipls_agg* h) {
 // Fold every queued device arrival: runs of consecutive partitions of one
 // target with the same queue length and byte order go as one launch (the
 // batch kernel's table is [partition][peer]).
-int flush_pending(ipls_agg* h) {
+int flush_pending(ipls_dev* h) {
   if (h->pending.empty()) return IPLS_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   int rc = IPLS_OK;
@@ -922,7 +953,7 @@ int flush_pending(ipls_agg* h) {
 
 }  // namespace
 
-int ipls_agg_reduce_batch(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k,
+int dev_reduce_batch(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k,
                           int src_kind, int start_mode, int target) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
@@ -937,7 +968,7 @@ int ipls_agg_reduce_batch(ipls_agg* h, int p_first, int n_parts, const void* con
   return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, target);
 }
 
-int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind) {
+int dev_accumulate(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1008,7 +1039,7 @@ int ipls_agg_accumulate(ipls_agg* h, int p, int target, const void* src, int64_t
   return staged ? release_stage(h) : IPLS_OK;
 }
 
-int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind,
+int dev_accumulate_async(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind,
                               uint64_t* ticket) {
   if (!h || !ticket) return fail(h, IPLS_E_INVAL, "null argument");
   if (src && (src_kind == IPLS_DEV_F64 || src_kind == IPLS_DEV_BE)) {
@@ -1039,7 +1070,7 @@ int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, i
   const bool host = src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE;
   if (!src || !host || ((uintptr_t)src & 15) || !is_pinned_host(src, &alias) || !alias) {
     // not a pinned host bucket: the synchronous path, already complete on return
-    int rc = ipls_agg_accumulate(h, p, target, src, n, src_kind);
+    int rc = dev_accumulate(h, p, target, src, n, src_kind);
     std::lock_guard<std::mutex> lk(h->mu);
     *ticket = h->ticket_done;
     return rc;
@@ -1057,30 +1088,27 @@ int ipls_agg_accumulate_async(ipls_agg* h, int p, int target, const void* src, i
   return end_batch(h);
 }
 
-int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, int64_t n_bytes) {
-  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
-  IPLS_LOCK(h);
-  if (int rc = check_part(h, p)) return rc;
-  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
-  if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
-  HIP_TRY(h, hipSetDevice(h->device));
+// GetParameters(hash, Gradient_Buff) (MyIPFSClass.java:444-455) into the
+// engine's Gradient_Buff (Updater.java:162, zeroed once, Updater.java:165-167):
+// arr[i] = getDouble() for i < data.length/8; past arr.length it throws after
+// the in-range stores (IPLS_E_RANGE, buffer already overwritten).  Entries
+// beyond the file keep the previous request's values.  *zero_copy: the kernel
+// reads the caller's pinned bytes (wait before returning to the caller).
+static int gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, bool* zero_copy) {
   const int64_t G = h->gbuf_len;
-  if (!h->d_gbuf) {   // the Java loop fills it with 0.0 before the first request (Updater.java:165-167)
+  *zero_copy = false;
+  if (!h->d_gbuf) {
     HIP_TRY(h, hipMalloc(&h->d_gbuf, (size_t)std::max<int64_t>(G, 1) * 8));
     HIP_TRY(h, hipMemsetAsync(h->d_gbuf, 0, (size_t)std::max<int64_t>(G, 1) * 8, h->stream));
   }
-  // GetParameters(hash, Gradient_Buff) (MyIPFSClass.java:444-455): arr[i] =
-  // getDouble() for i < data.length/8; past arr.length it throws after the
-  // in-range stores.  Entries beyond the file keep the previous request's values.
   const int64_t nd = n_bytes / 8;
   const int64_t nw = std::min(nd, G);
-  bool zero_copy = false;
   if (nw > 0) {
     const void* dsrc = nullptr;
     void* alias = nullptr;
     if (((uintptr_t)bytes & 7) == 0 && (size_t)nw * 8 >= (1u << 16) && is_pinned_host(bytes, &alias) && alias) {
       dsrc = alias;
-      zero_copy = true;
+      *zero_copy = true;
     } else {
       // double-buffered like the per-arrival buckets (stage_bucket)
       if (int rc = stage_bucket(h, bytes, (size_t)nw * 8, &dsrc)) return rc;
@@ -1088,14 +1116,27 @@ int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, 
     hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(nw, kBlock), 4096)), dim3(kBlock), 0,
                        h->stream, (const unsigned long long*)dsrc, h->d_gbuf, nw);
     HIP_TRY(h, hipGetLastError());
-    if (!zero_copy)
+    if (!*zero_copy)
       if (int rc = release_stage(h)) return rc;
   }
   if (nd > G) {
-    if (zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (*zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
     return fail(h, IPLS_E_RANGE, "GetParameters: %lld doubles > Gradient_Buff length %lld "
                 "(ArrayIndexOutOfBoundsException, MyIPFSClass.java:451)", (long long)nd, (long long)G);
   }
+  return IPLS_OK;
+}
+
+int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64_t n_bytes) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  IPLS_LOCK(h);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
+  HIP_TRY(h, hipSetDevice(h->device));
+  const int64_t G = h->gbuf_len;
+  bool zero_copy = false;
+  if (int rc = gbuf_load(h, bytes, n_bytes, &zero_copy)) return rc;
   // _Update(Gradient_Buff, ...): target[p][i] += Gradient_Buff[i], i < L_p
   if (h->len[p] > G)
     return fail(h, IPLS_E_RANGE, "partition length %lld > Gradient_Buff length %lld", (long long)h->len[p],
@@ -1106,7 +1147,24 @@ int ipls_agg_update_indirect(ipls_agg* h, int p, int target, const void* bytes, 
   return IPLS_OK;
 }
 
-int ipls_agg_reset(ipls_agg* h, int p) {
+// The Gradient_Buff load alone, for a request whose partition lives in
+// another engine (the handle keeps ONE Gradient_Buff, as the reference has
+// one Updater thread): *gbuf / *glen describe the device buffer afterwards;
+// the caller orders the fold after this engine's stream.
+int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** gbuf, int64_t* glen) {
+  if (!h || !gbuf || !glen) return fail(h, IPLS_E_INVAL, "null argument");
+  IPLS_LOCK(h);
+  if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
+  HIP_TRY(h, hipSetDevice(h->device));
+  bool zero_copy = false;
+  if (int rc = gbuf_load(h, bytes, n_bytes, &zero_copy)) return rc;
+  if (zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
+  *gbuf = h->d_gbuf;
+  *glen = h->gbuf_len;
+  return IPLS_OK;
+}
+
+int dev_reset(ipls_dev* h, int p) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (p == IPLS_ALL_PARTITIONS) {
@@ -1118,7 +1176,7 @@ int ipls_agg_reset(ipls_agg* h, int p) {
   return IPLS_OK;
 }
 
-int ipls_agg_promote_future(ipls_agg* h, const int32_t* parts, int n_parts) {
+int dev_promote_future(ipls_dev* h, const int32_t* parts, int n_parts) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (n_parts < 0 || (n_parts > 0 && !parts)) return fail(h, IPLS_E_INVAL, "bad partition list");
@@ -1134,7 +1192,7 @@ int ipls_agg_promote_future(ipls_agg* h, const int32_t* parts, int n_parts) {
   return IPLS_OK;
 }
 
-int ipls_agg_device_ptr(ipls_agg* h, int p, int target, void** ptr) {
+int dev_device_ptr(ipls_dev* h, int p, int target, void** ptr) {
   if (!h || !ptr) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1145,7 +1203,7 @@ int ipls_agg_device_ptr(ipls_agg* h, int p, int target, void** ptr) {
   return IPLS_OK;
 }
 
-int ipls_agg_read(ipls_agg* h, int p, int target, void* dst, int64_t n, int dst_kind) {
+int dev_read(ipls_dev* h, int p, int target, void* dst, int64_t n, int dst_kind) {
   if (!h || !dst) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1178,7 +1236,7 @@ int ipls_agg_read(ipls_agg* h, int p, int target, void* dst, int64_t n, int dst_
   }
 }
 
-int ipls_agg_checksum(ipls_agg* h, int p, int target, uint64_t* out) {
+int dev_checksum(ipls_dev* h, int p, int target, uint64_t* out) {
   if (!h || !out) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1198,7 +1256,7 @@ int ipls_agg_checksum(ipls_agg* h, int p, int target, uint64_t* out) {
 }
 
 // AggregatePartition's W = AGG + REP for partitions [p0, p0+np) (IPLS.java:1256-1269).
-static int finalize_range(ipls_agg* h, int p0, int np) {
+static int finalize_range(ipls_dev* h, int p0, int np) {
   // AGG logically zero but present as an operand -> make it physical.
   bool rep_zero_all = true;
   for (int q = p0; q < p0 + np; ++q) {
@@ -1233,7 +1291,7 @@ static int finalize_range(ipls_agg* h, int p0, int np) {
 
 // GetPartitions' divide (IPLS.java:1159-1174) of Weights[p0..p0+np) into d_out,
 // partition p at flat_off[p] - flat_off[p0].
-static int divide_range(ipls_agg* h, int p0, int np, unsigned long long* d_out, bool be) {
+static int divide_range(ipls_dev* h, int p0, int np, unsigned long long* d_out, bool be) {
   std::vector<DivDesc> dd(np);
   int64_t maxn = 0;
   for (int q = 0; q < np; ++q) {
@@ -1255,7 +1313,7 @@ static int divide_range(ipls_agg* h, int p0, int np, unsigned long long* d_out, 
   return IPLS_OK;
 }
 
-int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* avg_out) {
+int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_out) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   int p0 = p, np = 1;
@@ -1266,6 +1324,10 @@ int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* a
   } else if (int rc = check_part(h, p)) {
     return rc;
   }
+  // validate the outputs before anything is consumed: finalize_range flags
+  // AGG/REP logically zero, so a rejected call must not get that far
+  if (sum_out && sum_kind != IPLS_HOST_F64 && sum_kind != IPLS_HOST_BE)
+    return fail(h, IPLS_E_INVAL, "sum_kind must be HOST_F64 or HOST_BE");
   HIP_TRY(h, hipSetDevice(h->device));
   if (int rc = finalize_range(h, p0, np)) return rc;
 
@@ -1294,7 +1356,7 @@ int ipls_agg_finalize(ipls_agg* h, int p, void* sum_out, int sum_kind, double* a
   return IPLS_OK;
 }
 
-int ipls_agg_set_weights(ipls_agg* h, int p, const void* src, int64_t n, int src_kind) {
+int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind) {
   if (!h || !src) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1352,7 +1414,7 @@ int ipls_agg_set_weights(ipls_agg* h, int p, const void* src, int64_t n, int src
 
 // Bring a flat vector of n doubles (host or device, native or BE) onto the
 // device; returns a device pointer and whether it is big-endian.
-static int flat_to_device(ipls_agg* h, const void* flat, int64_t n, int kind, const unsigned long long** d,
+static int flat_to_device(ipls_dev* h, const void* flat, int64_t n, int kind, const unsigned long long** d,
                           bool* be) {
   switch (kind) {
     case IPLS_DEV_F64:
@@ -1373,7 +1435,7 @@ static int flat_to_device(ipls_agg* h, const void* flat, int64_t n, int kind, co
   }
 }
 
-int ipls_agg_other_replica(ipls_agg* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
+int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1396,7 +1458,7 @@ int ipls_agg_other_replica(ipls_agg* h, int p, int32_t aggregator, const void* s
   unsigned long long* dst;
   if (first) {   // Other.put(key, GetParameters(Hash)): a new array of the file's length (:263)
     HIP_TRY(h, hipMalloc(&dst, (size_t)std::max<int64_t>(n, 1) * 8));
-    h->other[key] = ipls_agg::OtherRep{dst, n, 1};
+    h->other[key] = ipls_dev::OtherRep{dst, n, 1};
   } else {
     dst = it->second.d;
     it->second.received += 1;   // Other_Replica_Gradients_Received + 1 (:260)
@@ -1413,7 +1475,7 @@ int ipls_agg_other_replica(ipls_agg* h, int p, int32_t aggregator, const void* s
   return IPLS_OK;
 }
 
-int ipls_agg_collect_replicas(ipls_agg* h, int32_t* participants) {
+int dev_collect_replicas(ipls_dev* h, int32_t* participants) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   HIP_TRY(h, hipSetDevice(h->device));
@@ -1446,7 +1508,7 @@ int ipls_agg_collect_replicas(ipls_agg* h, int32_t* participants) {
   return folded;
 }
 
-int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {
+int dev_load_model(ipls_dev* h, const void* src, int64_t n, int src_kind) {
   if (!h || !src) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (n < h->flat_total)
@@ -1454,16 +1516,19 @@ int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {
   HIP_TRY(h, hipSetDevice(h->device));
   const unsigned long long* d;
   bool be;
-  if (int rc = flat_to_device(h, src, h->flat_total, src_kind, &d, &be)) return rc;
+  // only this engine's segment [flat_base, flat_total) of the model
+  if (int rc = flat_to_device(h, (const char*)src + 8 * h->flat_base, h->flat_total - h->flat_base, src_kind, &d,
+                              &be))
+    return rc;
   for (int p = 0; p < h->P; ++p) {
     const int64_t L = h->len[p];
     // IPLS.java:1883-1895: values for j < min((i+1)c, M), count slot 0.0
     if (be)
       hipLaunchKernelGGL(k_load_model<true>, dim3(blocks_for(L, kBlock)), dim3(kBlock), 0, h->stream, d,
-                         h->flat_off[p], L - 1, L, h->arena + h->w_off[p]);
+                         h->flat_off[p] - h->flat_base, L - 1, L, h->arena + h->w_off[p]);
     else
       hipLaunchKernelGGL(k_load_model<false>, dim3(blocks_for(L, kBlock)), dim3(kBlock), 0, h->stream, d,
-                         h->flat_off[p], L - 1, L, h->arena + h->w_off[p]);
+                         h->flat_off[p] - h->flat_base, L - 1, L, h->arena + h->w_off[p]);
     HIP_TRY(h, hipGetLastError());
     h->agg_zero[p] = h->rep_zero[p] = h->fut_zero[p] = 1;   // IPLS.java:1886-1898
   }
@@ -1472,7 +1537,7 @@ int ipls_agg_load_model(ipls_agg* h, const void* src, int64_t n, int src_kind) {
 }
 
 // OrganizeGradients bounds for partition p of a flat vector of n values.
-static int split_bounds(ipls_agg* h, int p, int64_t n, int64_t* ncopy) {
+static int split_bounds(ipls_dev* h, int p, int64_t n, int64_t* ncopy) {
   const int64_t lo = h->flat_off[p];
   const int64_t hi = std::min(lo + h->chunk, n);
   const int64_t nc = std::max<int64_t>(0, hi - lo);
@@ -1483,7 +1548,7 @@ static int split_bounds(ipls_agg* h, int p, int64_t n, int64_t* ncopy) {
   return IPLS_OK;
 }
 
-int ipls_agg_split(ipls_agg* h, const void* flat, int64_t n, int src_kind, int p, void* dst, int dst_kind) {
+int dev_split(ipls_dev* h, const void* flat, int64_t n, int src_kind, int p, void* dst, int dst_kind) {
   if (!h || !flat || !dst) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1526,7 +1591,7 @@ int ipls_agg_split(ipls_agg* h, const void* flat, int64_t n, int src_kind, int p
   return IPLS_OK;
 }
 
-int ipls_agg_update_gradient(ipls_agg* h, const void* flat, int64_t n, int src_kind, const int32_t* owned,
+int dev_update_gradient(ipls_dev* h, const void* flat, int64_t n, int src_kind, const int32_t* owned,
                              int n_owned) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   if (!flat) return IPLS_OK;  // Gradients == null (IPLS.java:1708-1713, 1738 `&& Gradients != null`)
@@ -1543,7 +1608,9 @@ int ipls_agg_update_gradient(ipls_agg* h, const void* flat, int64_t n, int src_k
   HIP_TRY(h, hipSetDevice(h->device));
   const unsigned long long* d;
   bool be;
-  if (int rc = flat_to_device(h, flat, std::min(n, h->flat_total), src_kind, &d, &be)) return rc;
+  // only this engine's segment of the gradient vector (flat_base on)
+  const int64_t seg = std::max<int64_t>(0, std::min(n, h->flat_total) - h->flat_base);
+  if (int rc = flat_to_device(h, (const char*)flat + 8 * h->flat_base, seg, src_kind, &d, &be)) return rc;
   for (int i = 0; i < n_owned; ++i) {
     const int p = owned[i];
     const int64_t L = h->len[p];
@@ -1553,19 +1620,22 @@ int ipls_agg_update_gradient(ipls_agg* h, const void* flat, int64_t n, int src_k
     // Logically-zero accumulator: write +0.0 + v (== fold into zeros).
     if (zero) HIP_TRY(h, hipMemsetAsync(acc, 0, (size_t)L * 8, h->stream));
     if (be)
-      hipLaunchKernelGGL((k_split<true, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p], nc[p], L, acc);
+      hipLaunchKernelGGL((k_split<true, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p] - h->flat_base,
+                         nc[p], L, acc);
     else
-      hipLaunchKernelGGL((k_split<false, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p], nc[p], L, acc);
+      hipLaunchKernelGGL((k_split<false, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p] - h->flat_base,
+                         nc[p], L, acc);
     HIP_TRY(h, hipGetLastError());
     h->agg_zero[p] = 0;
   }
   return IPLS_OK;
 }
 
-int ipls_agg_get_partitions(ipls_agg* h, void* out, int64_t n, int out_kind) {
+int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind) {
   if (!h || !out) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
-  const int64_t M = h->flat_total;
+  // out holds this engine's segment: flat offsets [flat_base, flat_total)
+  const int64_t M = h->flat_total - h->flat_base;
   if (n < M) return fail(h, IPLS_E_RANGE, "output of %lld < model size %lld", (long long)n, (long long)M);
   if (out_kind != IPLS_HOST_F64 && out_kind != IPLS_HOST_BE_CANON && out_kind != IPLS_DEV_F64)
     return fail(h, IPLS_E_INVAL, "bad out_kind %d", out_kind);
@@ -1628,7 +1698,7 @@ int ipls_checksum_dev(const void* src, int64_t n, int src_kind, uint64_t* out, v
   return IPLS_OK;
 }
 
-int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+int dev_reduce_batch_out(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                               int start_mode, void* const* dst, int dst_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
@@ -1645,7 +1715,7 @@ int ipls_agg_reduce_batch_out(ipls_agg* h, int p_first, int n_parts, const void*
                     dst_kind == IPLS_DEV_BE);
 }
 
-int ipls_agg_aggregate_round(ipls_agg* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+int dev_aggregate_round(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                              void* avg_out, int avg_kind) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
@@ -1691,57 +1761,14 @@ int ipls_agg_aggregate_round(ipls_agg* h, int p_first, int n_parts, const void* 
 // ---- pubsub ingest: base64url (x layers) -> frame -> fold, on the device ----
 namespace {
 
-// Strip and validate the '=' tail of a java.util.Base64 URL text (the rules
-// Decoder.decode0 enforces) -> data chars, or -1 (IllegalArgumentException).
-// `tail` holds the last k >= min(n, 3) chars of an n-char text, so the inner
-// layer's ends can be checked from a few host-decoded bytes: the '=' rules
-// hang on the data-char count of the WHOLE text, not of the window.
-int64_t b64_data_chars(const uint8_t* tail, int64_t k, int64_t n) {
-  int64_t pad = 0;
-  while (pad < k && pad < 3 && tail[k - 1 - pad] == '=') ++pad;
-  const int64_t d = n - pad;
-  const int64_t r = d % 4;
-  if (r == 1) return -1;                       // dangling single char
-  if (pad == 0) return d;
-  if (pad == 1 && r == 3) return d;            // "xxx="
-  if (pad == 2 && r == 2) return d;            // "xx=="
-  return -1;                                   // "=" / "x=" / "xx=" / "===" ...
-}
-
-int64_t b64_out_len(int64_t d) { return 3 * (d / 4) + (d % 4 == 2 ? 1 : d % 4 == 3 ? 2 : 0); }
-
 // Copy-issuing threads of the pubsub ingest (IPLS_INGEST_COPY_THREADS, 1..4).
 int ingest_copy_threads() {
   static const int n = [] {
     const char* e = std::getenv("IPLS_INGEST_COPY_THREADS");
     const int v = e ? std::atoi(e) : 2;
-    return std::max(1, std::min(v, (int)ipls_agg::kCopyThreads));
+    return std::max(1, std::min(v, (int)ipls_dev::kCopyThreads));
   }();
   return n;
-}
-
-// Host decode of output bytes [lo, hi) of a base64url text with `d` data chars
-// (hi <= b64_out_len(d)), as Decoder.decode0 produces them.  false if a char
-// of the units touched is outside the alphabet; the device flags it too.
-bool b64_host_bytes(const uint8_t* t, int64_t d, int64_t lo, int64_t hi, uint8_t* out) {
-  bool ok = true;
-  for (int64_t u = lo / 3; 3 * u < hi; ++u) {
-    unsigned v = 0;
-    for (int c = 0; c < 4; ++c) {
-      const int64_t i = 4 * u + c;
-      if (i >= d) break;
-      const unsigned ch = t[i];
-      unsigned x = ch - 'A' < 26u ? ch - 'A' : ch - 'a' < 26u ? ch - 'a' + 26 : ch - '0' < 10u ? ch - '0' + 52
-                 : ch == '-' ? 62u : ch == '_' ? 63u : 0x100u;
-      if (x > 63) ok = false;
-      v |= (x & 63u) << (18 - 6 * c);
-    }
-    for (int b = 0; b < 3; ++b) {
-      const int64_t j = 3 * u + b;
-      if (j >= lo && j < hi) out[j - lo] = (uint8_t)(v >> (16 - 8 * b));
-    }
-  }
-  return ok;
 }
 
 }  // namespace
@@ -1752,7 +1779,7 @@ bool b64_host_bytes(const uint8_t* t, int64_t d, int64_t lo, int64_t hi, uint8_t
 // copy_stream while `stream` decodes the previous ones behind a per-message
 // event; one sync reads the invalid-char flags, then each partition's frames
 // are folded in message order.
-int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
+int dev_ingest_pubsub(ipls_dev* h, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
                            int layers, const int32_t* parts, int32_t* status) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
@@ -1768,38 +1795,14 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
   std::vector<int64_t> dc(n_msgs, 0), dc2(n_msgs, 0);
   std::vector<uint8_t> decode(n_msgs, 0);
   for (int i = 0; i < n_msgs; ++i) {
-    const int64_t d = lens[i] >= 0 ? b64_data_chars(msgs[i], lens[i], lens[i]) : -1;
-    if (d < 0) { st[i] = IPLS_E_FORMAT; continue; }
-    dc[i] = d;
-    bool ok = true;
-    int64_t fl = 0;   // frame length
-    uint8_t hdr[14];
-    if (layers == 2) {
-      const int64_t n = b64_out_len(d), k = std::min<int64_t>(4, n);
-      uint8_t tail[4];
-      ok = b64_host_bytes(msgs[i], d, n - k, n, tail);
-      const int64_t t = ok ? b64_data_chars(tail, k, n) : -1;
-      if (t < 0) { st[i] = IPLS_E_FORMAT; continue; }
-      dc2[i] = t;
-      fl = b64_out_len(dc2[i]);
-      if (fl >= 14) {
-        uint8_t mid[20];
-        const int64_t c = std::min<int64_t>(dc2[i], 20);   // 20 inner chars -> frame bytes 0..14
-        ok = b64_host_bytes(msgs[i], d, 0, c, mid) && b64_host_bytes(mid, c, 0, 14, hdr);
-      }
-    } else {
-      dc2[i] = d;
-      fl = b64_out_len(d);
-      if (fl >= 14) ok = b64_host_bytes(msgs[i], d, 0, 14, hdr);
-    }
-    if (!ok) { st[i] = IPLS_E_FORMAT; continue; }
-    // [i16 pid][i32 n][i32 partition][i32 iteration] -- n against the real frame length
-    const int32_t n = fl >= 14 ? (int32_t)rd_be32_host(&hdr[2]) : 0;
-    if (fl < 14 || n < 0 || 14 + 8 * (int64_t)n > fl) { st[i] = IPLS_E_FORMAT; continue; }
+    const pubsub::Pre pre = pubsub::precheck(msgs[i], lens[i], layers);   // pubsub_host.cpp
+    if (pre.status) { st[i] = pre.status; continue; }
+    dc[i] = pre.dc;
+    dc2[i] = pre.dc2;
     decode[i] = 1;
-    if (n == 0) { post[i] = 1; continue; }          // arr_len == 0 -> null gradient: no fold
-    const int p = parts ? parts[i] : (int32_t)rd_be32_host(&hdr[6]);
-    if (p < 0 || p >= h->P || n < h->len[p]) { post[i] = IPLS_E_RANGE; continue; }
+    if (pre.n == 0) { post[i] = 1; continue; }      // arr_len == 0 -> null gradient: no fold
+    const int p = parts ? parts[i] : pre.a;
+    if (p < 0 || p >= h->P || pre.n < h->len[p]) { post[i] = IPLS_E_RANGE; continue; }
     route[i] = p;
   }
 
@@ -1908,7 +1911,7 @@ int ipls_agg_ingest_pubsub(ipls_agg* h, int target, const uint8_t* const* msgs, 
   return 0;
 }
 
-int ipls_agg_blend(ipls_agg* h, int p, int target, const void* src, int64_t n, int src_kind, double a, double b) {
+int dev_blend(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind, double a, double b) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -1935,7 +1938,7 @@ int ipls_agg_blend(ipls_agg* h, int p, int target, const void* src, int64_t n, i
   return IPLS_OK;
 }
 
-int ipls_agg_scale(ipls_agg* h, int p, int dst_target, int src_target, double c) {
+int dev_scale(ipls_dev* h, int p, int dst_target, int src_target, double c) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -2041,7 +2044,7 @@ int64_t ipls_pair_encode(int32_t workers, const void* g, int64_t n, int g_kind, 
   return total;
 }
 
-int64_t ipls_agg_commit_partial(ipls_agg* h, int p, int32_t workers, uint8_t* out, int64_t out_cap) {
+int64_t dev_commit_partial(ipls_dev* h, int p, int32_t workers, uint8_t* out, int64_t out_cap) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
@@ -2064,7 +2067,7 @@ int64_t ipls_agg_commit_partial(ipls_agg* h, int p, int32_t workers, uint8_t* ou
   return total;
 }
 
-int64_t ipls_agg_merge_files(ipls_agg* h, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
+int64_t dev_merge_files(ipls_dev* h, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
                              uint8_t* out, int64_t out_cap) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
@@ -2157,4 +2160,93 @@ int64_t ipls_frame_encode(const double* g, int64_t n, int g_kind, int32_t a, int
   return total;
 }
 
-}  // extern "C"
+// ---- Marshall_Packet of an accumulator, encoded on the device (a9) ----
+// IPLS.java:1429-1430 publishes the aggregator's partial sum as
+// Marshall_Packet(Aggregated_Gradients[p], id, iteration, workers + 1, 3):
+// the frame (MyIPFSClass.java:990-1013) base64url-encoded with padding
+// (:1016).  The text is produced by k_b64url_encode_frame straight from the
+// accumulator: no host pass over the doubles, no blocking copy of them.
+int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_t pid, const uint8_t* origin,
+                    int32_t origin_len, void* out, int64_t out_cap, int out_kind) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  IPLS_LOCK(h);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (origin_len < 0 || (origin_len > 0 && !origin)) return fail(h, IPLS_E_INVAL, "bad origin");
+  if (out_kind != IPLS_HOST_TEXT && out_kind != IPLS_DEV_TEXT) return fail(h, IPLS_E_INVAL, "out_kind HOST_TEXT/DEV_TEXT");
+  const int64_t n = h->len[p];
+  const int64_t F = 14 + 8 * n + origin_len;
+  const int64_t T = pubsub::b64_enc_len(F);
+  if (!out) return T;
+  if (out_cap < T) return fail(h, IPLS_E_RANGE, "publish text needs %lld bytes", (long long)T);
+  HIP_TRY(h, hipSetDevice(h->device));
+  FrameEnc fe{};
+  const uint32_t hv[3] = {(uint32_t)n, (uint32_t)a, (uint32_t)b};
+  fe.hdr[0] = (unsigned char)((uint16_t)pid >> 8);   // putShort(0, pid)
+  fe.hdr[1] = (unsigned char)pid;
+  for (int f = 0; f < 3; ++f)                        // putInt(2 | 6 | 10, ...)
+    for (int i = 0; i < 4; ++i) fe.hdr[2 + 4 * f + i] = (unsigned char)(hv[f] >> (24 - 8 * i));
+  fe.n = n;
+  fe.origin_len = origin_len;
+  fe.origin = nullptr;
+  if (origin_len > 0) {
+    void* d = nullptr;
+    if (int rc = upload_table(h, origin, (size_t)origin_len, &d)) return rc;
+    fe.origin = (const unsigned char*)d;
+  }
+  uint8_t* zf = zero_flag(h, p, target);
+  const unsigned long long* src =
+      (zf && *zf) ? nullptr : (const unsigned long long*)(h->arena + target_off(h, p, target));
+  unsigned char* dst = (unsigned char*)out;
+  const bool dev_direct = out_kind == IPLS_DEV_TEXT && !((uintptr_t)out & 15);
+  if (!dev_direct) {
+    if (int rc = ensure_scratch(h, (size_t)T + 64)) return rc;
+    dst = (unsigned char*)h->d_scratch;
+  }
+  const int64_t groups = (F + 23) / 24;
+  hipLaunchKernelGGL(k_b64url_encode_frame, dim3(std::max(1u, std::min<unsigned>(blocks_for(groups, kBlock), 8192))),
+                     dim3(kBlock), 0, h->stream, fe, src, dst, groups, T);
+  HIP_TRY(h, hipGetLastError());
+  if (out_kind == IPLS_DEV_TEXT) {
+    // stream-ordered like every device-only call (the origin bytes were
+    // already copied into the pinned upload ring)
+    if (!dev_direct) HIP_TRY(h, hipMemcpyAsync(out, dst, (size_t)T, hipMemcpyDeviceToDevice, h->stream));
+    return T;
+  }
+  if (int rc = d2h(h, out, dst, (size_t)T)) return rc;
+  return T;
+}
+
+// ---- engine plumbing used by the multi-device front (ipls_agg.cpp) ----
+int dev_device(const ipls_dev* h) { return h ? h->device : -1; }
+
+int dev_last_launch(const ipls_dev* h, ipls_launch_info* out) {
+  if (!h || !out) return IPLS_E_INVAL;
+  *out = h->last_launch;
+  return IPLS_OK;
+}
+
+// Fixed-order fold of k device buckets per destination into caller device
+// buffers that are NOT this engine's partitions (a replica slot's partial
+// sums): lens[q] doubles each, dst[q] native doubles.  Same kernels, same
+// order as reduce_batch_out.
+int dev_reduce_ext(ipls_dev* h, int n, const int64_t* lens, const void* const* bufs, int k, bool be_in,
+                   int start_mode, void* const* dst) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  IPLS_LOCK(h);
+  HIP_TRY(h, hipSetDevice(h->device));
+  return reduce_dev(h, 0, n, bufs, k, be_in, start_mode, IPLS_TGT_AGG, dst, false, nullptr, false, lens);
+}
+
+// Collect_Replicas' length rule (IPLS.java:1225) over this engine's stored
+// Other_Replica_Gradients, without folding anything.
+int dev_other_check(ipls_dev* h) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  std::lock_guard<std::mutex> lk(h->mu);
+  for (auto& kv : h->other)
+    if (kv.second.n > h->len[kv.first.first])
+      return fail(h, IPLS_E_RANGE, "stored replica of %lld doubles > partition %d length %lld "
+                  "(ArrayIndexOutOfBoundsException, IPLS.java:1225)", (long long)kv.second.n,
+                  kv.first.first + h->p_lo, (long long)h->len[kv.first.first]);
+  return IPLS_OK;
+}

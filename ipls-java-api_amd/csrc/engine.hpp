@@ -1,0 +1,66 @@
+// engine.hpp -- the single-device aggregation engine (engine.hip) as the
+// multi-device front (ipls_agg.cpp) sees it.  One engine holds the
+// accumulators of a contiguous block of the handle's partitions on one GPU;
+// engine partition q is handle partition p_lo + q.  Every function has the
+// meaning of the C-ABI entry point of the same suffix (include/ipls_agg.h)
+// restricted to that block; none of them is exported from the library.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/ipls_agg.h"
+
+struct ipls_dev;
+
+const char* dev_last_error(const ipls_dev* h);
+void dev_set_thread_error(const char* msg);
+int dev_geometry(const ipls_agg_cfg* cfg, std::vector<int64_t>& len, std::vector<int64_t>& off, int64_t& chunk,
+                 std::string& why);
+int dev_open(const ipls_agg_cfg* cfg, int device, int p_lo, int p_hi, ipls_dev** out);
+int dev_close(ipls_dev* h);
+int dev_device(const ipls_dev* h);
+void* dev_stream(ipls_dev* h);
+int dev_sync(ipls_dev* h);
+int dev_wait(ipls_dev* h, uint64_t ticket);
+int dev_flush(ipls_dev* h);
+int dev_set_coalesce(ipls_dev* h, int max_group);
+int dev_last_launch(const ipls_dev* h, ipls_launch_info* out);
+
+int dev_load_model(ipls_dev* h, const void* src, int64_t n, int src_kind);
+int dev_split(ipls_dev* h, const void* flat, int64_t n, int src_kind, int p, void* dst, int dst_kind);
+int dev_update_gradient(ipls_dev* h, const void* flat, int64_t n, int src_kind, const int32_t* owned, int n_owned);
+int dev_accumulate(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind);
+int dev_accumulate_async(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind, uint64_t* ticket);
+int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64_t n_bytes);
+int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** gbuf, int64_t* glen);
+int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind);
+int dev_other_check(ipls_dev* h);
+int dev_collect_replicas(ipls_dev* h, int32_t* participants);
+int dev_reduce_batch(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+                     int start_mode, int target);
+int dev_reduce_batch_out(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+                         int start_mode, void* const* dst, int dst_kind);
+int dev_reduce_ext(ipls_dev* h, int n, const int64_t* lens, const void* const* bufs, int k, bool be_in,
+                   int start_mode, void* const* dst);
+int dev_ingest_pubsub(ipls_dev* h, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
+                      int layers, const int32_t* parts, int32_t* status);
+int dev_blend(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind, double a, double b);
+int dev_scale(ipls_dev* h, int p, int dst_target, int src_target, double c);
+int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_out);
+int dev_aggregate_round(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
+                        void* avg_out, int avg_kind);
+int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind);
+int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind);
+int dev_read(ipls_dev* h, int p, int target, void* dst, int64_t n, int dst_kind);
+int dev_promote_future(ipls_dev* h, const int32_t* parts, int n_parts);
+int dev_reset(ipls_dev* h, int p);
+int dev_device_ptr(ipls_dev* h, int p, int target, void** ptr);
+int dev_checksum(ipls_dev* h, int p, int target, uint64_t* out);
+int64_t dev_commit_partial(ipls_dev* h, int p, int32_t workers, uint8_t* out, int64_t out_cap);
+int64_t dev_merge_files(ipls_dev* h, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
+                        uint8_t* out, int64_t out_cap);
+int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_t pid, const uint8_t* origin,
+                    int32_t origin_len, void* out, int64_t out_cap, int out_kind);

@@ -23,6 +23,7 @@ namespace ipls {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4w __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
 
@@ -836,6 +837,98 @@ __global__ __launch_bounds__(kBlock) void k_b64url_decode(const unsigned char* _
     }
   }
   if (bad) atomicOr(err + m, 1);
+}
+
+// ---------------------------------------------------------------------------
+// k_b64url_encode_frame: Marshall_Packet (MyIPFSClass.java:990-1017) of an
+// accumulator, straight from HBM -- the frame
+//   [i16 pid][i32 n][i32 a][i32 b][n x f64 big-endian][origin bytes]
+// encoded by Base64.getUrlEncoder (with '=' padding, :1016).  Lane g writes
+// the 32 chars of frame bytes [24g, 24g+24).  Lanes whose window lies inside
+// the payload (all but the first and the last few) load the 4 doubles it
+// spans (it starts 2 bytes into one: 24g - 14 = 8(3g-2) + 2), take the
+// window's 6 big-endian words by funnel shifts and emit 8 units = 2 x 16 B;
+// the others assemble their bytes one at a time.  src == null: the
+// accumulator is logically +0.0 (all payload bytes zero).
+// ---------------------------------------------------------------------------
+struct FrameEnc {
+  unsigned char hdr[16];          // 14 header bytes
+  int64_t n;                      // doubles in the payload
+  int64_t origin_len;
+  const unsigned char* origin;    // device copy of the origin bytes
+};
+
+__device__ __forceinline__ unsigned b64url_char(unsigned v) {
+  return v < 26 ? 'A' + v : v < 52 ? 'a' + (v - 26) : v < 62 ? '0' + (v - 52) : v == 62 ? '-' : '_';
+}
+// 24 bits -> 4 chars packed little-endian (first char in the low byte)
+__device__ __forceinline__ unsigned b64url_quad(unsigned v) {
+  return b64url_char((v >> 18) & 63) | (b64url_char((v >> 12) & 63) << 8) | (b64url_char((v >> 6) & 63) << 16) |
+         (b64url_char(v & 63) << 24);
+}
+
+__device__ __forceinline__ unsigned frame_byte(const FrameEnc& f, const unsigned long long* __restrict__ src,
+                                               int64_t j) {
+  if (j < 14) return f.hdr[j];
+  const int64_t q = j - 14;
+  if (q < 8 * f.n) {
+    if (!src) return 0;
+    const unsigned long long v = ld8(src + (q >> 3));
+    return (unsigned)(v >> (8 * (7 - (q & 7)))) & 0xFF;   // putDouble: big-endian
+  }
+  return f.origin[q - 8 * f.n];
+}
+
+__global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, const unsigned long long* __restrict__ src,
+                                                               unsigned char* __restrict__ out, int64_t groups,
+                                                               int64_t text_len) {
+  const int64_t F = 14 + 8 * f.n + f.origin_len;   // frame bytes
+  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (int64_t)gridDim.x * kBlock) {
+    const int64_t b0 = 24 * g;
+    if (g >= 1 && b0 + 24 <= 14 + 8 * f.n && src) {
+      const unsigned long long* s = src + (3 * g - 2);
+      const unsigned long long v0 = ld8(s), v1 = ld8(s + 1), v2 = ld8(s + 2), v3 = ld8(s + 3);
+      // big-endian words of the 32 payload bytes, then the window's 6 (2 bytes in)
+      const unsigned W[8] = {(unsigned)(v0 >> 32), (unsigned)v0, (unsigned)(v1 >> 32), (unsigned)v1,
+                             (unsigned)(v2 >> 32), (unsigned)v2, (unsigned)(v3 >> 32), (unsigned)v3};
+      unsigned O[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) O[k] = (W[k] << 16) | (W[k + 1] >> 16);
+      const unsigned long long X0 = ((unsigned long long)O[0] << 32) | O[1];
+      const unsigned long long X1 = ((unsigned long long)O[2] << 32) | O[3];
+      const unsigned long long X2 = ((unsigned long long)O[4] << 32) | O[5];
+      u4w c0, c1;
+      c0.x = b64url_quad((unsigned)(X0 >> 40) & 0xFFFFFF);
+      c0.y = b64url_quad((unsigned)(X0 >> 16) & 0xFFFFFF);
+      c0.z = b64url_quad((unsigned)((X0 << 8) | (X1 >> 56)) & 0xFFFFFF);
+      c0.w = b64url_quad((unsigned)(X1 >> 32) & 0xFFFFFF);
+      c1.x = b64url_quad((unsigned)(X1 >> 8) & 0xFFFFFF);
+      c1.y = b64url_quad((unsigned)((X1 << 16) | (X2 >> 48)) & 0xFFFFFF);
+      c1.z = b64url_quad((unsigned)(X2 >> 24) & 0xFFFFFF);
+      c1.w = b64url_quad((unsigned)X2 & 0xFFFFFF);
+      *(IPLS_GLOBAL u4w*)(out + 32 * g) = c0;
+      *(IPLS_GLOBAL u4w*)(out + 32 * g + 16) = c1;
+      continue;
+    }
+    // header / tail lanes: byte by byte, '=' padding on the last unit
+    for (int u = 0; u < 8; ++u) {
+      const int64_t j = b0 + 3 * u;
+      if (j >= F) break;
+      const int nb = F - j >= 3 ? 3 : (int)(F - j);
+      unsigned v = frame_byte(f, src, j) << 16;
+      if (nb > 1) v |= frame_byte(f, src, j + 1) << 8;
+      if (nb > 2) v |= frame_byte(f, src, j + 2);
+      unsigned q = b64url_quad(v);
+      if (nb < 3) q = (q & 0x00FFFFFFu) | ((unsigned)'=' << 24);
+      if (nb < 2) q = (q & 0x0000FFFFu) | ((unsigned)'=' << 16);
+      unsigned char* o = out + 32 * g + 4 * u;
+      o[0] = (unsigned char)q;
+      o[1] = (unsigned char)(q >> 8);
+      o[2] = (unsigned char)(q >> 16);
+      o[3] = (unsigned char)(q >> 24);
+    }
+  }
+  (void)text_len;
 }
 
 // ---------------------------------------------------------------------------

@@ -6,13 +6,14 @@ The arithmetic runs in hand-written gfx950 HIP kernels inside
 binding plus the Middleware wire codec.
 """
 from ._native import (  # noqa: F401
-    ALL_PARTITIONS, DEV_BE, DEV_F64, HOST_BE, HOST_BE_CANON, HOST_F64, HOST_FRAME, HOST_PAIR,
-    START_ACCUM, START_FIRST, START_ZERO, TGT_AGG, TGT_FUTURE, TGT_REP, TGT_WADDR, TGT_WEIGHTS,
+    ALL_PARTITIONS, DEV_BE, DEV_F64, DEV_TEXT, HOST_BE, HOST_BE_CANON, HOST_F64, HOST_FRAME, HOST_PAIR,
+    HOST_TEXT, KERNEL_FOLD1, KERNEL_REDUCE, KERNEL_REDUCE_SCALAR, KERNEL_ROUND, SHAPE_BIG, SHAPE_MID,
+    SHAPE_SMALL, START_ACCUM, START_FIRST, START_ZERO, TGT_AGG, TGT_FUTURE, TGT_REP, TGT_WADDR, TGT_WEIGHTS,
     IplsError, lib,
 )
 from .aggregator import (  # noqa: F401
     Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, encode_secure, frame_encode, frame_parse, pair_encode,
-    pair_parse, synth_fill,
+    pair_parse, shard_plan, synth_fill,
 )
 
 SEED = 0x1B5_2026  # synthetic workload seed (SURVEY.md §8(d))

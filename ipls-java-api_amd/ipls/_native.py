@@ -22,6 +22,10 @@ IPLS_E_DEVICE, IPLS_E_FORMAT, IPLS_E_NODEV = -5, -6, -7
 
 TGT_AGG, TGT_REP, TGT_WEIGHTS, TGT_WADDR, TGT_FUTURE = 0, 1, 2, 3, 4
 HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON, HOST_PAIR = 0, 1, 2, 3, 4, 5, 6
+HOST_TEXT, DEV_TEXT = 7, 8
+KERNEL_REDUCE, KERNEL_ROUND, KERNEL_FOLD1, KERNEL_REDUCE_SCALAR = 1, 2, 3, 4
+SHAPE_BIG, SHAPE_MID, SHAPE_SMALL = 1, 2, 3
+ABI_VERSION = 2
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1
 
@@ -56,6 +60,19 @@ class AggCfg(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("flags", ctypes.c_int32),
         ("bucket_len", ctypes.c_int64),
+        ("devices", ctypes.POINTER(ctypes.c_int32)),
+        ("n_devices", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class LaunchInfo(ctypes.Structure):
+    _fields_ = [
+        ("kernel", ctypes.c_int32), ("shape", ctypes.c_int32), ("block", ctypes.c_int32),
+        ("vectors", ctypes.c_int32), ("seqf", ctypes.c_int32), ("map", ctypes.c_int32),
+        ("grid", ctypes.c_int64),
+        ("be_in", ctypes.c_int32), ("be_out", ctypes.c_int32), ("start", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -107,6 +124,12 @@ SIGNATURES = {
     "ipls_pair_encode": (_i64, [_i32, _vp, _i64, _i, _vp, _i64]),
     "ipls_agg_commit_partial": (_i64, [_vp, _i, _i32, _vp, _i64]),
     "ipls_agg_merge_files": (_i64, [_vp, _P(_vp), _P(_i64), _i, _i, _vp, _i64]),
+    "ipls_agg_partition_device": (_i, [_vp, _i, _P(_i32), _P(_vp)]),
+    "ipls_shard_plan": (_i, [_i32, _i32, _P(_i32)]),
+    "ipls_agg_reduce_partial": (_i, [_vp, _i, _i, _i, _P(_vp), _i, _i, _i]),
+    "ipls_agg_combine_partials": (_i, [_vp, _i, _i]),
+    "ipls_agg_publish_partial": (_i64, [_vp, _i, _i, _i32, _i32, _i16, _vp, _i32, _vp, _i64, _i]),
+    "ipls_agg_last_launch": (_i, [_vp, _P(LaunchInfo)]),
 }
 
 _lib = None

@@ -88,18 +88,24 @@ class Aggregator:
 
     def __init__(self, model_size: int = 0, n_partitions: int = 1, *, max_peers: int = 0,
                  partial_aggregation: int = 0, secure: bool = False, device: int = 0,
-                 bucket_len: int = 0):
+                 bucket_len: int = 0, devices=None):
+        """``devices``: a list of HIP device ordinals shards the partitions over
+        several GPUs in contiguous blocks (cfg.devices, ipls_shard_plan); a
+        device may repeat (several shards on one GPU)."""
         self._lib = N.lib()
+        devs = None if devices is None else (ctypes.c_int32 * len(devices))(*devices)
         cfg = N.AggCfg(model_size=model_size, n_partitions=n_partitions, max_peers=max_peers,
                        partial_aggregation=partial_aggregation, secure=int(bool(secure)),
-                       device=device, flags=0, bucket_len=bucket_len)
+                       device=device, flags=0, bucket_len=bucket_len,
+                       devices=devs, n_devices=0 if devices is None else len(devices), reserved=0)
         h = ctypes.c_void_p()
         N.check(self._lib.ipls_agg_open(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
         self.model_size = model_size
         self.n_partitions = n_partitions
         self.secure = bool(secure)
-        self.device = device
+        self.device = device if devices is None else devices[0]
+        self.devices = [device] if devices is None else list(devices)
         self.lengths = [self.partition_len(p) for p in range(n_partitions)]
         self.offsets = [self.partition_offset(p) for p in range(n_partitions)]
         self.flat_size = max(o + L - 1 for o, L in zip(self.offsets, self.lengths))
@@ -478,6 +484,61 @@ class Aggregator:
         else:
             self.Update(d, partition, from_clients=False)
 
+    # ---- multi-GPU: shards and replica slots (include/ipls_agg.h, cfg.devices) ----
+    def partition_device(self, partition: int):
+        """(device ordinal, HIP stream) of the shard that owns ``partition``."""
+        d, st = ctypes.c_int32(), ctypes.c_void_p()
+        self._chk(self._lib.ipls_agg_partition_device(self._h, partition, ctypes.byref(d), ctypes.byref(st)))
+        return d.value, int(st.value or 0)
+
+    def reduce_partial(self, slot: int, p_first: int, buckets, *, start_mode: int = N.START_ZERO,
+                       big_endian: bool = False):
+        """Replica slot ``slot`` (a shard that does not own these partitions)
+        folds buckets resident on its GPU into its partial sums (an aggregator
+        of the partition other than its owner, IPLS.java:1402-1431)."""
+        n_parts = len(buckets)
+        k = len(buckets[0]) if n_parts else 0
+        flat = [b.ptr if isinstance(b, DeviceBuffer) else int(b) for row in buckets for b in row]
+        if len(flat) != n_parts * k:
+            raise ValueError("every partition needs the same number of buckets")
+        arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
+        self._chk(self._lib.ipls_agg_reduce_partial(self._h, slot, p_first, n_parts, arr, k,
+                                                    N.DEV_BE if big_endian else N.DEV_F64, start_mode))
+
+    def combine_partials(self, p_first: int = 0, n_parts: int | None = None) -> int:
+        """REP[p] += every slot's partial of p, slots ascending, read over xGMI
+        by the owner's fold kernel (Collect_Replicas, IPLS.java:1449).
+        Returns the number of partials folded."""
+        n = self.n_partitions - p_first if n_parts is None else n_parts
+        return self._chk(self._lib.ipls_agg_combine_partials(self._h, p_first, n))
+
+    # ---- publish-side codec (a9) ----
+    def publish_partial(self, partition: int, a: int, b: int, *, pid: int = 3, origin: bytes = b"",
+                        target: int = N.TGT_AGG, out=None) -> bytes | int:
+        """Marshall_Packet(target[p], origin, a, b, pid) as Base64.getUrlEncoder
+        text (MyIPFSClass.java:990-1016; IPLS.java:1429-1430 publishes AGG with
+        a = iteration, b = workers + 1, pid 3), encoded on the GPU.  Returns the
+        text bytes, or its length when ``out`` is a DeviceBuffer/int address
+        (device text, stream-ordered)."""
+        o = np.frombuffer(bytes(origin), dtype=np.uint8)
+        op = o.ctypes.data if o.size else None
+        n = self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op, o.size,
+                                                         None, 0, N.HOST_TEXT))
+        if out is not None:
+            ptr = out.ptr if isinstance(out, DeviceBuffer) else int(out)
+            return self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op,
+                                                                o.size, ptr, n, N.DEV_TEXT))
+        buf = np.empty(max(1, n), dtype=np.uint8)
+        self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op, o.size,
+                                                     buf.ctypes.data, n, N.HOST_TEXT))
+        return buf[:n].tobytes()
+
+    def last_launch(self) -> dict:
+        """What the last fold launch ran (kernel, shape, lanes, vectors, SEQ code, map, grid)."""
+        li = N.LaunchInfo()
+        self._chk(self._lib.ipls_agg_last_launch(self._h, ctypes.byref(li)))
+        return {f: getattr(li, f) for f, _ in N.LaunchInfo._fields_ if f != "reserved"}
+
     # ---- state access ----
     def read(self, partition: int, target: int = N.TGT_AGG, *, big_endian: bool = False):
         L = self.lengths[partition]
@@ -530,6 +591,13 @@ class PinnedBuffer:
 
 
 # ---- handle-free device utilities ----
+def shard_plan(n_partitions: int, n_shards: int) -> list[int]:
+    """Owner shard of every partition (contiguous blocks, p / ceil(P/G))."""
+    out = (ctypes.c_int32 * max(1, n_partitions))()
+    N.check(N.lib().ipls_shard_plan(n_partitions, n_shards, out))
+    return list(out)[:n_partitions]
+
+
 def synth_fill(buf: DeviceBuffer, p: int, k: int, seed: int, stream: int = 0):
     N.check(N.lib().ipls_synth_fill(buf.ptr, buf.n, seed, p, k, buf.kind, stream or None))
 

@@ -181,10 +181,14 @@ def main():
     # full-size synthetic configs: per-partition checksum of the ZERO-start
     # fixed-order sum (C oracle, OpenMP over elements, per-element order intact)
     full = {}
-    for name, (P, L, K) in {"B": (16, 1048576, 8), "C": (16, 4194304, 32)}.items():
+    for name, (P, L, K) in {"B": (16, 1048576, 8), "C": (16, 4194304, 32), "D": (64, 4194304, 32)}.items():
         full[name] = {"partitions": P, "bucket_len": L, "peers": K,
                       "sum_checksum": [O.c_synth_sum_checksum(L, p, K) for p in range(P)]}
         print(name, full[name]["sum_checksum"][:2], flush=True)
+    # the fused round's averages (GetPartitions divide of the same sums), config C
+    full["C"]["avg_checksum"] = [O.c_synth_avg_checksum(4194304, p, 32) for p in range(16)]
+    # D's first 16 partitions are C's (the counter formula is keyed by (p, k, i))
+    assert full["D"]["sum_checksum"][:16] == full["C"]["sum_checksum"]
     # spot-check the C checksum path against the Python fold on one partition of B
     bufs = [O.synth_bucket(1048576, 3, k) for k in range(8)]
     assert O.checksum(O.reduce(bufs, 1048576)) == full["B"]["sum_checksum"][3]

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for s in declared_symbols():
         assert hasattr(L, s), f"{s} declared in include/ipls_agg.h but not exported"
         assert s in N.SIGNATURES, f"{s} has no ctypes signature"
-    assert L.ipls_agg_abi_version() == 1
+    assert L.ipls_agg_abi_version() == N.ABI_VERSION == 2
 
 
 def test_header_constants_match_binding():
@@ -44,7 +44,10 @@ def test_header_constants_match_binding():
     assert defs["IPLS_START_ZERO"] == N.START_ZERO and defs["IPLS_START_FIRST"] == N.START_FIRST
     assert defs["IPLS_E_RANGE"] == N.IPLS_E_RANGE and defs["IPLS_E_NODEV"] == N.IPLS_E_NODEV
     assert defs["IPLS_ALL_PARTITIONS"] == N.ALL_PARTITIONS
-    assert ctypes.sizeof(N.AggCfg) == 40
+    assert ctypes.sizeof(N.AggCfg) == 56
+    assert ctypes.sizeof(N.LaunchInfo) == 48
+    assert defs["IPLS_HOST_TEXT"] == N.HOST_TEXT and defs["IPLS_DEV_TEXT"] == N.DEV_TEXT
+    assert defs["IPLS_SHAPE_BIG"] == N.SHAPE_BIG and defs["IPLS_KERNEL_ROUND"] == N.KERNEL_ROUND
 
 
 def test_library_is_gfx950_code_object():
@@ -116,3 +119,24 @@ def test_null_handle_fails_cleanly():
         checked += 1
     assert checked >= 25
     assert L.ipls_agg_close(None) == 0                     # closing nothing is a no-op
+
+
+@pytest.mark.parametrize("P,G", [(16, 1), (64, 4), (128, 8), (3, 8), (17, 4), (5, 2)])
+def test_shard_plan_contiguous_blocks(P, G):
+    """-pa segments map to devices in contiguous blocks,
+    partition p on shard p / ceil(P/G) (no GPU needed)."""
+    import ipls
+    per = -(-P // G)
+    owner = ipls.shard_plan(P, G)
+    assert owner == [p // per for p in range(P)]
+    assert owner == sorted(owner) and max(owner) < G
+    if P % G == 0:
+        assert all(owner.count(s) == P // G for s in range(G))   # 16/GPU in configs E and F
+
+
+def test_shard_plan_rejects_bad_arguments():
+    import ipls
+    with pytest.raises(ipls.IplsError):
+        ipls.shard_plan(0, 2)
+    with pytest.raises(ipls.IplsError):
+        ipls.shard_plan(4, 0)

@@ -1,0 +1,284 @@
+"""GPU parity of the multi-GPU handle (cfg.devices) and of the publish-side
+codec, through the C-ABI.
+
+The box has one MI355X, so the sharded handle runs with device lists like
+[0, 0] or [0, 0, 0]: every shard is its own engine (own stream, own arena),
+partitions are routed by the same contiguous-block plan as on eight GPUs, and
+the replica-slot combine runs the same cross-shard event ordering and the
+same owner-side fold kernel over the slots' partials -- only the xGMI hop is
+missing (peer access is enabled between distinct devices at open).  It is
+"unmeasured on hardware" beyond one GPU until the driver's 8-GPU run.
+
+References: IPLS.java:1402-1468 (replica aggregators' partials, Collect_Replicas,
+AggregatePartition), Updater.java:40-44 (REP fold), MyIPFSClass.java:990-1016
+(Marshall_Packet), IPLS.java:1429-1430 (the publish call), IPLS.java:851-866
+(ThreadReceiver decode).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_bits_equal
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ipls():
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    import ipls as m
+    return m
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle as o   # checker only
+    return o
+
+
+def dev_buckets(ipls, P, L, K, p0=0, k0=0, be=False, seed=None):
+    from oracle import oracle as O
+    t = torch.empty(P * K * (L + 2), dtype=torch.float64, device="cuda")
+    base = (int(t.data_ptr()) + 15) // 16 * 16
+    rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * (L + 2), L, big_endian=be) for k in range(K)]
+            for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[q][k], p0 + q, k0 + k, O.SEED if seed is None else seed)
+    torch.cuda.synchronize()
+    return t, rows
+
+
+def test_sharded_handle_routes_like_one_engine(ipls, O):
+    """A model-geometry handle (M = 1,000,003, -pa 5) over shards [0, 0]
+    (partitions 0-2 | 3-4) against the one-shard handle on the same calls:
+    InitializeWeights, UpdateGradient over every shard, arrivals from host
+    and device, a reduce_batch spanning both shards, AggregatePartition(all),
+    GetPartitions (doubles, the Middleware wire stream, device), and the
+    fused round with host averages."""
+    M, P, K = 1_000_003, 5, 4
+    one = ipls.Aggregator(M, P, max_peers=K)
+    two = ipls.Aggregator(M, P, max_peers=K, devices=[0, 0])
+    assert [two.partition_device(p)[0] for p in range(P)] == [0] * P
+    assert ipls.shard_plan(P, 2) == [0, 0, 0, 1, 1]
+    assert two.partition_device(0)[1] != two.partition_device(4)[1]   # one stream per shard
+    model = O.synth_bucket(M, 9, 9)
+    peers = [O.synth_bucket(M, 7, k) for k in range(K)]
+    for agg in (one, two):
+        agg.InitializeWeights(model)
+        agg.UpdateGradient(peers[0], auth_list=[4, 0, 3, 1, 2])
+        for k in (1, 2):
+            parts = O.organize_gradients(peers[k], M, P)
+            for p in range(P):
+                agg.Update(O.be_encode(parts[p]) if k == 1 else parts[p], p)
+    keep, rows = [], []
+    parts3 = O.organize_gradients(peers[3], M, P)
+    for p in range(P):
+        t = torch.from_numpy(parts3[p]).to("cuda")
+        keep.append(t)
+        rows.append([ipls.DeviceBuffer.from_tensor(t)])
+    for agg in (one, two):
+        # rows have one bucket per partition but ragged lengths: one call per partition
+        for p in range(P):
+            agg.reduce_batch(p, [rows[p]], start_mode=ipls.START_ACCUM)
+    for p in range(P):
+        assert_bits_equal(two.read(p), one.read(p), f"AGG[{p}]")
+        assert_bits_equal(two.read(p), O.reduce([O.organize_gradients(g, M, P)[p] for g in peers], one.lengths[p]),
+                          f"oracle AGG[{p}]")
+    for agg in (one, two):
+        agg.AggregatePartition(ipls.ALL_PARTITIONS)
+    assert_bits_equal(two.GetPartitions(), one.GetPartitions(), "GetPartitions")
+    assert two.GetPartitions(wire=True) == one.GetPartitions(wire=True)
+    flat = torch.empty(M, dtype=torch.float64, device="cuda")
+    two.GetPartitions(out=ipls.DeviceBuffer.from_tensor(flat))
+    two.sync()
+    assert_bits_equal(flat.cpu().numpy(), one.GetPartitions(), "GetPartitions device")
+    # fused round across both shards, host averages (one thread per shard)
+    L = 50_001
+    one2, two2 = ipls.Aggregator(n_partitions=4, bucket_len=L), ipls.Aggregator(n_partitions=4, bucket_len=L,
+                                                                                devices=[0, 0])
+    t, rws = dev_buckets(ipls, 4, L, 6)
+    a1 = one2.aggregate_round(0, rws)
+    a2 = two2.aggregate_round(0, rws)
+    assert_bits_equal(a2, a1, "fused round averages")
+    a3 = two2.aggregate_round(1, rws[1:3])        # a sub-range that straddles the shard boundary
+    assert_bits_equal(a3, one2.aggregate_round(1, rws[1:3]), "straddling round")
+    for agg in (one, two, one2, two2):
+        agg.close()
+
+
+def test_replica_slots_combine_in_slot_order(ipls, O):
+    """Contributors of a partition spanning GPUs: the owner
+    folds peers [0, 4), the other shard -- a replica aggregator of the same
+    partitions -- folds peers [4, 8) into its partials; the combine adds the
+    partial to REP and AggregatePartition gives W = AGG + (+0.0 + R), the
+    oracle's replica checksum (IPLS.java:1256, Updater.java:40-44)."""
+    P, L, K, kh = 4, 1_000_003, 8, 4
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0, 0])
+    t, rows = dev_buckets(ipls, P, L, K)
+    own = [r[:kh] for r in rows]
+    far = [r[kh:] for r in rows]
+    agg.reduce_batch(0, own, start_mode=ipls.START_ZERO)
+    # shard 1 is the replica of partitions 0-1, shard 0 of partitions 2-3
+    agg.reduce_partial(1, 0, far[0:2])
+    agg.reduce_partial(0, 2, far[2:4])
+    with pytest.raises(ipls.IplsError):
+        agg.reduce_partial(0, 0, far[0:1])        # shard 0 owns partition 0
+    assert agg.combine_partials() == P
+    assert agg.combine_partials() == 0           # consumed
+    agg.AggregatePartition(ipls.ALL_PARTITIONS)
+    for p in range(P):
+        assert agg.checksum(p, ipls.TGT_WEIGHTS) == O.c_synth_replica_checksum(L, p, K, kh), p
+    # the partial of a second round starts from +0.0 again
+    agg.reduce_batch(0, own, start_mode=ipls.START_ZERO)
+    agg.reduce_partial(1, 0, far[0:2])
+    agg.reduce_partial(0, 2, far[2:4])
+    agg.combine_partials(0, 4)
+    agg.AggregatePartition(ipls.ALL_PARTITIONS)
+    assert [agg.checksum(p, ipls.TGT_WEIGHTS) for p in range(P)] == \
+        [O.c_synth_replica_checksum(L, p, K, kh) for p in range(P)]
+    agg.close()
+
+
+def test_three_slots_fold_order_and_accum(ipls, O):
+    """Three shards, every partition with two remote slots: REP = ((+0.0 +
+    R_a) + R_b) with a < b, on top of a REP that already holds a replica
+    bucket; the partial of one slot built by two reduce_partial calls
+    (ZERO, then ACCUM); BE buckets in one slot."""
+    P, L = 3, 200_003
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0, 0, 0])
+    t, rows = dev_buckets(ipls, P, L, 6)
+    tb, rows_be = dev_buckets(ipls, P, L, 6, be=True)
+    b = [[O.synth_bucket(L, q, k) for k in range(6)] for q in range(P)]
+    pre = [O.synth_bucket(L, 50 + q, 0) for q in range(P)]
+    for q in range(P):
+        agg.reduce_batch(q, [rows[q][0:2]], start_mode=ipls.START_ZERO)
+        agg.Update(pre[q], q, from_clients=False)
+        slots = [s for s in range(3) if s != q]
+        agg.reduce_partial(slots[0], q, [rows[q][2:3]], start_mode=ipls.START_ZERO)
+        agg.reduce_partial(slots[0], q, [rows[q][3:4]], start_mode=ipls.START_ACCUM)
+        agg.reduce_partial(slots[1], q, [rows_be[q][4:6]], big_endian=True)
+    assert agg.combine_partials() == 2 * P
+    for q in range(P):
+        agg_own = O.reduce(b[q][0:2], L)
+        ra = O.reduce(b[q][2:4], L)
+        rb = O.reduce(b[q][4:6], L)
+        rep = ((0.0 + pre[q]) + ra) + rb
+        assert_bits_equal(agg.read(q, ipls.TGT_REP), rep, f"REP[{q}]")
+        s, _ = agg.AggregatePartition(q, with_sum=True, sum_big_endian=False)
+        assert_bits_equal(s, agg_own + rep, f"W[{q}]")
+    agg.close()
+
+
+def test_sharded_ingest_indirect_async_and_replicas(ipls, O):
+    """The rest of the surface on shards [0, 0]: pubsub ingest routed by the
+    frame's partition field, hash-only requests through the handle's ONE
+    Gradient_Buff (a short file folds the previous file's tail even when the
+    two requests land on different shards), queued device arrivals with
+    handle-wide tickets, Other_Replica_Gradients + Collect_Replicas with the
+    Participants counts, and the promotion of future gradients."""
+    M, P = 100_003, 4
+    one = ipls.Aggregator(M, P, max_peers=4)
+    two = ipls.Aggregator(M, P, max_peers=4, devices=[0, 0])
+    Ls = one.lengths
+    msgs = []
+    for k in range(3):
+        g = O.organize_gradients(O.synth_bucket(M, 3, k), M, P)
+        for p in (3, 0, 2, 1):
+            msgs.append(O.pubsub_message(O.frame_encode(g[p], p, 5, 3, b"QmX")))
+    msgs.append(b"not base64!")                               # dropped: FORMAT
+    msgs.append(O.pubsub_message(O.frame_encode(np.ones(9), 7, 5, 3, b"QmX")))   # partition 7: RANGE
+    r1, r2 = one.ingest_pubsub(msgs), two.ingest_pubsub(msgs)
+    assert r1 == r2 and r1[0] == 12 and r1[1][-2:] == [-6, -2]   # FORMAT, RANGE
+    # hash-only requests, alternating shards, short files reuse the stale tail
+    for p, n in ((3, Ls[3]), (0, Ls[0] - 50), (2, 10), (1, 0)):
+        data = O.be_encode(O.synth_bucket(n, p, 11))
+        one.UpdateIndirect(data, p)
+        two.UpdateIndirect(data, p)
+    # queued device arrivals on both shards
+    t, rows = dev_buckets(ipls, P, max(Ls), 2)
+    tickets = []
+    for k in range(2):
+        for p in range(P):
+            b = ipls.DeviceBuffer(rows[p][k].ptr, Ls[p])
+            one.UpdateAsync(b, p)
+            tickets.append(two.UpdateAsync(b, p))
+    two.Wait(tickets[-1])
+    # Other_Replica_Gradients on both shards
+    for agg in (one, two):
+        for p, a in ((0, 7), (3, 2), (3, 9), (1, 2)):
+            agg.OtherReplicaGradients(p, a, O.synth_bucket(Ls[p], p, a))
+            agg.OtherReplicaGradients(p, a, O.synth_bucket(Ls[p] - 3, p, a + 1))
+    c1, c2 = one.Collect_Replicas(), two.Collect_Replicas()
+    assert c1 == c2 and c1[0] == 4 and c1[1] == [2, 2, 0, 4]
+    for p in range(P):
+        assert_bits_equal(two.read(p), one.read(p), f"AGG[{p}]")
+        assert_bits_equal(two.read(p, ipls.TGT_REP), one.read(p, ipls.TGT_REP), f"REP[{p}]")
+    # from-future fold and promotion on a subset spanning both shards
+    for agg in (one, two):
+        for p in range(P):
+            agg.Update(O.synth_bucket(Ls[p], p, 33), p, from_future=True)
+        agg.PromoteFuture([1, 3])
+    for p in range(P):
+        assert_bits_equal(two.read(p), one.read(p), f"promoted AGG[{p}]")
+    one.close()
+    two.close()
+
+
+# ---------------------------------------------------------------------------
+# a9: Marshall_Packet + Base64.getUrlEncoder on the device
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("L,origin", [(7, b""), (7, b"Q"), (7, b"Qm"),
+                                      (100_000, b"QmPeerOrigin46charsxxxxxxxxxxxxxxxxxxxxxxxxxxx"),
+                                      (1_048_581, b"QmY"), (1_048_580, b"QmY")])
+def test_publish_partial_matches_marshall_packet(ipls, O, L, origin):
+    """ipls_agg_publish_partial = Base64.getUrlEncoder().encodeToString(frame)
+    for the frame Marshall_Packet builds from Aggregated_Gradients[p]
+    (MyIPFSClass.java:990-1016), as IPLS.java:1429-1430 calls it (a = the
+    iteration, b = workers + 1, pid 3): every '=' padding case (frame length
+    mod 3), the header-only and tail lanes, a logically-zero accumulator, and
+    device output; and the round trip through the GPU ingest."""
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    # logically +0.0 accumulator (src == null path)
+    z = agg.publish_partial(0, 12, 4, origin=origin)
+    assert z == O.java_b64url_encode(O.frame_encode(np.zeros(L), 12, 4, 3, origin))
+    vals = O.synth_bucket(L, 1, 2)
+    vals[:3] = [-0.0, np.inf, 5e-324]
+    agg.Update(vals, 1)
+    text = agg.publish_partial(1, 12, 4, origin=origin)
+    want = O.java_b64url_encode(O.frame_encode(agg.read(1), 12, 4, 3, origin))
+    assert len(text) == len(want) and text == want
+    # device text
+    buf = torch.empty(len(want) + 16, dtype=torch.uint8, device="cuda")
+    n = agg.publish_partial(1, 12, 4, origin=origin, out=int(buf.data_ptr()))
+    agg.sync()
+    assert n == len(want) and bytes(buf[:n].cpu().numpy()) == want
+    # round trip: the IPFS daemon wraps the text once more (IPLS.java:855-859)
+    rx = ipls.Aggregator(n_partitions=13, bucket_len=L)
+    k, st = rx.ingest_pubsub([O.java_b64url_encode(text)], layers=2)   # routed by field a = 12
+    assert (k, st) == (1, [0])
+    assert_bits_equal(rx.read(12), 0.0 + agg.read(1), "round trip")
+    k, st = rx.ingest_pubsub([text], layers=1, partitions=[0])
+    assert (k, st) == (1, [0])
+    assert_bits_equal(rx.read(0), 0.0 + agg.read(1), "round trip, one layer")
+    rx.close()
+    agg.close()
+
+
+def test_publish_partial_rejects_bad_arguments(ipls):
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=10)
+    with pytest.raises(ipls.IplsError):
+        agg.publish_partial(1, 0, 0)
+    import ctypes
+    from ipls import _native as N
+    lib = N.lib()
+    need = lib.ipls_agg_publish_partial(agg.handle, 0, N.TGT_AGG, 0, 0, 3, None, 0, None, 0, N.HOST_TEXT)
+    buf = (ctypes.c_uint8 * need)()
+    out = ctypes.addressof(buf)
+    assert need == 4 * -(-(14 + 8 * 10) // 3)
+    assert lib.ipls_agg_publish_partial(agg.handle, 0, N.TGT_AGG, 0, 0, 3, None, 0, out, need - 1,
+                                        N.HOST_TEXT) == N.IPLS_E_RANGE
+    assert lib.ipls_agg_publish_partial(agg.handle, 0, N.TGT_AGG, 0, 0, 3, None, 0, out, need,
+                                        N.HOST_F64) == N.IPLS_E_INVAL
+    agg.close()

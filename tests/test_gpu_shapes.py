@@ -1,0 +1,221 @@
+"""GPU parity of the launch shapes the production sizes take.
+
+The fold kernel's dispatch picks a tile shape by how many tiles a batch fills
+(engine.hip launch_reduce_v: big = 1024 lanes x 16 vectors, mid = 256 lanes x
+16 vectors, small = 256 lanes x 8 peers in flight).  Big-endian input at
+R = 16 runs the hand-fenced SEQ schedule (SEQF = 42), START_ACCUM runs R = 8,
+partial last tiles run map 3.  Every case below asserts through
+ipls_agg_last_launch that it reached the shape it was written for, then
+compares with the oracle: bit for bit on whole partitions (C oracle,
+oracle/ipls_oracle.c) and by per-partition checksums of the counter
+workload (tests/golden/golden.json "full", config D = 64 x 4M x 32 in full).
+References: MyIPFSClass.java:444-455 (GetParameters BE decode),
+:105-116 (update_file BE encode), Decentralized_Storage_Receiver.java:239-257
+(FIRST-start merge), Updater.java:115-117 (the fold), IPLS.java:1248-1274 and
+1159-1174 (the fused round).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_bits_equal
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ipls():
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    import ipls as m
+    return m
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle as o   # checker only
+    return o
+
+
+class Pool:
+    """P x K synthetic device buckets of L doubles (BE bytes when `be`), with
+    a 256-B pad between buckets as the bench lays them out, plus one output
+    buffer per partition."""
+
+    def __init__(self, ipls, P, L, K, be, seed, p0=0, out=True):
+        elem = (L + 32 + 31) // 32 * 32
+        self.arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
+        base = (int(self.arena.data_ptr()) + 255) // 256 * 256
+        self.rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L, big_endian=be) for k in range(K)]
+                     for q in range(P)]
+        for q in range(P):
+            for k in range(K):
+                ipls.synth_fill(self.rows[q][k], p0 + q, k, seed)
+        self.outs = None
+        if out:
+            self.out_arena = torch.empty(P * elem + 32, dtype=torch.float64, device="cuda")
+            ob = (int(self.out_arena.data_ptr()) + 255) // 256 * 256
+            self.outs = [ob + 8 * q * elem for q in range(P)]
+        torch.cuda.synchronize()
+
+    def out_host(self, q, L, be):
+        off = self.outs[q] - int(self.out_arena.data_ptr())
+        a = self.out_arena.view(torch.uint8)[off:off + 8 * L].cpu().numpy()
+        return np.frombuffer(a.tobytes(), dtype=">f8" if be else "<f8").astype(np.float64)
+
+    def free(self):
+        del self.arena
+        self.rows = None
+        if self.outs is not None:
+            del self.out_arena
+        torch.cuda.empty_cache()
+
+
+def ref_sum(O, L, p, K, start=None, acc=None):
+    bufs = [O.c_synth_bucket(L, p, k) for k in range(K)]
+    if start is None:
+        start = O.START_ZERO
+    return O.c_reduce(bufs, L, start, acc)
+
+
+def expect(li, ipls, kernel, shape, vectors, seqf, be_in, be_out, mapping=None):
+    got = (li["kernel"], li["shape"], li["vectors"], li["seqf"], li["be_in"], li["be_out"])
+    assert got == (kernel, shape, vectors, seqf, int(be_in), int(be_out)), li
+    if mapping is not None:
+        assert li["map"] == mapping, li
+
+
+def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
+    """Config D exactly: 64 partitions x 4,194,304 BE doubles x 32 peers, BE
+    sum bytes out -- the shipped big shape with the SEQF = 42 schedule
+    (2048 tiles, no partial tile), ZERO and FIRST start; then BE in with
+    native doubles out into the accumulators, and ACCUM (R = 8) on top."""
+    m = golden_meta["full"]["D"]
+    P, L, K = m["partitions"], m["bucket_len"], m["peers"]
+    pool = Pool(ipls, P, L, K, True, golden_meta["seed"])
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    want = m["sum_checksum"]
+    for start in (ipls.START_ZERO, ipls.START_FIRST):
+        agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=True)
+        li = agg.last_launch()
+        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 42, True, True, mapping=0)
+        assert li["block"] == 1024 and li["grid"] == P * L // (1024 * 2 * 16)
+        agg.sync()
+        got = [ipls.checksum_dev(ipls.DeviceBuffer(o, L, big_endian=True)) for o in pool.outs]
+        assert got == want, f"start {start}: partitions {[q for q in range(P) if got[q] != want[q]]} differ"
+    # whole partitions bit for bit (first and last of the batch)
+    for q in (0, P - 1):
+        assert_bits_equal(pool.out_host(q, L, True), ref_sum(O, L, q, K), f"D partition {q}")
+    # BE in, native doubles into AGG (GetParameters decode fused, Updater fold)
+    agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ZERO, big_endian=True)
+    expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 42, True, False)
+    assert [agg.checksum(q) for q in range(P)] == want
+    # ACCUM: S + fold again, BE out (R = 8, compiler schedule)
+    agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ACCUM, big_endian_in=True,
+                         big_endian_out=True)
+    expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 8, 0, True, True)
+    agg.sync()
+    for q in (0, 37):
+        s = ref_sum(O, L, q, K)
+        assert_bits_equal(pool.out_host(q, L, True), ref_sum(O, L, q, K, O.START_ACCUM, s), f"D accum {q}")
+    agg.close()
+    pool.free()
+
+
+@pytest.mark.parametrize("be_out", [True, False])
+def test_be_big_shape_partial_tile(ipls, O, be_out):
+    """>= 512 big tiles with a partial last tile (map 3): 4 x 4,200,001 x 32."""
+    P, L, K = 4, 4_200_001, 32
+    pool = Pool(ipls, P, L, K, True, O.SEED)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    want = [O.c_synth_sum_checksum(L, q, K) for q in range(P)]
+    for start in (ipls.START_ZERO, ipls.START_FIRST):
+        agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=be_out)
+        expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 42, True, be_out, mapping=3)
+        agg.sync()
+        assert [ipls.checksum_dev(ipls.DeviceBuffer(o, L, big_endian=be_out)) for o in pool.outs] == want
+    assert_bits_equal(pool.out_host(P - 1, L, be_out), ref_sum(O, L, P - 1, K), "partial-tile partition")
+    agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ACCUM, big_endian_in=True,
+                         big_endian_out=be_out)
+    expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 8, 0, True, be_out, mapping=3)
+    agg.sync()
+    s = ref_sum(O, L, 2, K)
+    assert_bits_equal(pool.out_host(2, L, be_out), ref_sum(O, L, 2, K, O.START_ACCUM, s), "accum partial tile")
+    agg.close()
+    pool.free()
+
+
+@pytest.mark.parametrize("P,L", [(1, 4_194_304 + 4099), (2, 2_100_003)])
+def test_be_mid_shape(ipls, O, P, L):
+    """One or two partitions: too few big tiles, so the 256-lane mid shape
+    (SEQF = 42 for BE input) with a partial last tile."""
+    K = 32
+    pool = Pool(ipls, P, L, K, True, O.SEED)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    refs = [ref_sum(O, L, q, K) for q in range(P)]
+    for start in (ipls.START_ZERO, ipls.START_FIRST):
+        agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=True)
+        li = agg.last_launch()
+        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_MID, 16, 42, True, True, mapping=3)
+        assert li["block"] == 256
+        agg.sync()
+        for q in range(P):
+            assert_bits_equal(pool.out_host(q, L, True), refs[q], f"mid start {start} partition {q}")
+    agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ACCUM, big_endian_in=True,
+                         big_endian_out=True)
+    li = agg.last_launch()
+    assert (li["kernel"], li["vectors"], li["be_in"]) == (ipls.KERNEL_REDUCE, 8, 1), li
+    agg.sync()
+    for q in range(P):
+        assert_bits_equal(pool.out_host(q, L, True), O.c_reduce([O.c_synth_bucket(L, q, k) for k in range(K)], L,
+                                                                O.START_ACCUM, refs[q]), f"mid accum {q}")
+    agg.close()
+    pool.free()
+
+
+def test_be_fused_round_config_c(ipls, O, golden_meta):
+    """The fused round (k_round: fold + W = AGG + REP + GetPartitions divide)
+    on config C's shape with BE buckets: big shape, SEQF = 42; W and the
+    averages against the oracle's checksums."""
+    m = golden_meta["full"]["C"]
+    P, L, K = m["partitions"], m["bucket_len"], m["peers"]
+    pool = Pool(ipls, P, L, K, True, golden_meta["seed"], out=False)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    avg = torch.empty(P * (L - 1), dtype=torch.float64, device="cuda")
+    agg.aggregate_round(0, pool.rows, big_endian=True, out=ipls.DeviceBuffer.from_tensor(avg))
+    expect(agg.last_launch(), ipls, ipls.KERNEL_ROUND, ipls.SHAPE_BIG, 16, 42, True, False)
+    agg.sync()
+    assert [agg.checksum(q, ipls.TGT_WEIGHTS) for q in range(P)] == m["sum_checksum"]
+    base = int(avg.data_ptr())
+    got = [ipls.checksum_dev(ipls.DeviceBuffer(base + 8 * q * (L - 1), L - 1)) for q in range(P)]
+    assert got == m["avg_checksum"]
+    # partition 1 in full (its averages start 8 mod 16: the shuffled-pair store path)
+    w = agg.read(1, ipls.TGT_WEIGHTS)
+    ref = ref_sum(O, L, 1, K)
+    assert_bits_equal(w, ref, "W[1]")
+    assert_bits_equal(avg[(L - 1):2 * (L - 1)].cpu().numpy(), O.c_divide(ref), "avg[1]")
+    agg.close()
+    del avg
+    pool.free()
+
+
+@pytest.mark.parametrize("P,L,K", [(4, 4_200_001, 8), (1, 4_194_304 + 4099, 16)])
+def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
+    """The fused round's big shape with a partial tile, and its mid shape,
+    on BE buckets, on top of a REP accumulator that is not zero."""
+    pool = Pool(ipls, P, L, K, True, O.SEED, out=False)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    rep = [O.c_synth_bucket(L, 100 + q, 0) for q in range(P)]
+    for q in range(P):
+        agg.Update(rep[q], q, from_clients=False)          # Replicas_Gradients = +0.0 + R
+    out = agg.aggregate_round(0, pool.rows, big_endian=True)
+    li = agg.last_launch()
+    assert (li["kernel"], li["vectors"], li["seqf"], li["be_in"]) == (ipls.KERNEL_ROUND, 16, 42, 1), li
+    assert li["shape"] == (ipls.SHAPE_BIG if P > 1 else ipls.SHAPE_MID) and li["map"] == 3, li
+    for q in range(P):
+        s = ref_sum(O, L, q, K)
+        w = s + (0.0 + rep[q])                             # AggregatePartition, IPLS.java:1256
+        assert_bits_equal(agg.read(q, ipls.TGT_WEIGHTS), w, f"W[{q}]")
+        assert_bits_equal(out[q * (L - 1):(q + 1) * (L - 1)], O.c_divide(w), f"avg[{q}]")
+    agg.close()
+    pool.free()
