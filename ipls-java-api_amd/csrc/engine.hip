@@ -114,7 +114,11 @@ struct ipls_dev {
     std::vector<const void*> bufs;
     bool be = false;
   };
-  std::map<std::pair<int, int>, Pending> pending;   // (target, p) -> queued buckets
+  // queue of (target, p) at pend[target * P + p]; pend_keys lists the
+  // non-empty ones (a flat table: the per-arrival call is a few loads and a
+  // push, no map walk)
+  std::vector<Pending> pend;
+  std::vector<int> pend_keys;
   int pending_n = 0;
   int coalesce = 32;                                // queue length that triggers a flush (ipls_agg_set_coalesce)
   // Tickets complete in issue order: a launch happens only after every earlier
@@ -925,27 +929,30 @@ int end_batch(ipls_dev* h) {
 // target with the same queue length and byte order go as one launch (the
 // batch kernel's table is [partition][peer]).
 int flush_pending(ipls_dev* h) {
-  if (h->pending.empty()) return IPLS_OK;
+  if (h->pend_keys.empty()) return IPLS_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   int rc = IPLS_OK;
+  std::vector<int>& keys = h->pend_keys;
+  std::sort(keys.begin(), keys.end());   // (target, p) ascending
   std::vector<const void*> tab;
-  for (auto it = h->pending.begin(); it != h->pending.end() && !rc;) {
-    const int target = it->first.first, p0 = it->first.second;
-    const size_t k = it->second.bufs.size();
-    const bool be = it->second.be;
-    auto jt = std::next(it);
+  for (size_t i = 0; i < keys.size() && !rc;) {
+    const int key = keys[i], target = key / h->P, p0 = key % h->P;
+    const ipls_dev::Pending& q0 = h->pend[key];
+    const size_t k = q0.bufs.size();
+    size_t j = i + 1;
     int n = 1;
-    while (jt != h->pending.end() && jt->first.first == target && jt->first.second == p0 + n &&
-           jt->second.bufs.size() == k && jt->second.be == be) {
+    while (j < keys.size() && keys[j] == key + n && keys[j] / h->P == target && h->pend[keys[j]].bufs.size() == k &&
+           h->pend[keys[j]].be == q0.be) {
       ++n;
-      ++jt;
+      ++j;
     }
     tab.clear();
-    for (auto q = it; q != jt; ++q) tab.insert(tab.end(), q->second.bufs.begin(), q->second.bufs.end());
-    rc = reduce_dev(h, p0, n, tab.data(), (int)k, be, IPLS_START_ACCUM, target);
-    it = jt;
+    for (size_t t = i; t < j; ++t) tab.insert(tab.end(), h->pend[keys[t]].bufs.begin(), h->pend[keys[t]].bufs.end());
+    rc = reduce_dev(h, p0, n, tab.data(), (int)k, q0.be, IPLS_START_ACCUM, target);
+    i = j;
   }
-  h->pending.clear();
+  for (int key : keys) h->pend[key].bufs.clear();   // keeps the capacity
+  keys.clear();
   h->pending_n = 0;
   if (rc) return rc;
   return end_batch(h);
@@ -1052,17 +1059,20 @@ int dev_accumulate_async(ipls_dev* h, int p, int target, const void* src, int64_
                   (long long)h->len[p]);
     if ((uintptr_t)src & 7) return fail(h, IPLS_E_INVAL, "device bucket not 8-byte aligned");
     const bool be = src_kind == IPLS_DEV_BE;
-    auto& q = h->pending[{target, p}];
+    // Weights and Weight_Address are one array (IPLS.java:1141): one queue
+    const int qt = target == IPLS_TGT_WADDR ? IPLS_TGT_WEIGHTS : target;
+    if (h->pend.empty()) h->pend.resize((size_t)5 * h->P);   // 5 targets (include/ipls_agg.h)
+    ipls_dev::Pending& q = h->pend[(size_t)qt * h->P + p];
     if (!q.bufs.empty() && q.be != be)
       if (int rc = flush_pending(h)) return rc;
-    auto& q2 = h->pending[{target, p}];
-    q2.be = be;
-    q2.bufs.push_back(src);
+    if (q.bufs.empty()) h->pend_keys.push_back(qt * h->P + p);
+    q.be = be;
+    q.bufs.push_back(src);
     ++h->pending_n;
     *ticket = h->ticket_next++;
     // flush when the queues average `coalesce` buckets (arrivals spread over
     // partitions flush as one rectangular launch), or one queue holds twice that
-    if ((int)q2.bufs.size() >= 2 * h->coalesce || h->pending_n >= h->coalesce * (int)h->pending.size())
+    if ((int)q.bufs.size() >= 2 * h->coalesce || h->pending_n >= h->coalesce * (int)h->pend_keys.size())
       return flush_pending(h);
     return IPLS_OK;
   }

@@ -920,7 +920,7 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
       if (nb > 2) v |= frame_byte(f, src, j + 2);
       unsigned q = b64url_quad(v);
       if (nb < 3) q = (q & 0x00FFFFFFu) | ((unsigned)'=' << 24);
-      if (nb < 2) q = (q & 0x0000FFFFu) | ((unsigned)'=' << 16);
+      if (nb < 2) q = (q & 0xFF00FFFFu) | ((unsigned)'=' << 16);
       unsigned char* o = out + 32 * g + 4 * u;
       o[0] = (unsigned char)q;
       o[1] = (unsigned char)(q >> 8);

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -365,6 +366,7 @@ class UpdaterThread {
     const void* device = nullptr;   // or a device-resident bucket, kept alive by the caller until drain()
     int64_t device_n = 0;
     bool device_big_endian = false;
+    std::string origin;             // value0: the sending peer (a client's request clears its Client_Wait_Ack)
   };
 
   // idle_flush: when no request arrives for this long, the queued device
@@ -403,6 +405,26 @@ class UpdaterThread {
     return failures_;
   }
 
+  // The round's PeerData.Client_Wait_Ack: the trainers this aggregator
+  // waits for (IPLS.java:1402-1404 spins until the list is empty).  The
+  // request that clears the last one is the flush hint: the queued device
+  // folds start at once instead of after the idle timeout or at the daemon's
+  // AggregatePartition.
+  void Client_Wait_Ack(std::set<std::string> peers) {
+    std::lock_guard<std::mutex> lk(mu_);
+    wait_ack_ = std::move(peers);
+  }
+  // Wait_Client_Gradients (IPLS.java:1402-1404): block until every expected
+  // trainer's request has been taken by the Updater.
+  void Wait_Client_Gradients() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_.wait(lk, [this] { return wait_ack_.empty(); });
+  }
+  uint64_t hint_flushes() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return hint_flushes_;
+  }
+
  private:
   void loop() {
     Updater u(ipls_);
@@ -425,6 +447,7 @@ class UpdaterThread {
         r = std::move(q_.front());
         q_.pop_front();
       }
+      bool hint = false;
       try {
         if (r.device) {
           uint64_t t = 0;
@@ -444,6 +467,19 @@ class UpdaterThread {
       }
       {
         std::lock_guard<std::mutex> lk(mu_);
+        if (r.from_clients && !wait_ack_.empty() && wait_ack_.erase(r.origin) && wait_ack_.empty() && queued_) {
+          hint = true;   // Client_Wait_Ack drained: every expected bucket of the round is queued
+          queued_ = false;
+        }
+      }
+      if (hint) {
+        const int rc = ipls_agg_flush(ipls_.handle());
+        std::lock_guard<std::mutex> lk(mu_);
+        ++hint_flushes_;
+        if (rc < 0) failures_.push_back(ipls_agg_last_error(ipls_.handle()));
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu_);
         ++done_n_;
       }
       idle_.notify_all();
@@ -456,7 +492,8 @@ class UpdaterThread {
   std::condition_variable cv_, idle_;
   std::deque<Request> q_;
   bool stop_ = false, queued_ = false;
-  uint64_t put_n_ = 0, done_n_ = 0;
+  uint64_t put_n_ = 0, done_n_ = 0, hint_flushes_ = 0;
+  std::set<std::string> wait_ack_;
   std::vector<std::string> failures_;
   std::thread th_;   // last: starts after every member above exists
 };

@@ -114,13 +114,18 @@ def combine_replicas(agg, plan: ReplicaPlan, rank: int, *, device=None, mode: st
     import torch.distributed as dist
 
     exchanges = plan.exchanges()
+    if mode == "rccl_reduce" and group is not None:
+        # dist.reduce is collective over its group: a caller group that does not
+        # hold exactly each partition's (owner, replicas) set would hang the
+        # ranks outside it
+        raise ValueError("rccl_reduce builds one group per (owner, replicas) set; pass group=None")
     if mode == "rccl_reduce":
         # new_group is collective over the WORLD: every rank creates every group.
         groups = {}
         for p, owner, others in exchanges:
             key = tuple(sorted([owner, *others]))
             if key not in groups:
-                groups[key] = dist.new_group(list(key)) if group is None else group
+                groups[key] = dist.new_group(list(key))
         filled = []
         for p, owner, others in exchanges:
             if rank not in (owner, *others):
@@ -162,6 +167,11 @@ def combine_replicas(agg, plan: ReplicaPlan, rank: int, *, device=None, mode: st
         _landed(landing[0][1])
     for p, buf in landing:                                # fold in (partition, replica) order
         agg.import_partial(p, buf)                        # REP[p] += R_r (Updater.java:40-44)
+    if landing:
+        # the folds above are queued on the aggregator's stream and read the
+        # transport buffers, which the next round's irecv (on RCCL's stream)
+        # overwrites: wait for them before the buffers are handed out again
+        agg.sync()
     return filled
 
 
@@ -194,6 +204,11 @@ class RankShard:
 
     def import_partial(self, p, tensor, replace_agg=False):
         self.own.import_partial(p - self.first, tensor, replace_agg=replace_agg)
+
+    def sync(self):
+        self.own.sync()
+        if self.rep is not None:
+            self.rep.sync()
 
 
 def _landed(buf):

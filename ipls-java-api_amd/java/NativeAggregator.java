@@ -19,12 +19,28 @@ public final class NativeAggregator implements AutoCloseable {
     public static final int ALL_PARTITIONS = -1;
 
     private long handle;
+    private final int partitions;
 
     /** IPLS.init -> InitializeWeights(): -pa, -n, -aggr from Middleware.parse_arguments. */
     public NativeAggregator(long modelSize, int partitions, int minPeers, boolean partialAggregation,
                             boolean secure, int device) {
         handle = open(modelSize, partitions, minPeers, partialAggregation ? 1 : 0, secure ? 1 : 0, device);
+        this.partitions = partitions;
     }
+
+    /** The same over several GPUs of one node: the -pa partitions are sharded over
+     *  `devices` in contiguous blocks (partition p on devices[p / ceil(P/G)]). */
+    public NativeAggregator(long modelSize, int partitions, int minPeers, boolean partialAggregation,
+                            boolean secure, int[] devices) {
+        handle = openDevices(modelSize, partitions, minPeers, partialAggregation ? 1 : 0, secure ? 1 : 0, devices);
+        this.partitions = partitions;
+    }
+
+    /** HIP device that owns partition p (allocate p's device buckets there). */
+    public int partitionDevice(int p) { return partitionDevice(handle, p); }
+
+    /** The contiguous-block plan: owner shard of every partition. */
+    public static int[] shards(int partitions, int nShards) { return shardPlan(partitions, nShards); }
 
     public int partitionLength(int p) { return (int) partitionLen(handle, p); }
 
@@ -52,19 +68,21 @@ public final class NativeAggregator implements AutoCloseable {
      *  gradient file go through the handle's Gradient_Buff, as GetParameters(hash,
      *  Gradient_Buff) + _Update do (short files fold the previous file's tail). */
     public void updateFromFile(ByteBuffer catBytes, int p, boolean fromClients) {
-        updateIndirect(handle, p, fromClients ? TGT_AGG : TGT_REP, catBytes, catBytes.remaining());
+        updateIndirect(handle, p, fromClients ? TGT_AGG : TGT_REP, catBytes, catBytes.position(), catBytes.remaining());
     }
 
     /** A bucket already decoded to exactly L_p big-endian doubles (no Gradient_Buff). */
     public void updateFromBytes(ByteBuffer beDoubles, int p, boolean fromClients) {
-        accumulateDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
+        accumulateDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.position(),
+                         beDoubles.remaining() / 8, 1);
     }
 
     /** The same fold without waiting (one call per queue.take(), Updater.java:169-211):
      *  beDoubles is a direct buffer from hostAllocDirect (pinned), folded over PCIe
      *  while the next `ipfs cat` fills another buffer.  Keep it until await(ticket). */
     public long updateFromBytesAsync(ByteBuffer beDoubles, int p, boolean fromClients) {
-        return accumulateAsyncDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.remaining() / 8, 1);
+        return accumulateAsyncDirect(handle, p, fromClients ? TGT_AGG : TGT_REP, beDoubles, beDoubles.position(),
+                                     beDoubles.remaining() / 8, 1);
     }
 
     /** Block until fold `ticket` (and every fold queued before it) has finished. */
@@ -85,11 +103,11 @@ public final class NativeAggregator implements AutoCloseable {
     /** Download_Scheduler.download_gradients (:254-266): another aggregator's
      *  bucket for partition p, kept per (p, aggregator) until collectReplicas(). */
     public void otherReplica(int p, int aggregator, ByteBuffer catBytes) {
-        otherReplicaDirect(handle, p, aggregator, catBytes, catBytes.remaining() / 8);
+        otherReplicaDirect(handle, p, aggregator, catBytes, catBytes.position(), catBytes.remaining() / 8);
     }
 
     /** IPLS.Collect_Replicas (IPLS.java:1217-1241); returns Participants per partition. */
-    public int[] collectReplicas(int partitions) {
+    public int[] collectReplicas() {
         int[] participants = new int[partitions];
         collectReplicas(handle, participants);
         return participants;
@@ -138,14 +156,14 @@ public final class NativeAggregator implements AutoCloseable {
     /** AggregatePartition into a direct buffer from hostAlloc (pinned): the sum's
      *  D2H runs at the PCIe rate; a heap byte[] costs 10-15 % of a round. */
     public void aggregatePartition(int p, ByteBuffer directOut) {
-        if (!directOut.isDirect() || directOut.capacity() < 8L * partitionLength(p))
+        if (!directOut.isDirect() || directOut.remaining() < 8L * partitionLength(p))
             throw new IllegalArgumentException("need a direct buffer of 8*L_p bytes");
-        finalizePartitionDirect(handle, p, directOut);
+        finalizePartitionDirect(handle, p, directOut, directOut.position());
     }
 
     /** Download_Scheduler.cache_partition: Weight_Address[p] = GetParameters(hash). */
     public void cachePartition(int p, ByteBuffer beDoubles) {
-        setWeightsDirect(handle, p, beDoubles, beDoubles.remaining() / 8);
+        setWeightsDirect(handle, p, beDoubles, beDoubles.position(), beDoubles.remaining() / 8);
     }
 
     /** ThreadReceiver pid 4 (IPLS.java:491-498): the ACK frame's payload becomes Weight_Address[p]. */
@@ -159,15 +177,43 @@ public final class NativeAggregator implements AutoCloseable {
     }
 
     /** AggregatePartition for partitions [pFirst, pFirst+nParts) and their
-     *  GetPartitions averages in one fused launch (ipls_agg_aggregate_round). */
-    public double[] aggregateRound(int pFirst, int nParts, int nValues) {
-        double[] out = new double[nValues];
+     *  GetPartitions averages in one fused launch (ipls_agg_aggregate_round);
+     *  the result is sized here from the partition geometry. */
+    public double[] aggregateRound(int pFirst, int nParts) {
+        long first = offsetOf(pFirst), last = offsetOf(pFirst + nParts - 1) + partitionLength(pFirst + nParts - 1) - 1;
+        double[] out = new double[(int) (last - first)];
         aggregateRound(handle, pFirst, nParts, out);
         return out;
     }
 
+    private long offsetOf(int p) { return partitionOffset(handle, p); }   // p * chunk (IPLS.java:1019-1028)
+
     /** Middleware task 3: the writeDouble stream in one bulk write. */
-    public void getPartitionsWire(ByteBuffer direct) { getPartitionsWire(handle, direct); }
+    public void getPartitionsWire(ByteBuffer direct) {
+        getPartitionsWire(handle, direct, direct.position(), direct.remaining());
+    }
+
+    /** The aggregator's partial sum published every round (IPLS.java:1429-1430):
+     *  ipfsClass.send(topic, publishPartial(p, iteration, workers + 1, id)) --
+     *  Marshall_Packet + Base64.getUrlEncoder, encoded on the GPU. */
+    public String publishPartial(int p, int iteration, int workersPlusOne, String originPeer) {
+        byte[] o = java.util.Arrays.copyOf(originPeer.getBytes(), originPeer.length());   // finalbarr's origin bytes
+        return new String(publishPartial(handle, p, TGT_AGG, iteration, workersPlusOne, (short) 3, o),
+                          java.nio.charset.StandardCharsets.US_ASCII);
+    }
+
+    /** Device-resident batches: n_parts x k device addresses, partition-major. */
+    public void reduceBatch(int pFirst, int nParts, long[] devPtrs, int k, boolean bigEndian, int start, int target) {
+        reduceBatchDevice(handle, pFirst, nParts, devPtrs, k, bigEndian ? 4 : 3, start, target);
+    }
+
+    /** A replica slot (another GPU of this handle) folds its buckets of partitions it
+     *  does not own; combinePartials adds every slot's partial to REP in slot order. */
+    public void reducePartial(int slot, int pFirst, int nParts, long[] devPtrs, int k, boolean bigEndian, int start) {
+        reducePartialDevice(handle, slot, pFirst, nParts, devPtrs, k, bigEndian ? 4 : 3, start);
+    }
+
+    public int combinePartials(int pFirst, int nParts) { return combinePartials(handle, pFirst, nParts); }
 
     public static ByteBuffer hostAlloc(int bytes) { return hostAllocDirect(bytes); }
 
@@ -175,22 +221,34 @@ public final class NativeAggregator implements AutoCloseable {
 
     // ---- natives (ipls_jni.c) ----
     private static native long open(long modelSize, int partitions, int maxPeers, int aggr, int secure, int device);
+    private static native long openDevices(long modelSize, int partitions, int maxPeers, int aggr, int secure,
+                                           int[] devices);
+    private static native int partitionDevice(long h, int p);
+    private static native int[] shardPlan(int partitions, int shards);
+    private static native void reduceBatchDevice(long h, int pFirst, int nParts, long[] ptrs, int k, int kind,
+                                                 int start, int target);
+    private static native void reducePartialDevice(long h, int slot, int pFirst, int nParts, long[] ptrs, int k,
+                                                   int kind, int start);
+    private static native int combinePartials(long h, int pFirst, int nParts);
+    private static native byte[] publishPartial(long h, int p, int target, int a, int b, short pid, byte[] origin);
     private static native void close(long h);
     private static native long partitionLen(long h, int p);
+    private static native long partitionOffset(long h, int p);
     private static native void loadModel(long h, double[] model);
     private static native void split(long h, double[] flat, int p, double[] out);
     private static native void updateGradient(long h, double[] flat, int[] owned);
     private static native void accumulate(long h, int p, int target, double[] g);
-    private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
-    private static native long accumulateAsyncDirect(long h, int p, int target, ByteBuffer buf, long n, int kind);
+    private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, int pos, long n, int kind);
+    private static native long accumulateAsyncDirect(long h, int p, int target, ByteBuffer buf, int pos, long n,
+                                                     int kind);
     private static native void waitTicket(long h, long ticket);
     private static native void flushQueued(long h);
     private static native int ingestTexts(long h, int target, byte[][] msgs, int layers, int[] parts, int[] status);
     private static native void accumulateFrame(long h, int p, int target, byte[] frame);
-    private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, long nBytes);
+    private static native void updateIndirect(long h, int p, int target, ByteBuffer buf, int pos, long nBytes);
     private static native void finalizePartition(long h, int p, byte[] sumOut);
-    private static native void finalizePartitionDirect(long h, int p, ByteBuffer sumOut);
-    private static native void setWeightsDirect(long h, int p, ByteBuffer buf, long n);
+    private static native void finalizePartitionDirect(long h, int p, ByteBuffer sumOut, int pos);
+    private static native void setWeightsDirect(long h, int p, ByteBuffer buf, int pos, long n);
     private static native void setWeightsFrame(long h, int p, byte[] frame);
     private static native void getPartitions(long h, double[] out);
     private static native void aggregateRound(long h, int pFirst, int nParts, double[] avgOut);
@@ -199,8 +257,8 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void commitPartial(long h, int p, int workers, byte[] out);
     private static native void accumulatePair(long h, int p, int target, byte[] file);
     private static native byte[] mergeFiles(long h, byte[][] files, boolean partialUpdates);
-    private static native void otherReplicaDirect(long h, int p, int aggregator, ByteBuffer buf, long n);
-    private static native void collectReplicas(long h, int[] participants);
-    private static native void getPartitionsWire(long h, ByteBuffer direct);
+    private static native void otherReplicaDirect(long h, int p, int aggregator, ByteBuffer buf, int pos, long n);
+    private static native int collectReplicas(long h, int[] participants);
+    private static native void getPartitionsWire(long h, ByteBuffer direct, int pos, long nBytes);
     private static native ByteBuffer hostAllocDirect(int bytes);
 }

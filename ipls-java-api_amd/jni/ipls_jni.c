@@ -1,16 +1,32 @@
 /*
  * ipls_jni.c -- JNI half of NativeAggregator (ipls-java-api_amd/java/).
  * A 1:1 map onto include/ipls_agg.h: no arithmetic here.  Negative return
- * codes become the Java exception the reference would have thrown.
+ * codes become the Java exception the reference would have thrown
+ * (throw_for); every array or buffer the library writes is checked against
+ * what it will write BEFORE the call, so a wrong size from the Java side is
+ * an IllegalArgumentException and never a write past a Java array.
  *
- * Built only where a JDK exists (make -C ipls-java-api_amd jni); this image
- * has none, so it is compiled on the Java side's build host.
+ * Direct ByteBuffers: GetDirectBufferAddress ignores position() and returns
+ * NULL for a heap buffer, so the Java wrappers pass position() and the byte
+ * count, and the shim adds the position and checks both against capacity.
+ *
+ * Built against the JDK's <jni.h> on the Java side's build host (make -C
+ * ipls-java-api_amd jni).  This image has no JDK: tests/test_jni.py compiles
+ * it with -Wall -Wextra -Werror against tests/jni/jni.h and drives every
+ * native through tests/jni/fake_jvm.c.
  */
 #include <jni.h>
+#include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../include/ipls_agg.h"
+
+static void throw_msg(JNIEnv *env, const char *cls, const char *msg) {
+    jclass c = (*env)->FindClass(env, cls);
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
 
 static void throw_for(JNIEnv *env, int rc, ipls_agg *h) {
     const char *cls = "java/lang/RuntimeException";
@@ -22,12 +38,53 @@ static void throw_for(JNIEnv *env, int rc, ipls_agg *h) {
         case IPLS_E_NOMEM: cls = "java/lang/OutOfMemoryError"; break;
         default: break;
     }
-    jclass c = (*env)->FindClass(env, cls);
-    if (c) (*env)->ThrowNew(env, c, ipls_agg_last_error(h));
+    throw_msg(env, cls, ipls_agg_last_error(h));
+}
+
+static void throw_iae(JNIEnv *env, const char *what) {
+    throw_msg(env, "java/lang/IllegalArgumentException", what);
 }
 
 #define H(x) ((ipls_agg *)(intptr_t)(x))
 #define CHECK(rc, h) do { int rc_ = (rc); if (rc_ < 0) { throw_for(env, rc_, (h)); } } while (0)
+
+/* The bytes [pos, pos + nbytes) of a direct buffer, or NULL with an
+ * IllegalArgumentException pending. */
+static void *direct_span(JNIEnv *env, jobject buf, jint pos, jlong nbytes) {
+    if (!buf) { throw_iae(env, "null buffer"); return NULL; }
+    char *a = (char *)(*env)->GetDirectBufferAddress(env, buf);
+    const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (!a || cap < 0) { throw_iae(env, "not a direct ByteBuffer (allocate it with hostAlloc)"); return NULL; }
+    if (pos < 0 || nbytes < 0 || (jlong)pos + nbytes > cap) { throw_iae(env, "position/length outside the buffer"); return NULL; }
+    return a + pos;
+}
+
+/* L_p (or -1 with the exception pending). */
+static int64_t part_len(JNIEnv *env, jlong h, jint p) {
+    int64_t L = 0;
+    int rc = ipls_agg_partition_len(H(h), p, &L);
+    if (rc < 0) { throw_for(env, rc, H(h)); return -1; }
+    return L;
+}
+
+/* Java array length >= need, else an IllegalArgumentException. */
+static int need_len(JNIEnv *env, jarray a, int64_t need, const char *what) {
+    if (!a) { throw_iae(env, what); return 0; }
+    if ((int64_t)(*env)->GetArrayLength(env, a) < need) {
+        char m[160];
+        snprintf(m, sizeof m, "%s: array shorter than the %lld elements the library writes", what, (long long)need);
+        throw_iae(env, m);
+        return 0;
+    }
+    return 1;
+}
+
+static jlong open_cfg(JNIEnv *env, ipls_agg_cfg *cfg) {
+    ipls_agg *h = NULL;
+    int rc = ipls_agg_open(cfg, &h);
+    if (rc < 0) { throw_for(env, rc, NULL); return 0; }
+    return (jlong)(intptr_t)h;
+}
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_open(JNIEnv *env, jclass c, jlong m, jint pa, jint n,
                                                      jint aggr, jint secure, jint dev) {
@@ -36,10 +93,25 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_open(JNIEnv *env, jclass c, jlong 
     memset(&cfg, 0, sizeof cfg);
     cfg.model_size = m; cfg.n_partitions = pa; cfg.max_peers = n;
     cfg.partial_aggregation = aggr; cfg.secure = secure; cfg.device = dev;
-    ipls_agg *h = NULL;
-    int rc = ipls_agg_open(&cfg, &h);
-    if (rc < 0) { throw_for(env, rc, NULL); return 0; }
-    return (jlong)(intptr_t)h;
+    return open_cfg(env, &cfg);
+}
+
+/* The same over several GPUs: -pa partitions in contiguous blocks over devices[]. */
+JNIEXPORT jlong JNICALL Java_NativeAggregator_openDevices(JNIEnv *env, jclass c, jlong m, jint pa, jint n,
+                                                            jint aggr, jint secure, jintArray devices) {
+    (void)c;
+    if (!devices || (*env)->GetArrayLength(env, devices) < 1) { throw_iae(env, "need at least one device"); return 0; }
+    ipls_agg_cfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.model_size = m; cfg.n_partitions = pa; cfg.max_peers = n;
+    cfg.partial_aggregation = aggr; cfg.secure = secure;
+    cfg.n_devices = (*env)->GetArrayLength(env, devices);
+    jint *d = (*env)->GetIntArrayElements(env, devices, NULL);
+    cfg.devices = (const int32_t *)d;
+    cfg.device = d ? d[0] : 0;
+    jlong h = d ? open_cfg(env, &cfg) : 0;   /* the list is copied by ipls_agg_open */
+    if (d) (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
+    return h;
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_close(JNIEnv *env, jclass c, jlong h) {
@@ -49,13 +121,43 @@ JNIEXPORT void JNICALL Java_NativeAggregator_close(JNIEnv *env, jclass c, jlong 
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_partitionLen(JNIEnv *env, jclass c, jlong h, jint p) {
     (void)c;
-    int64_t L = 0;
-    CHECK(ipls_agg_partition_len(H(h), p, &L), H(h));
-    return (jlong)L;
+    return (jlong)part_len(env, h, p);
+}
+
+JNIEXPORT jlong JNICALL Java_NativeAggregator_partitionOffset(JNIEnv *env, jclass c, jlong h, jint p) {
+    (void)c;
+    int64_t off = 0;
+    CHECK(ipls_agg_partition_offset(H(h), p, &off), H(h));
+    return (jlong)off;
+}
+
+JNIEXPORT jint JNICALL Java_NativeAggregator_partitionDevice(JNIEnv *env, jclass c, jlong h, jint p) {
+    (void)c;
+    int32_t d = -1;
+    CHECK(ipls_agg_partition_device(H(h), p, &d, NULL), H(h));
+    return d;
+}
+
+JNIEXPORT jintArray JNICALL Java_NativeAggregator_shardPlan(JNIEnv *env, jclass c, jint partitions, jint shards) {
+    (void)c;
+    if (partitions <= 0) { throw_iae(env, "partitions must be > 0"); return NULL; }
+    int32_t *o = (int32_t *)malloc(sizeof(int32_t) * (size_t)partitions);
+    if (!o) { throw_msg(env, "java/lang/OutOfMemoryError", "shard plan"); return NULL; }
+    int rc = ipls_shard_plan(partitions, shards, o);
+    jintArray res = NULL;
+    if (rc < 0) {
+        throw_for(env, rc, NULL);
+    } else {
+        res = (*env)->NewIntArray(env, partitions);
+        if (res) (*env)->SetIntArrayRegion(env, res, 0, partitions, (const jint *)o);
+    }
+    free(o);
+    return res;
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_loadModel(JNIEnv *env, jclass c, jlong h, jdoubleArray a) {
     (void)c;
+    if (!a) { throw_iae(env, "null model"); return; }
     jsize n = (*env)->GetArrayLength(env, a);
     void *p = (*env)->GetPrimitiveArrayCritical(env, a, NULL);
     int rc = ipls_agg_load_model(H(h), p, n, IPLS_HOST_F64);
@@ -66,6 +168,8 @@ JNIEXPORT void JNICALL Java_NativeAggregator_loadModel(JNIEnv *env, jclass c, jl
 JNIEXPORT void JNICALL Java_NativeAggregator_split(JNIEnv *env, jclass c, jlong h, jdoubleArray flat, jint part,
                                                      jdoubleArray out) {
     (void)c;
+    const int64_t L = part_len(env, h, part);
+    if (L < 0 || !need_len(env, out, L, "split output") || !need_len(env, flat, 0, "null gradients")) return;
     jsize n = (*env)->GetArrayLength(env, flat);
     void *src = (*env)->GetPrimitiveArrayCritical(env, flat, NULL);
     void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
@@ -78,18 +182,21 @@ JNIEXPORT void JNICALL Java_NativeAggregator_split(JNIEnv *env, jclass c, jlong 
 JNIEXPORT void JNICALL Java_NativeAggregator_updateGradient(JNIEnv *env, jclass c, jlong h, jdoubleArray flat,
                                                               jintArray owned) {
     (void)c;
+    if (!flat) return;   /* Gradients == null: no-op (IPLS.java:1738) */
+    if (!owned) { throw_iae(env, "null auth list"); return; }
     jsize n = (*env)->GetArrayLength(env, flat), no = (*env)->GetArrayLength(env, owned);
+    jint *own = (*env)->GetIntArrayElements(env, owned, NULL);   /* before the critical region */
     void *src = (*env)->GetPrimitiveArrayCritical(env, flat, NULL);
-    void *own = (*env)->GetPrimitiveArrayCritical(env, owned, NULL);
     int rc = ipls_agg_update_gradient(H(h), src, n, IPLS_HOST_F64, (const int32_t *)own, no);
-    (*env)->ReleasePrimitiveArrayCritical(env, owned, own, JNI_ABORT);
     (*env)->ReleasePrimitiveArrayCritical(env, flat, src, JNI_ABORT);
+    (*env)->ReleaseIntArrayElements(env, owned, own, JNI_ABORT);
     CHECK(rc, H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                           jdoubleArray g) {
     (void)c;
+    if (!g) return;   /* Gradient == null: the Updater loops do nothing (Updater.java:115) */
     jsize n = (*env)->GetArrayLength(env, g);
     void *src = (*env)->GetPrimitiveArrayCritical(env, g, NULL);
     int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_F64);
@@ -98,16 +205,19 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
-                                                                jobject buf, jlong n, jint kind) {
+                                                                jobject buf, jint pos, jlong n, jint kind) {
     (void)c;
-    void *src = (*env)->GetDirectBufferAddress(env, buf);
+    void *src = direct_span(env, buf, pos, 8 * n);
+    if (!src) return;
     CHECK(ipls_agg_accumulate(H(h), p, tgt, src, n, kind), H(h));
 }
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_accumulateAsyncDirect(JNIEnv *env, jclass c, jlong h, jint p,
-                                                                      jint tgt, jobject buf, jlong n, jint kind) {
+                                                                      jint tgt, jobject buf, jint pos, jlong n,
+                                                                      jint kind) {
     (void)c;
-    void *src = (*env)->GetDirectBufferAddress(env, buf);
+    void *src = direct_span(env, buf, pos, 8 * n);
+    if (!src) return 0;
     uint64_t t = 0;
     CHECK(ipls_agg_accumulate_async(H(h), p, tgt, src, n, kind, &t), H(h));
     return (jlong)t;
@@ -124,15 +234,17 @@ JNIEXPORT void JNICALL Java_NativeAggregator_flushQueued(JNIEnv *env, jclass c, 
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
-                                                              jobject buf, jlong nBytes) {
+                                                              jobject buf, jint pos, jlong nBytes) {
     (void)c;
-    void *src = (*env)->GetDirectBufferAddress(env, buf);
+    void *src = direct_span(env, buf, pos, nBytes);
+    if (!src) return;
     CHECK(ipls_agg_update_indirect(H(h), p, tgt, src, nBytes), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateFrame(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                                jbyteArray frame) {
     (void)c;
+    if (!frame) { throw_iae(env, "null frame"); return; }
     jsize n = (*env)->GetArrayLength(env, frame);
     void *src = (*env)->GetPrimitiveArrayCritical(env, frame, NULL);
     int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_FRAME);
@@ -149,6 +261,8 @@ JNIEXPORT jint JNICALL Java_NativeAggregator_ingestTexts(JNIEnv *env, jclass c, 
                                                          jintArray status) {
     (void)c;
     const jsize n = msgs ? (*env)->GetArrayLength(env, msgs) : 0;
+    if (parts && (*env)->GetArrayLength(env, parts) < n) { throw_iae(env, "partitions shorter than the texts"); return 0; }
+    if (status && (*env)->GetArrayLength(env, status) < n) { throw_iae(env, "status shorter than the texts"); return 0; }
     jbyteArray *arr = calloc((size_t)n + 1, sizeof *arr);
     const uint8_t **ptr = calloc((size_t)n + 1, sizeof *ptr);
     int64_t *len = calloc((size_t)n + 1, sizeof *len);
@@ -182,27 +296,38 @@ out:
 JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jclass c, jlong h, jint p,
                                                                  jbyteArray sum) {
     (void)c;
-    void *dst = (*env)->GetPrimitiveArrayCritical(env, sum, NULL);
+    if (sum) {
+        const int64_t L = part_len(env, h, p);
+        if (L < 0 || !need_len(env, sum, 8 * L, "commit_update bytes")) return;
+    }
+    void *dst = sum ? (*env)->GetPrimitiveArrayCritical(env, sum, NULL) : NULL;
     int rc = ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL);
-    (*env)->ReleasePrimitiveArrayCritical(env, sum, dst, 0);
+    if (sum) (*env)->ReleasePrimitiveArrayCritical(env, sum, dst, 0);
     CHECK(rc, H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartitionDirect(JNIEnv *env, jclass c, jlong h, jint p,
-                                                                       jobject sum) {
+                                                                       jobject sum, jint pos) {
     (void)c;
-    CHECK(ipls_agg_finalize(H(h), p, (*env)->GetDirectBufferAddress(env, sum), IPLS_HOST_BE, NULL), H(h));
+    const int64_t L = part_len(env, h, p);
+    if (L < 0) return;
+    void *dst = direct_span(env, sum, pos, 8 * L);
+    if (!dst) return;
+    CHECK(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclass c, jlong h, jint p, jobject buf,
-                                                                jlong n) {
+                                                                jint pos, jlong n) {
     (void)c;
-    CHECK(ipls_agg_set_weights(H(h), p, (*env)->GetDirectBufferAddress(env, buf), n, IPLS_HOST_BE), H(h));
+    void *src = direct_span(env, buf, pos, 8 * n);
+    if (!src) return;
+    CHECK(ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_BE), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass c, jlong h, jint p,
                                                                jbyteArray frame) {
     (void)c;
+    if (!frame) { throw_iae(env, "null frame"); return; }
     jsize n = (*env)->GetArrayLength(env, frame);
     void *src = (*env)->GetPrimitiveArrayCritical(env, frame, NULL);
     int rc = ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_FRAME);
@@ -212,7 +337,8 @@ JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass
 
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c, jlong h, jdoubleArray out) {
     (void)c;
-    jsize n = (*env)->GetArrayLength(env, out);
+    if (!out) { throw_iae(env, "null output"); return; }
+    jsize n = (*env)->GetArrayLength(env, out);   /* the library checks n against the model size */
     void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
     int rc = ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64);
     (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
@@ -222,14 +348,22 @@ JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c
 JNIEXPORT void JNICALL Java_NativeAggregator_aggregateRound(JNIEnv *env, jclass c, jlong h, jint p0, jint np,
                                                               jdoubleArray out) {
     (void)c;
-    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    int rc = ipls_agg_aggregate_round(H(h), p0, np, NULL, 0, IPLS_DEV_F64, dst, IPLS_HOST_F64);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    /* the averages of [p0, p0+np): flat offsets off[p0] .. off[p_last] + L_last - 1 */
+    int64_t o0 = 0, ol = 0, Ll = 0;
+    int rc = np > 0 ? ipls_agg_partition_offset(H(h), p0, &o0) : IPLS_E_RANGE;
+    if (rc >= 0) rc = ipls_agg_partition_offset(H(h), p0 + np - 1, &ol);
+    if (rc >= 0) rc = ipls_agg_partition_len(H(h), p0 + np - 1, &Ll);
+    if (rc < 0) { throw_for(env, rc, H(h)); return; }
+    if (out && !need_len(env, out, ol + Ll - 1 - o0, "averages")) return;
+    void *dst = out ? (*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+    rc = ipls_agg_aggregate_round(H(h), p0, np, NULL, 0, IPLS_DEV_F64, dst, IPLS_HOST_F64);
+    if (out) (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
     CHECK(rc, H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c, jlong h, jintArray parts) {
     (void)c;
+    if (!parts) { throw_iae(env, "null partition list"); return; }
     jsize n = (*env)->GetArrayLength(env, parts);
     jint *ps = (*env)->GetIntArrayElements(env, parts, NULL);
     int rc = ipls_agg_promote_future(H(h), (const int32_t *)ps, n);
@@ -238,17 +372,30 @@ JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_otherReplicaDirect(JNIEnv *env, jclass c, jlong h, jint p, jint a,
-                                                                  jobject buf, jlong n) {
+                                                                  jobject buf, jint pos, jlong n) {
     (void)c;
-    CHECK(ipls_agg_other_replica(H(h), p, a, (*env)->GetDirectBufferAddress(env, buf), n, IPLS_HOST_BE), H(h));
+    void *src = direct_span(env, buf, pos, 8 * n);
+    if (!src) return;
+    CHECK(ipls_agg_other_replica(H(h), p, a, src, n, IPLS_HOST_BE), H(h));
 }
 
-JNIEXPORT void JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass c, jlong h, jintArray out) {
+JNIEXPORT jint JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass c, jlong h, jintArray out) {
     (void)c;
-    jint *ps = (*env)->GetIntArrayElements(env, out, NULL);
+    /* the library writes one count per partition: out.length >= P, i.e.
+     * partition out.length must NOT exist */
+    if (out) {
+        int64_t L;
+        const jsize n = (*env)->GetArrayLength(env, out);
+        if (n == 0 || ipls_agg_partition_len(H(h), n, &L) == IPLS_OK) {
+            throw_iae(env, "participants array shorter than the number of partitions");
+            return 0;
+        }
+    }
+    jint *ps = out ? (*env)->GetIntArrayElements(env, out, NULL) : NULL;
     int rc = ipls_agg_collect_replicas(H(h), (int32_t *)ps);
-    (*env)->ReleaseIntArrayElements(env, out, ps, 0);
+    if (ps) (*env)->ReleaseIntArrayElements(env, out, ps, 0);
     CHECK(rc, H(h));
+    return rc;
 }
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_commitPartialLen(JNIEnv *env, jclass c, jlong h, jint p, jint w) {
@@ -261,7 +408,8 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_commitPartialLen(JNIEnv *env, jcla
 JNIEXPORT void JNICALL Java_NativeAggregator_commitPartial(JNIEnv *env, jclass c, jlong h, jint p, jint w,
                                                              jbyteArray out) {
     (void)c;
-    jsize n = (*env)->GetArrayLength(env, out);
+    if (!out) { throw_iae(env, "null output"); return; }
+    jsize n = (*env)->GetArrayLength(env, out);   /* passed as the capacity: the library checks it */
     void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
     int64_t rc = ipls_agg_commit_partial(H(h), p, w, (uint8_t *)dst, n);
     (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
@@ -271,6 +419,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_commitPartial(JNIEnv *env, jclass c
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulatePair(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                               jbyteArray file) {
     (void)c;
+    if (!file) { throw_iae(env, "null file"); return; }
     jsize n = (*env)->GetArrayLength(env, file);
     void *src = (*env)->GetPrimitiveArrayCritical(env, file, NULL);
     int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_PAIR);
@@ -281,16 +430,20 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulatePair(JNIEnv *env, jclass 
 JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclass c, jlong h, jobjectArray files,
                                                                 jboolean partial) {
     (void)c;
-    jsize k = (*env)->GetArrayLength(env, files);
-    if (k < 1) { throw_for(env, IPLS_E_INVAL, H(h)); return NULL; }
+    jsize k = files ? (*env)->GetArrayLength(env, files) : 0;
+    if (k < 1) { throw_iae(env, "need at least one file"); return NULL; }
     jbyteArray *arr = (jbyteArray *)calloc((size_t)k, sizeof(jbyteArray));
     const uint8_t **ptrs = (const uint8_t **)calloc((size_t)k, sizeof(uint8_t *));
     int64_t *lens = (int64_t *)calloc((size_t)k, sizeof(int64_t));
     jbyteArray res = NULL;
-    for (jsize i = 0; i < k; ++i) {   /* copies: several arrays cannot be held critical across a JNI call */
-        arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, files, i);
-        lens[i] = (*env)->GetArrayLength(env, arr[i]);
-        ptrs[i] = (const uint8_t *)(*env)->GetByteArrayElements(env, arr[i], NULL);
+    uint8_t *out = NULL;
+    jsize got = 0;
+    if (!arr || !ptrs || !lens) { throw_msg(env, "java/lang/OutOfMemoryError", "mergeFiles"); goto done; }
+    for (; got < k; ++got) {   /* copies: several arrays cannot be held critical across a JNI call */
+        arr[got] = (jbyteArray)(*env)->GetObjectArrayElement(env, files, got);
+        if (!arr[got]) { throw_iae(env, "null file"); goto done; }
+        lens[got] = (*env)->GetArrayLength(env, arr[got]);
+        ptrs[got] = (const uint8_t *)(*env)->GetByteArrayElements(env, arr[got], NULL);
     }
     int64_t cap = 8 * (lens[0] / 8);
     if (partial) {
@@ -298,30 +451,106 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclas
         int64_t n0 = ipls_pair_parse(ptrs[0], lens[0], &w, &off);
         cap = n0 < 0 ? 0 : 8 * n0;
     }
-    uint8_t *out = (uint8_t *)malloc((size_t)(cap > 0 ? cap : 1));
+    out = (uint8_t *)malloc((size_t)(cap > 0 ? cap : 1));
+    if (!out) { throw_msg(env, "java/lang/OutOfMemoryError", "mergeFiles"); goto done; }
     int64_t nb = ipls_agg_merge_files(H(h), ptrs, lens, k, partial ? IPLS_HOST_PAIR : IPLS_HOST_BE, out, cap);
-    for (jsize i = 0; i < k; ++i) (*env)->ReleaseByteArrayElements(env, arr[i], (jbyte *)ptrs[i], JNI_ABORT);
     if (nb < 0) {
         throw_for(env, (int)nb, H(h));
     } else {
         res = (*env)->NewByteArray(env, (jsize)nb);
         if (res) (*env)->SetByteArrayRegion(env, res, 0, (jsize)nb, (const jbyte *)out);
     }
+done:
+    for (jsize i = 0; i < got; ++i)
+        if (ptrs[i]) (*env)->ReleaseByteArrayElements(env, arr[i], (jbyte *)ptrs[i], JNI_ABORT);
+    if (arr)
+        for (jsize i = 0; i <= got && i < k; ++i)
+            if (arr[i]) (*env)->DeleteLocalRef(env, arr[i]);
     free(out); free(lens); free(ptrs); free(arr);
     return res;
 }
 
-JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf) {
+JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf,
+                                                                 jint pos, jlong nBytes) {
     (void)c;
-    jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
-    CHECK(ipls_agg_get_partitions(H(h), (*env)->GetDirectBufferAddress(env, buf), cap / 8, IPLS_HOST_BE_CANON),
-          H(h));
+    void *dst = direct_span(env, buf, pos, nBytes);
+    if (!dst) return;
+    CHECK(ipls_agg_get_partitions(H(h), dst, nBytes / 8, IPLS_HOST_BE_CANON), H(h));
 }
 
 JNIEXPORT jobject JNICALL Java_NativeAggregator_hostAllocDirect(JNIEnv *env, jclass c, jint bytes) {
     (void)c;
+    if (bytes < 0) { throw_iae(env, "negative size"); return NULL; }
     void *p = NULL;
     int rc = ipls_host_alloc((size_t)bytes, &p);
     if (rc < 0) { throw_for(env, rc, NULL); return NULL; }
     return (*env)->NewDirectByteBuffer(env, p, bytes);
+}
+
+/* ---- device-resident batches (ipls_agg_reduce_batch / reduce_partial) ----
+ * ptrs holds n_parts * k device addresses (long), partition-major. */
+static const void *const *dev_ptrs(JNIEnv *env, jlongArray ptrs, jint np, jint k, jlong **held) {
+    *held = NULL;
+    if (np <= 0 || k < 0) { throw_iae(env, "bad batch shape"); return NULL; }
+    if (!need_len(env, ptrs, (int64_t)np * k, "device pointers")) return NULL;
+    *held = (*env)->GetLongArrayElements(env, ptrs, NULL);
+    if (!*held) { throw_msg(env, "java/lang/OutOfMemoryError", "device pointers"); return NULL; }
+    return (const void *const *)*held;   /* jlong and void* are both 64-bit here */
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_reduceBatchDevice(JNIEnv *env, jclass c, jlong h, jint p0, jint np,
+                                                                 jlongArray ptrs, jint k, jint kind, jint start,
+                                                                 jint target) {
+    (void)c;
+    jlong *held;
+    const void *const *b = dev_ptrs(env, ptrs, np, k, &held);
+    if (!b) return;
+    int rc = ipls_agg_reduce_batch(H(h), p0, np, b, k, kind, start, target);
+    (*env)->ReleaseLongArrayElements(env, ptrs, held, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT void JNICALL Java_NativeAggregator_reducePartialDevice(JNIEnv *env, jclass c, jlong h, jint slot, jint p0,
+                                                                   jint np, jlongArray ptrs, jint k, jint kind,
+                                                                   jint start) {
+    (void)c;
+    jlong *held;
+    const void *const *b = dev_ptrs(env, ptrs, np, k, &held);
+    if (!b) return;
+    int rc = ipls_agg_reduce_partial(H(h), slot, p0, np, b, k, kind, start);
+    (*env)->ReleaseLongArrayElements(env, ptrs, held, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
+JNIEXPORT jint JNICALL Java_NativeAggregator_combinePartials(JNIEnv *env, jclass c, jlong h, jint p0, jint np) {
+    (void)c;
+    int rc = ipls_agg_combine_partials(H(h), p0, np);
+    CHECK(rc, H(h));
+    return rc;
+}
+
+/* Marshall_Packet(target[p], origin, a, b, pid) as the Base64.getUrlEncoder
+ * text (MyIPFSClass.java:990-1016), encoded on the GPU. */
+JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_publishPartial(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
+                                                                    jint a, jint b, jshort pid, jbyteArray origin) {
+    (void)c;
+    jsize ol = origin ? (*env)->GetArrayLength(env, origin) : 0;
+    jbyte *o = origin ? (*env)->GetByteArrayElements(env, origin, NULL) : NULL;
+    jbyteArray res = NULL;
+    int64_t n = ipls_agg_publish_partial(H(h), p, tgt, a, b, pid, (const uint8_t *)o, ol, NULL, 0, IPLS_HOST_TEXT);
+    uint8_t *text = n >= 0 ? (uint8_t *)malloc((size_t)(n > 0 ? n : 1)) : NULL;
+    if (n >= 0 && !text) {
+        throw_msg(env, "java/lang/OutOfMemoryError", "publish text");
+    } else if (n >= 0) {
+        n = ipls_agg_publish_partial(H(h), p, tgt, a, b, pid, (const uint8_t *)o, ol, text, n, IPLS_HOST_TEXT);
+    }
+    if (o) (*env)->ReleaseByteArrayElements(env, origin, o, JNI_ABORT);
+    if (n < 0) {
+        throw_for(env, (int)n, H(h));
+    } else if (text) {
+        res = (*env)->NewByteArray(env, (jsize)n);
+        if (res) (*env)->SetByteArrayRegion(env, res, 0, (jsize)n, (const jbyte *)text);
+    }
+    free(text);
+    return res;
 }

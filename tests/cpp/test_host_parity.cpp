@@ -280,6 +280,57 @@ int main(int argc, char** argv) {
       }
     });
 
+    run("Client_Wait_Ack drained -> the queued folds start (flush hint)", [&] {
+      PeerData pd;
+      pd._MODEL_SIZE = 120001;
+      pd._PARTITIONS = 4;
+      IPLS ipls(pd, {0, 1, 2, 3});
+      IPLS src(pd);
+      check(ipls_agg_set_coalesce(ipls.handle(), 1 << 20), ipls.handle());   // no size-triggered flush
+      std::vector<int64_t> L(4);
+      std::vector<std::vector<std::vector<double>>> vals(4);
+      std::vector<std::vector<double>> dv(4);
+      std::vector<const void*> dptr(4);
+      for (int p = 0; p < 4; ++p) {
+        L[p] = ipls.partition_length(p);
+        dv[p] = synth(L[p], p, 5);
+        check(ipls_agg_accumulate(src.handle(), p, IPLS_TGT_AGG, dv[p].data(), L[p], IPLS_HOST_F64), src.handle());
+        void* d = nullptr;
+        check(ipls_agg_device_ptr(src.handle(), p, IPLS_TGT_AGG, &d), src.handle());
+        dptr[p] = d;
+      }
+      check(ipls_agg_sync(src.handle()), src.handle());
+      const char* peers[3] = {"QmA", "QmB", "QmC"};
+      {
+        UpdaterThread ut(ipls, std::chrono::seconds(30));   // an idle flush would take 30 s
+        ut.Client_Wait_Ack({peers[0], peers[1], peers[2]});
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < 3; ++k)
+          for (int p = 0; p < 4; ++p) {
+            UpdaterThread::Request r;
+            r.partition = p;
+            r.device = dptr[p];
+            r.device_n = L[p];
+            r.origin = peers[k];
+            ut.put(std::move(r));
+          }
+        ut.Wait_Client_Gradients();
+        // the request that cleared the last trainer launched the folds
+        for (int i = 0; i < 2000 && ut.hint_flushes() == 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        CHECK(ut.hint_flushes() == 1, "one flush at the drain of Client_Wait_Ack");
+        CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10), "not the idle flush");
+        ut.drain();
+        CHECK(ut.failures().empty(), "no failures");
+      }
+      for (int p = 0; p < 4; ++p) {
+        const double* bp[3] = {dv[p].data(), dv[p].data(), dv[p].data()};
+        std::vector<double> ref((size_t)L[p]), got((size_t)L[p]);
+        ipls_oracle_reduce(ref.data(), bp, 3, L[p], 1);
+        check(ipls_agg_read(ipls.handle(), p, IPLS_TGT_AGG, got.data(), L[p], IPLS_HOST_F64), ipls.handle());
+        CHECK(bits_equal(got.data(), ref.data(), (size_t)L[p]), "three queued arrivals per partition");
+      }
+    });
+
     run("partial updates (-i 1): commit, replica fold, storage merge", [&] {
       PeerData pd;
       pd._MODEL_SIZE = 20001;

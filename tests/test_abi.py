@@ -82,10 +82,10 @@ def test_open_without_gpu_fails_loudly():
 
 
 def test_jni_shim_matches_java_natives():
-    """No JDK here, so the JNI shim is not compiled; this keeps it consistent
-    with NativeAggregator.java (every native has its Java_NativeAggregator_*
-    function and no function is orphaned) and with include/ipls_agg.h (every
-    ipls_* it calls is declared)."""
+    """The JNI shim against NativeAggregator.java (every native has its
+    Java_NativeAggregator_* function and no function is orphaned) and
+    include/ipls_agg.h (every ipls_* it calls is declared).  tests/test_jni.py
+    compiles and drives it."""
     import re
     pkg = ROOT / "ipls-java-api_amd"
     java = (pkg / "java" / "NativeAggregator.java").read_text()

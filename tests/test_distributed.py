@@ -40,6 +40,9 @@ class NumpyAggregator:
     def finalize(self, p):
         return self.agg[p] + self.rep[p]
 
+    def sync(self):
+        pass
+
 
 def free_port():
     s = socket.socket()
@@ -256,3 +259,12 @@ def test_replica_exchange_hip_aggregators_two_processes():
     assert sorted(got) == sorted(exp)
     for p in exp:
         assert_bits_equal(got[p], exp[p], f"partition {p}")
+
+
+def test_rccl_reduce_rejects_a_caller_group():
+    """dist.reduce over a caller-given group would hang the ranks
+    outside it; the mode builds its own per-partition groups instead."""
+    from ipls.distributed import ReplicaPlan, combine_replicas
+    plan = ReplicaPlan.build(4, 2, {1: [1]})
+    with pytest.raises(ValueError):
+        combine_replicas(NumpyAggregator(4, 8), plan, 0, mode="rccl_reduce", group=object())

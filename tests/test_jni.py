@@ -1,0 +1,328 @@
+"""The JNI shim (ipls-java-api_amd/jni/ipls_jni.c), compiled and driven
+without a JDK (ADVICE r1 JNI items).
+
+tests/jni/jni.h declares exactly the JNI types and JNIEnv entries the shim
+uses; tests/jni/fake_jvm.c implements them (Java arrays, direct ByteBuffers,
+pending exceptions) and counts breaks of the JNI rules (calls inside a
+critical region, calls with an exception pending, unreleased elements,
+region writes past an array).  The shim is built with -Wall -Wextra -Werror
+into one test library with the fake JVM and linked to the real
+libipls_agg.so.  CPU tests cover the argument checks the shim does before
+the library is called; -m gpu tests run whole Java-API sequences through the
+natives against the oracle, including the exception mapping and the
+guarantee that a rejected call leaves the accumulators unchanged.
+"""
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, assert_bits_equal
+
+BUILD = ROOT / "tests" / "jni" / "build"
+LIB = BUILD / "libfakejni.so"
+AGG = ROOT / "ipls-java-api_amd" / "lib"
+
+_j = None
+
+
+def build():
+    BUILD.mkdir(parents=True, exist_ok=True)
+    subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
+                    f"-I{ROOT / 'tests' / 'jni'}", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "jni" / "fake_jvm.c"), str(ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c"),
+                    f"-L{AGG}", "-lipls_agg", f"-Wl,-rpath,{AGG}", "-o", str(LIB)], check=True)
+
+
+class JVM:
+    """ctypes view of the fake JVM + the natives of NativeAggregator."""
+
+    def __init__(self):
+        build()
+        L = ctypes.CDLL(str(LIB))
+        vp = ctypes.c_void_p
+        for name, res, args in [
+            ("fj_env", vp, []), ("fj_new_bytes", vp, [vp, ctypes.c_int32]), ("fj_new_ints", vp, [vp, ctypes.c_int32]),
+            ("fj_new_longs", vp, [vp, ctypes.c_int32]), ("fj_new_doubles", vp, [vp, ctypes.c_int32]),
+            ("fj_new_objects", vp, [vp, ctypes.c_int32]), ("fj_new_direct", vp, [vp, ctypes.c_int64]),
+            ("fj_data", vp, [vp]), ("fj_len", ctypes.c_int32, [vp]), ("fj_free", None, [vp]),
+            ("fj_exception", ctypes.c_char_p, []), ("fj_exception_msg", ctypes.c_char_p, []), ("fj_clear", None, []),
+            ("fj_violations", ctypes.c_int, []), ("fj_last_violation", ctypes.c_char_p, []),
+            ("fj_reset_violations", None, [])]:
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        self.L = L
+        self.env = ctypes.c_void_p(L.fj_env())
+        self.keep = []
+
+    # ---- Java objects ----
+    def doubles(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        return ctypes.c_void_p(self.L.fj_new_doubles(a.ctypes.data, a.size))
+
+    def bytes_(self, b):
+        a = np.frombuffer(bytes(b), dtype=np.uint8)
+        return ctypes.c_void_p(self.L.fj_new_bytes(a.ctypes.data if a.size else None, a.size))
+
+    def ints(self, a):
+        a = np.ascontiguousarray(a, dtype=np.int32)
+        return ctypes.c_void_p(self.L.fj_new_ints(a.ctypes.data if a.size else None, a.size))
+
+    def longs(self, a):
+        a = np.ascontiguousarray(a, dtype=np.int64)
+        return ctypes.c_void_p(self.L.fj_new_longs(a.ctypes.data if a.size else None, a.size))
+
+    def objects(self, objs):
+        arr = (ctypes.c_void_p * max(1, len(objs)))(*[o.value for o in objs])
+        return ctypes.c_void_p(self.L.fj_new_objects(arr, len(objs)))
+
+    def direct(self, nbytes=None, heap=False):
+        """A direct ByteBuffer over host memory this object keeps alive
+        (heap=True: a heap ByteBuffer, no address)."""
+        if heap:
+            return ctypes.c_void_p(self.L.fj_new_direct(None, -1)), None
+        mem = np.zeros(nbytes, dtype=np.uint8)
+        self.keep.append(mem)
+        return ctypes.c_void_p(self.L.fj_new_direct(mem.ctypes.data, nbytes)), mem
+
+    def data(self, obj, dtype, n=None):
+        n = self.L.fj_len(obj) if n is None else n
+        size = np.dtype(dtype).itemsize * n
+        buf = (ctypes.c_char * size).from_address(self.L.fj_data(obj))
+        return np.frombuffer(buf, dtype=dtype).copy()
+
+    # ---- calls ----
+    def call(self, name, *args, res=None):
+        f = getattr(self.L, "Java_NativeAggregator_" + name)
+        f.restype = res
+        self.L.fj_clear()
+        self.L.fj_reset_violations()
+        conv = []
+        for a in args:
+            if isinstance(a, float):
+                conv.append(ctypes.c_double(a))
+            elif isinstance(a, int):
+                assert abs(a) < 2 ** 31, "pass jlong arguments as ctypes.c_int64"
+                conv.append(ctypes.c_int32(a))
+            elif a is None:
+                conv.append(ctypes.c_void_p(None))
+            else:
+                conv.append(a)
+        r = f(self.env, None, *conv)
+        v = self.L.fj_violations()
+        assert v == 0, f"{name}: JNI rule broken: {self.L.fj_last_violation()}"
+        exc = self.L.fj_exception()
+        return r, (exc.decode() if exc else None)
+
+
+@pytest.fixture(scope="module")
+def jvm():
+    global _j
+    if _j is None:
+        _j = JVM()
+    return _j
+
+
+L64 = ctypes.c_int64
+
+
+def test_shim_builds_with_werror_and_exports_every_native(jvm):
+    import re
+    java = (ROOT / "ipls-java-api_amd" / "java" / "NativeAggregator.java").read_text()
+    natives = set(re.findall(r"\bnative\s+[\w\[\]<>.]+\s+(\w+)\s*\(", java))
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"Java_NativeAggregator_(\w+)", out))
+    assert natives == exported, natives ^ exported
+
+
+def test_shard_plan_native(jvm):
+    r, exc = jvm.call("shardPlan", 10, 4, res=ctypes.c_void_p)
+    assert exc is None
+    assert list(jvm.data(r, np.int32)) == [0, 0, 0, 1, 1, 1, 2, 2, 2, 3]
+    r, exc = jvm.call("shardPlan", 10, 0, res=ctypes.c_void_p)
+    assert r is None and exc == "java/lang/IllegalArgumentException"
+
+
+def test_direct_buffer_checks_before_the_library(jvm):
+    """a heap ByteBuffer (no address) or a position/length outside
+    the buffer is an IllegalArgumentException, never a silent no-op or a read
+    of the wrong bytes -- checked before the handle is even looked at."""
+    heap, _ = jvm.direct(heap=True)
+    buf, _ = jvm.direct(64)
+    for name, args in [("accumulateDirect", (L64(0), 0, 0, heap, 0, L64(4), 1)),
+                       ("accumulateDirect", (L64(0), 0, 0, buf, 40, L64(4), 1)),      # 40 + 32 > 64
+                       ("accumulateDirect", (L64(0), 0, 0, buf, -8, L64(1), 1)),
+                       ("accumulateAsyncDirect", (L64(0), 0, 0, heap, 0, L64(1), 1)),
+                       ("updateIndirect", (L64(0), 0, 0, buf, 8, L64(57))),
+                       ("setWeightsDirect", (L64(0), 0, heap, 0, L64(1))),
+                       ("otherReplicaDirect", (L64(0), 0, 1, buf, 0, L64(9))),
+                       ("getPartitionsWire", (L64(0), heap, 0, L64(8)))]:
+        _, exc = jvm.call(name, *args)
+        assert exc == "java/lang/IllegalArgumentException", (name, exc)
+
+
+def test_open_without_gpu_throws(jvm):
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h, exc = jvm.call("open", L64(443610), 3, 3, 0, 0, 0, res=ctypes.c_int64)
+    assert h == 0 and exc == "java/lang/RuntimeException"
+    assert b"device" in jvm.L.fj_exception_msg().lower()
+
+
+# ---------------------------------------------------------------------------
+# on the GPU: Java-API sequences through the natives
+# ---------------------------------------------------------------------------
+@pytest.fixture
+def gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle as o   # checker only
+    return o
+
+
+def _open(jvm, M, P, devices=None):
+    if devices is None:
+        h, exc = jvm.call("open", L64(M), P, 3, 0, 0, 0, res=ctypes.c_int64)
+    else:
+        h, exc = jvm.call("openDevices", L64(M), P, 3, 0, 0, jvm.ints(devices), res=ctypes.c_int64)
+    assert exc is None and h
+    return L64(h)
+
+
+@pytest.mark.gpu
+def test_jni_round_against_oracle(jvm, gpu, O):
+    """IPLS round through the natives: updateGradient (own partitions),
+    accumulate (heap double[]), updateFromBytes (direct buffer at a non-zero
+    position), finalizePartition (commit_update bytes), aggregateRound,
+    getPartitions and the Middleware wire stream."""
+    M, P, K = 30011, 3, 4
+    h = _open(jvm, M, P)
+    peers = [O.synth_bucket(M, 4, k) for k in range(K)]
+    parts = [O.organize_gradients(g, M, P) for g in peers]
+    _, exc = jvm.call("updateGradient", h, jvm.doubles(peers[0]), jvm.ints([0, 1, 2]))
+    assert exc is None
+    for p in range(P):
+        _, exc = jvm.call("accumulate", h, p, 0, jvm.doubles(parts[1][p]))
+        assert exc is None
+        # a direct buffer with position 16: the bucket starts 16 bytes in
+        be = O.be_encode(parts[2][p])
+        buf, mem = jvm.direct(16 + len(be) + 8)
+        mem[16:16 + len(be)] = np.frombuffer(be, dtype=np.uint8)
+        _, exc = jvm.call("accumulateDirect", h, p, 0, buf, 16, L64(len(be) // 8), 1)
+        assert exc is None
+        split_out = jvm.doubles(np.zeros(len(parts[3][p])))
+        _, exc = jvm.call("split", h, jvm.doubles(peers[3]), p, split_out)
+        assert exc is None
+        assert_bits_equal(jvm.data(split_out, np.float64), parts[3][p], "split")
+        _, exc = jvm.call("accumulate", h, p, 0, split_out)
+        assert exc is None
+    sums = []
+    for p in range(P):
+        s = O.reduce([parts[k][p] for k in range(K)], len(parts[0][p]))
+        sums.append(s)
+        out = jvm.bytes_(b"\0" * (8 * len(s)))
+        _, exc = jvm.call("finalizePartition", h, p, out)
+        assert exc is None
+        assert jvm.data(out, np.uint8).tobytes() == O.be_encode(s)
+    avg = O.get_partitions(sums)
+    got = jvm.doubles(np.zeros(M))
+    _, exc = jvm.call("getPartitions", h, got)
+    assert exc is None
+    assert_bits_equal(jvm.data(got, np.float64), avg, "getPartitions")
+    wire, mem = jvm.direct(8 * M + 24)
+    _, exc = jvm.call("getPartitionsWire", h, wire, 24, L64(8 * M))
+    assert exc is None and mem[24:].tobytes() == O.be_encode_canonical(avg)
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
+def test_jni_exceptions_leave_state_unchanged(jvm, gpu, O):
+    """A short bucket is ArrayIndexOutOfBoundsException with nothing folded
+    (Updater.java:115-117 would throw mid-loop; the library rejects it first,
+    DESIGN.md §1); wrong output sizes are IllegalArgumentException before the
+    library writes anything; a bad frame is BufferUnderflowException."""
+    M, P = 20003, 2
+    h = _open(jvm, M, P)
+    g = O.organize_gradients(O.synth_bucket(M, 1, 1), M, P)
+    _, exc = jvm.call("accumulate", h, 0, 0, jvm.doubles(g[0]))
+    assert exc is None
+    _, exc = jvm.call("accumulate", h, 0, 0, jvm.doubles(g[0][:-1]))     # one short
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    _, exc = jvm.call("accumulate", h, 5, 0, jvm.doubles(g[0]))          # no partition 5
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    _, exc = jvm.call("accumulateFrame", h, 0, 0, jvm.bytes_(b"\0\3\0\0"))
+    assert exc == "java/nio/BufferUnderflowException"
+    L0 = len(g[0])
+    _, exc = jvm.call("finalizePartition", h, 0, jvm.bytes_(b"\0" * (8 * L0 - 1)))
+    assert exc == "java/lang/IllegalArgumentException"
+    _, exc = jvm.call("aggregateRound", h, 0, P, jvm.doubles(np.zeros(M - 1)))
+    assert exc == "java/lang/IllegalArgumentException"
+    _, exc = jvm.call("collectReplicas", h, jvm.ints([0]), res=ctypes.c_int32)
+    assert exc == "java/lang/IllegalArgumentException"
+    _, exc = jvm.call("split", h, jvm.doubles(np.zeros(M)), 1, jvm.doubles(np.zeros(3)))
+    assert exc == "java/lang/IllegalArgumentException"
+    texts = jvm.objects([jvm.bytes_(O.pubsub_message(O.frame_encode(g[0], 0, 1, 3, b"Q")))] * 2)
+    _, exc = jvm.call("ingestTexts", h, 0, texts, 2, None, jvm.ints([0]), res=ctypes.c_int32)
+    assert exc == "java/lang/IllegalArgumentException"
+    # none of the rejected calls touched AGG[0]: finalize gives exactly the one good fold
+    out = jvm.bytes_(b"\0" * (8 * L0))
+    _, exc = jvm.call("finalizePartition", h, 0, out)
+    assert exc is None and jvm.data(out, np.uint8).tobytes() == O.be_encode(0.0 + g[0])
+    # the ingest itself, statuses into a right-sized array
+    st = jvm.ints([9, 9])
+    n, exc = jvm.call("ingestTexts", h, 0, texts, 2, None, st, res=ctypes.c_int32)
+    assert exc is None and n == 2 and list(jvm.data(st, np.int32)) == [0, 0]
+    parts_ok = jvm.ints([0, 0])
+    n, exc = jvm.call("collectReplicas", h, parts_ok, res=ctypes.c_int32)
+    assert exc is None and n == 0
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
+def test_jni_devices_publish_and_device_batches(jvm, gpu, O):
+    """openDevices over two shards of one GPU, partitionDevice, the device
+    batch natives (reduceBatchDevice / reducePartialDevice / combinePartials)
+    and publishPartial == Base64.getUrlEncoder(Marshall_Packet frame)."""
+    import torch
+    import ipls
+    L, P, K = 10_001, 4, 4
+    M = P * (L - 1)
+    h = _open(jvm, M, P, devices=[0, 0])
+    assert [jvm.call("partitionDevice", h, p, res=ctypes.c_int32)[0] for p in range(P)] == [0] * P
+    Ls = [jvm.call("partitionLen", h, p, res=ctypes.c_int64)[0] for p in range(P)]
+    t = torch.empty(P * K * (max(Ls) + 2), dtype=torch.float64, device="cuda")
+    base = (int(t.data_ptr()) + 15) // 16 * 16
+    ptr = [[base + 8 * (q * K + k) * (max(Ls) + 2) for k in range(K)] for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(ipls.DeviceBuffer(ptr[q][k], Ls[q]), q, k, O.SEED)
+    torch.cuda.synchronize()
+    own = [x for q in range(P) for x in ptr[q][:2]]
+    _, exc = jvm.call("reduceBatchDevice", h, 0, P, jvm.longs(own), 2, 3, 1, 0)
+    assert exc is None
+    # slot 1 replicates partitions 0-1, slot 0 partitions 2-3
+    _, exc = jvm.call("reducePartialDevice", h, 1, 0, 2, jvm.longs([x for q in (0, 1) for x in ptr[q][2:]]), 2, 3, 1)
+    assert exc is None
+    _, exc = jvm.call("reducePartialDevice", h, 0, 2, 2, jvm.longs([x for q in (2, 3) for x in ptr[q][2:]]), 2, 3, 1)
+    assert exc is None
+    n, exc = jvm.call("combinePartials", h, 0, P, res=ctypes.c_int32)
+    assert exc is None and n == P
+    for q in range(P):
+        b = [O.synth_bucket(Ls[q], q, k) for k in range(K)]
+        w = O.reduce(b[:2], Ls[q]) + (0.0 + O.reduce(b[2:], Ls[q]))
+        text, exc = jvm.call("publishPartial", h, q, 1, 7, 3, 3, jvm.bytes_(b"QmOrigin"), res=ctypes.c_void_p)
+        assert exc is None
+        assert jvm.data(text, np.uint8).tobytes() == O.java_b64url_encode(
+            O.frame_encode(0.0 + O.reduce(b[2:], Ls[q]), 7, 3, 3, b"QmOrigin"))   # REP = +0.0 + R
+        out = jvm.bytes_(b"\0" * (8 * Ls[q]))
+        _, exc = jvm.call("finalizePartition", h, q, out)
+        assert exc is None and jvm.data(out, np.uint8).tobytes() == O.be_encode(w)
+    jvm.call("close", h)
+    del t
