@@ -74,17 +74,43 @@ def parse():
     ap.add_argument("--no-strong-leg", action="store_true",
                     help="N>1: skip the fixed-total-work leg (config D split over the ranks)")
     ap.add_argument("--replica-reps", type=int, default=5)
-    ap.add_argument("--replica-timeout", type=float, default=120.0)
+    ap.add_argument("--no-multi-leg", action="store_true",
+                    help="N>1: skip the single-handle multi-GPU leg (rank 0 drives all N GPUs through the C-ABI)")
+    ap.add_argument("--multi-rehearsal", action="store_true",
+                    help="N=1: run the single-handle multi-GPU leg over two shards of GPU 0 (a functional "
+                         "rehearsal of the cross-GPU code path; the numbers measure one GPU)")
+    ap.add_argument("--replica-timeout", type=float, default=240.0)
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearsal of the N>1 code on one GPU (ranks share cuda:0, partials "
                          "travel through host memory); numbers are not a measurement")
     return ap.parse_args()
 
 
-def cpu_baseline(L: int, K: int, passes: int) -> dict:
+def cpu_share() -> tuple[int, dict]:
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU
+    quota and by OMP_NUM_THREADS (the GPU box sets both to its per-GPU share)."""
+    n = len(os.sched_getaffinity(0))
+    info = {"nproc": os.cpu_count(), "affinity": n}
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q[0] != "max":
+            info["cgroup_quota_cpus"] = round(int(q[0]) / int(q[1]), 2)
+            n = min(n, max(1, int(int(q[0]) // int(q[1]))))
+    except (OSError, ValueError, IndexError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        info["OMP_NUM_THREADS"] = int(os.environ["OMP_NUM_THREADS"])
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    return max(1, n), info
+
+
+def cpu_baseline(L: int, K: int, passes: int, mt_passes: int = 2) -> dict:
     """Reference Updater loop (Updater.java:162-187 + 115-117, MyIPFSClass.java:
     444-455) restated in C, ONE thread as the reference's single Updater thread:
-    per bucket a BE getDouble decode into a reused buffer, then the fold."""
+    per bucket a BE getDouble decode into a reused buffer, then the fold.
+    Beside it the N-thread partition-parallel variant of SURVEY.md §8(d): N
+    partitions with their OWN K buckets each, one thread per partition, N =
+    the CPUs this process may use (cpu_share)."""
     from oracle import oracle as O
     be = []
     for k in range(K):
@@ -96,17 +122,31 @@ def cpu_baseline(L: int, K: int, passes: int) -> dict:
         O.c_updater_loop(be, L)
     dt = time.perf_counter() - t0
     nbytes = passes * (K + 1) * L * 8
-    # N-thread partition-parallel variant (OMP_NUM_THREADS threads, 16 on the GPU box)
-    t1 = time.perf_counter()
-    _, threads = O.c_updater_loop_parts(be, L, passes)
-    dt_mt = time.perf_counter() - t1
+    del be
+    threads, share = cpu_share()
+    mt = {}
+    try:
+        bufs = O.c_synth_be_buckets(threads, K, L)     # threads x K distinct buckets (BE bytes)
+        O.c_updater_loop_partitions(bufs, threads, K, L, 1, threads)   # warm pages
+        t1 = time.perf_counter()
+        _, used = O.c_updater_loop_partitions(bufs, threads, K, L, mt_passes, threads)
+        dt_mt = time.perf_counter() - t1
+        mt_bytes = mt_passes * threads * (K + 1) * L * 8
+        mt = {"value": round(mt_bytes / dt_mt / 1e9, 3), "cores": used,
+              "sample": f"{mt_passes} passes x {threads} partitions (one per thread), each with its own {K} BE "
+                        f"buckets of {L} doubles ({threads * K * L * 8 / 1e9:.1f} GB of buckets, "
+                        f"{mt_bytes / 1e9:.1f} GB algorithmic, {dt_mt:.1f} s)",
+              "cpu_share": share,
+              "note": "N = the CPUs this process may use (affinity, cgroup quota, OMP_NUM_THREADS): the GPU box "
+                      "grants each GPU its share of the host, so N is that share, not nproc"}
+        del bufs
+    except MemoryError as e:
+        mt = {"error": f"MemoryError: {e}"}
     return {"value": round(nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"{passes} passes x 1 partition x {K} peers x {L} doubles "
                       f"({nbytes / 1e9:.1f} GB algorithmic, {dt:.1f} s), BE decode + fold, "
                       f"oracle/ipls_oracle.c ipls_oracle_updater_loop (JDK absent: C restatement)",
-            "multi_thread": {"value": round(nbytes / dt_mt / 1e9, 3), "cores": threads,
-                             "sample": f"{passes} partitions in parallel, one thread each"},
-            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
+            "multi_thread": mt, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
 def _cpu_model() -> str:
@@ -254,6 +294,106 @@ def replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, reps, verify,
         "note": "exchange_ms = export of the partials, one batched RCCL send/recv group, fold into REP "
                 "(max over ranks); round adds both folds and AggregatePartition",
     }
+
+
+def c_abi_multi_gpu(ipls, torch, devices, P: int, L: int, K: int, reps: int = 5, verify: bool = True) -> dict:
+    """ONE C-ABI handle over several GPUs (cfg.devices), as a single JVM drives
+    a node through the JNI shim: the -pa partitions sharded P per device in
+    contiguous blocks (ipls_shard_plan), K peers each.
+    (a) one ipls_agg_reduce_batch over all partitions: the front queues every
+        shard's launch on its own stream, so the GPUs fold concurrently;
+    (b) contributors spanning GPUs (the reference's replica
+        aggregators, IPLS.java:1402-1468): each partition's first K/2 peers fold
+        on its owner, the other K/2 on a replica slot (spread: partition q of
+        owner o on GPU (o + 1 + q mod (G-1)) mod G, so every owner pulls from
+        all G-1 others), ipls_agg_reduce_partial; ipls_agg_combine_partials
+        then pulls each partial over xGMI with peer loads in the owner's fold
+        kernel into REP, and AggregatePartition forms W = AGG + REP.
+    Buckets are resident on the GPU that folds them.  Checked against the
+    oracle's checksums (first and last partition; W of partition 0)."""
+    G = len(devices)
+    PT = P * G
+    kh = K // 2
+    elem = L + 32
+    pools, rows = [], []
+    for s, d in enumerate(devices):
+        with torch.cuda.device(d):
+            t = torch.empty(P * K * elem + 32, dtype=torch.float64, device=f"cuda:{d}")
+            base = (int(t.data_ptr()) + 255) // 256 * 256
+            pools.append(t)
+            for q in range(P):
+                row = [ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L) for k in range(K)]
+                for k in range(K):
+                    ipls.synth_fill(row[k], s * P + q, k, ipls.SEED)
+                rows.append(row)
+    for d in sorted(set(devices)):
+        torch.cuda.synchronize(d)
+    agg = ipls.Aggregator(n_partitions=PT, bucket_len=L, devices=list(devices))
+    out = {"devices": list(devices), "workload": f"{PT} partitions ({P} per GPU) x {L} doubles x {K} peers, "
+                                                 f"one handle over {G} GPUs"}
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    agg.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    agg.sync()
+    dt = (time.perf_counter() - t0) / reps
+    nbytes = PT * (K + 1) * L * 8
+    out["reduce_ms"] = round(dt * 1e3, 4)
+    out["reduce_GBps"] = round(nbytes / dt / 1e9, 1)
+    out["reduce_GBps_per_gpu"] = round(nbytes / dt / 1e9 / G, 1)
+    if verify:
+        from oracle import oracle as O   # checker only
+        out["verified_checksums"] = (agg.checksum(0) == O.c_synth_sum_checksum(L, 0, K) and
+                                     agg.checksum(PT - 1) == O.c_synth_sum_checksum(L, PT - 1, K))
+    if G > 1:
+        slot = {}
+        for o in range(G):
+            for q in range(P):
+                slot[o * P + q] = (o + 1 + q % (G - 1)) % G
+        spare = {s: [rows[s * P + q][kh:] for q in range(P)] for s in range(G)}
+        far = {}
+        for p in range(PT):
+            s = slot[p]
+            far[p] = spare[s].pop(0)
+            with torch.cuda.device(devices[s]):
+                for k in range(kh, K):
+                    ipls.synth_fill(far[p][k - kh], p, k, ipls.SEED)
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+        own = [r[:kh] for r in rows]
+
+        def one_round():
+            agg.reduce_batch(0, own, start_mode=ipls.START_ZERO)
+            for p in range(PT):
+                agg.reduce_partial(slot[p], p, [far[p]], start_mode=ipls.START_ZERO)
+            agg.sync()
+            t0 = time.perf_counter()
+            n = agg.combine_partials()
+            agg.sync()
+            t1 = time.perf_counter()
+            agg.AggregatePartition(ipls.ALL_PARTITIONS)
+            agg.sync()
+            return t1 - t0, n
+        one_round()
+        ex = []
+        for _ in range(reps):
+            ex.append(one_round()[0])
+        tex = float(np.median(ex))
+        moved = PT * L * 8
+        out["combine_ms"] = round(tex * 1e3, 4)
+        out["combine_xgmi_GBps"] = round(moved / tex / 1e9, 1)
+        out["combine_note"] = (f"{PT} partials of {L * 8 / 2**20:.0f} MiB pulled by their owners "
+                               "(peer loads over xGMI; shards on one GPU read local memory), folded into REP in "
+                               "slot order; median of the combine step alone")
+        if verify:
+            from oracle import oracle as O   # checker only
+            out["verified_replica_checksum_p0"] = (agg.checksum(0, ipls.TGT_WEIGHTS) ==
+                                                   O.c_synth_replica_checksum(L, 0, K, kh))
+    agg.close()
+    del pools, rows
+    torch.cuda.empty_cache()
+    return out
 
 
 def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, verify: bool = True) -> dict:
@@ -464,6 +604,53 @@ def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: f
     return info
 
 
+def publish_leg(ipls, torch, agg, stream, L: int, reps: int = 10, verify: bool = True) -> dict:
+    """a9: the aggregator's partial sum published every round (IPLS.java:
+    1429-1430: Marshall_Packet + Base64.getUrlEncoder, MyIPFSClass.java:
+    990-1016), encoded on the GPU straight from an accumulator
+    (k_b64url_encode_frame): here Weights[0], which the fused round left
+    holding partition 0's sum (AGG is logically zero after it; same kernel).
+    Device text: HIP events around the call on the handle's stream;
+    algorithmic bytes = 8 L read + the text written.  Host text: wall clock,
+    the D2H of the text included (PCIe-bound).  Checked against the oracle's
+    Java encoder on the partition's values."""
+    origin = b"QmPublishingPeerIdentity0123456789abcdefghijk"   # a 46-char IPFS peer id
+    text_len = 4 * -(-(14 + 8 * L + len(origin)) // 3)
+    buf = torch.empty(text_len + 64, dtype=torch.uint8, device="cuda")
+    ptr = int(buf.data_ptr())
+    agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=ptr)
+    agg.sync()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record(stream)
+    for i in range(reps):
+        agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=ptr)
+        ev[i + 1].record(stream)
+    agg.sync()
+    ms = float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]))
+    nbytes = 8 * L + text_len
+    pinned = ipls.PinnedBuffer(text_len)
+    agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=pinned)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=pinned)
+    dt = (time.perf_counter() - t0) / 5
+    host = bytes(pinned.view()[:text_len])
+    pinned.close()
+    ok = None
+    if verify:
+        from oracle import oracle as O   # checker only
+        ok = (host == O.java_b64url_encode(O.frame_encode(agg.read(0, ipls.TGT_WEIGHTS), 7, 33, 3, origin)) and
+              bytes(buf[:text_len].cpu().numpy()) == host)
+    del buf
+    return {"partition_doubles": L, "text_bytes": text_len, "device_ms": round(ms, 4),
+            "device_GBps": round(nbytes / ms / 1e6, 1), "device_frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "host_text_ms": round(dt * 1e3, 3), "host_text_GBps": round(text_len / dt / 1e9, 2),
+            "verified_vs_java_encoder": ok,
+            "note": "Marshall_Packet(W[0], origin, 7, 33, pid 3) -> base64url with padding; device_GBps counts "
+                    "8L read + the text written; host_text: the same call with the text landing in pinned host "
+                    "memory (C-ABI call wall time, D2H included)"}
+
+
 def strong_leg(ipls, torch, dist, rank: int, world: int, local: int, steps: int = 5, verify: bool = True) -> dict:
     """Fixed total work ('at fixed total work (config D)'):
     config D's 64 partitions x 4M doubles x 32 peers split over the ranks in
@@ -546,6 +733,7 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
+        side_group = dist.new_group(backend="gloo")   # host-side barriers of the side legs
 
     import ipls
     P, L, K = CONFIGS[args.config]
@@ -676,6 +864,8 @@ def main():
                 return fn(*a, **kw)
             except Exception as e:   # noqa: BLE001
                 return {"error": f"{type(e).__name__}: {e}"}
+        if world == 1 and not args.be:
+            out["publish"] = side(publish_leg, ipls, torch, agg, stream, L, verify=not args.no_verify)
         if world == 1 and not args.be and not args.no_per_arrival:
             out["per_arrival"] = side(per_arrival_leg, ipls, torch, agg, rows, P, L, K, stream, not args.no_verify)
         if world == 1 and not args.no_e2e:
@@ -697,7 +887,7 @@ def main():
     dog = None
     printed = []
     stage = ["replica_exchange"]
-    if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg):
+    if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg and args.no_multi_leg):
         # the multi-rank side legs are extra measurements: a watchdog makes sure
         # a stuck exchange (or a teardown stuck behind a peer that failed in
         # it) can never cost the main line -- every rank exits
@@ -730,6 +920,31 @@ def main():
                 sl = {"error": f"{type(e).__name__}: {e}"}
             if out is not None:
                 out["strong_scaling_D"] = sl
+        if not args.no_multi_leg:
+            # rank 0 drives every GPU through ONE C-ABI handle (what a JVM would
+            # do); the other ranks wait on a host-side (gloo) barrier, so no
+            # spinning collective kernel shares their GPUs with the leg
+            stage[0] = "c_abi_multi_gpu"
+            if "arena" in locals():
+                del arena, rows
+            torch.cuda.empty_cache()
+            devs = [0] * world if args.dist_backend == "gloo" else list(range(world))
+            if rank == 0:
+                P_m, L_m, K_m = CONFIGS["C"]
+                try:
+                    ml = c_abi_multi_gpu(ipls, torch, devs, P_m, L_m, K_m, verify=not args.no_verify)
+                except Exception as e:               # reported, never fatal to the main line
+                    ml = {"error": f"{type(e).__name__}: {e}"}
+                out["c_abi_multi_gpu"] = ml
+            dist.barrier(group=side_group)
+    if world == 1 and args.multi_rehearsal and out is not None:
+        if "arena" in locals():
+            del arena, rows
+        torch.cuda.empty_cache()
+        P_m, L_m, K_m = CONFIGS["C"]
+        out["c_abi_multi_gpu"] = side(c_abi_multi_gpu, ipls, torch, [local, local], P_m // 2, L_m, K_m,
+                                      verify=not args.no_verify)
+        out["c_abi_multi_gpu"]["note"] = "rehearsal: two shards of one GPU (same code path, no xGMI)"
     if out is not None:
         printed.append(True)
         print(json.dumps(out), flush=True)

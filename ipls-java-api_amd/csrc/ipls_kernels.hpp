@@ -882,10 +882,18 @@ __device__ __forceinline__ unsigned frame_byte(const FrameEnc& f, const unsigned
 __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, const unsigned long long* __restrict__ src,
                                                                unsigned char* __restrict__ out, int64_t groups,
                                                                int64_t text_len) {
+  // Each lane's 32 chars go through LDS so that every wave then stores its
+  // 2 KiB of text as two contiguous 1 KiB rows (lane-strided 16-B stores
+  // would leave every 128-B line half written per instruction).
+  __shared__ u4w stage[2 * kBlock];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  u4w* ws = stage + 128 * wv;
   const int64_t F = 14 + 8 * f.n + f.origin_len;   // frame bytes
-  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += (int64_t)gridDim.x * kBlock) {
+  for (int64_t g0 = (int64_t)blockIdx.x * kBlock; g0 < groups; g0 += (int64_t)gridDim.x * kBlock) {
+    const int64_t g = g0 + threadIdx.x;
     const int64_t b0 = 24 * g;
-    if (g >= 1 && b0 + 24 <= 14 + 8 * f.n && src) {
+    u4w c0 = {0u, 0u, 0u, 0u}, c1 = {0u, 0u, 0u, 0u};
+    if (g < groups && g >= 1 && b0 + 24 <= 14 + 8 * f.n && src) {
       const unsigned long long* s = src + (3 * g - 2);
       const unsigned long long v0 = ld8(s), v1 = ld8(s + 1), v2 = ld8(s + 2), v3 = ld8(s + 3);
       // big-endian words of the 32 payload bytes, then the window's 6 (2 bytes in)
@@ -897,7 +905,6 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
       const unsigned long long X0 = ((unsigned long long)O[0] << 32) | O[1];
       const unsigned long long X1 = ((unsigned long long)O[2] << 32) | O[3];
       const unsigned long long X2 = ((unsigned long long)O[4] << 32) | O[5];
-      u4w c0, c1;
       c0.x = b64url_quad((unsigned)(X0 >> 40) & 0xFFFFFF);
       c0.y = b64url_quad((unsigned)(X0 >> 16) & 0xFFFFFF);
       c0.z = b64url_quad((unsigned)((X0 << 8) | (X1 >> 56)) & 0xFFFFFF);
@@ -906,29 +913,41 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
       c1.y = b64url_quad((unsigned)((X1 << 16) | (X2 >> 48)) & 0xFFFFFF);
       c1.z = b64url_quad((unsigned)(X2 >> 24) & 0xFFFFFF);
       c1.w = b64url_quad((unsigned)X2 & 0xFFFFFF);
-      *(IPLS_GLOBAL u4w*)(out + 32 * g) = c0;
-      *(IPLS_GLOBAL u4w*)(out + 32 * g + 16) = c1;
-      continue;
+    } else if (g < groups) {
+      // header / tail lanes: byte by byte, '=' padding on the last unit
+      unsigned q8[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      for (int u = 0; u < 8; ++u) {
+        const int64_t j = b0 + 3 * u;
+        if (j >= F) break;
+        const int nb = F - j >= 3 ? 3 : (int)(F - j);
+        unsigned v = frame_byte(f, src, j) << 16;
+        if (nb > 1) v |= frame_byte(f, src, j + 1) << 8;
+        if (nb > 2) v |= frame_byte(f, src, j + 2);
+        unsigned q = b64url_quad(v);
+        if (nb < 3) q = (q & 0x00FFFFFFu) | ((unsigned)'=' << 24);
+        if (nb < 2) q = (q & 0xFF00FFFFu) | ((unsigned)'=' << 16);
+        q8[u] = q;
+      }
+      c0 = u4w{q8[0], q8[1], q8[2], q8[3]};
+      c1 = u4w{q8[4], q8[5], q8[6], q8[7]};
     }
-    // header / tail lanes: byte by byte, '=' padding on the last unit
-    for (int u = 0; u < 8; ++u) {
-      const int64_t j = b0 + 3 * u;
-      if (j >= F) break;
-      const int nb = F - j >= 3 ? 3 : (int)(F - j);
-      unsigned v = frame_byte(f, src, j) << 16;
-      if (nb > 1) v |= frame_byte(f, src, j + 1) << 8;
-      if (nb > 2) v |= frame_byte(f, src, j + 2);
-      unsigned q = b64url_quad(v);
-      if (nb < 3) q = (q & 0x00FFFFFFu) | ((unsigned)'=' << 24);
-      if (nb < 2) q = (q & 0xFF00FFFFu) | ((unsigned)'=' << 16);
-      unsigned char* o = out + 32 * g + 4 * u;
-      o[0] = (unsigned char)q;
-      o[1] = (unsigned char)(q >> 8);
-      o[2] = (unsigned char)(q >> 16);
-      o[3] = (unsigned char)(q >> 24);
+    ws[2 * lane] = c0;
+    ws[2 * lane + 1] = c1;
+    __syncthreads();
+    const int64_t wbase = 32 * (g0 + 64 * wv);   // this wave's 2 KiB of text
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u4w v = ws[64 * h + lane];
+      const int64_t o = wbase + 1024 * h + 16 * lane;
+      if (o + 16 <= text_len) {
+        __builtin_nontemporal_store(v, (IPLS_GLOBAL u4w*)(out + o));
+      } else if (o < text_len) {   // the text's last partial 16 B
+        const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+        for (int64_t c = 0; o + c < text_len; ++c) out[o + c] = (unsigned char)(w4[c >> 2] >> (8 * (c & 3)));
+      }
     }
+    __syncthreads();   // the stage is rewritten by the next iteration
   }
-  (void)text_len;
 }
 
 // ---------------------------------------------------------------------------

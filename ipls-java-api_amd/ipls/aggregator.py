@@ -519,11 +519,16 @@ class Aggregator:
         text (MyIPFSClass.java:990-1016; IPLS.java:1429-1430 publishes AGG with
         a = iteration, b = workers + 1, pid 3), encoded on the GPU.  Returns the
         text bytes, or its length when ``out`` is a DeviceBuffer/int address
-        (device text, stream-ordered)."""
+        (device text, stream-ordered) or a PinnedBuffer (host text)."""
         o = np.frombuffer(bytes(origin), dtype=np.uint8)
         op = o.ctypes.data if o.size else None
         n = self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op, o.size,
                                                          None, 0, N.HOST_TEXT))
+        if isinstance(out, PinnedBuffer):   # host text into pinned memory: the D2H runs at the PCIe rate
+            if out.nbytes < n:
+                raise ValueError(f"publish text needs {n} bytes")
+            return self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op,
+                                                                o.size, out.ptr, n, N.HOST_TEXT))
         if out is not None:
             ptr = out.ptr if isinstance(out, DeviceBuffer) else int(out)
             return self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op,

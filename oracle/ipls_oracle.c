@@ -286,3 +286,54 @@ int ipls_oracle_updater_loop_parts(int n_parts, const uint8_t *const *be_bufs, i
     }
     return threads;
 }
+
+/* BE byte images (the update_file / `ipfs cat` format) of the synthetic
+ * buckets (p, j), p < n_parts, j < k: outs[p*k + j] receives 8*L bytes.
+ * Element values as ipls_oracle_synth_fill; OpenMP over the buckets. */
+void ipls_oracle_synth_be_buckets(uint8_t *const *outs, int n_parts, int k, int64_t L, uint64_t seed) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int b = 0; b < n_parts * k; b++) {
+        const int p = b / k, j = b % k;
+        uint8_t *o = outs[b];
+        for (int64_t i = 0; i < L; i++) {
+            const double x = (i == L - 1) ? 1.0 : ipls_oracle_synth_value(seed, p, j, i);
+            uint64_t u;
+            memcpy(&u, &x, 8);
+            for (int c = 0; c < 8; c++) o[8 * i + c] = (uint8_t)(u >> (56 - 8 * c));
+        }
+    }
+}
+
+/* CPU baseline, N threads: n_parts partitions, each with
+ * its OWN k buckets (be_bufs[p*k + j]), each folded by one thread exactly as
+ * the single Updater thread folds (decode into a reused buffer, then
+ * Agg[i] = Agg[i] + g[i]; Updater.java:162-187, 115-117), `passes` times.
+ * threads > 0 sets the team size.  Returns the threads used; agg0 (nullable)
+ * receives partition 0's sum. */
+int ipls_oracle_updater_loop_partitions(int n_parts, const uint8_t *const *be_bufs, int k, int64_t L, int passes,
+                                        int threads, double *agg0) {
+    int used = 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+    {
+#ifdef _OPENMP
+#pragma omp single
+        used = omp_get_num_threads();
+#endif
+        double *agg = (double *)malloc((size_t)L * sizeof(double));
+        double *scratch = (double *)malloc((size_t)L * sizeof(double));
+        for (int r = 0; r < passes; r++) {
+#pragma omp for schedule(dynamic, 1)
+            for (int q = 0; q < n_parts; q++) {
+                memset(agg, 0, (size_t)L * sizeof(double));
+                ipls_oracle_updater_loop(agg, be_bufs + (size_t)q * k, k, L, scratch);
+                if (q == 0 && r == 0 && agg0) memcpy(agg0, agg, (size_t)L * sizeof(double));
+            }
+        }
+        free(scratch);
+        free(agg);
+    }
+    return used;
+}

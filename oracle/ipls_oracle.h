@@ -118,6 +118,11 @@ void ipls_oracle_updater_loop(double *agg, const uint8_t *const *be_bufs, int k,
 /* N-thread, partition-parallel variant (OpenMP); returns threads used. */
 int ipls_oracle_updater_loop_parts(int n_parts, const uint8_t *const *be_bufs, int k, int64_t L,
                                    double *agg0);
+/* BE images of the synthetic buckets (p, j) for p < n_parts, j < k. */
+void ipls_oracle_synth_be_buckets(uint8_t *const *outs, int n_parts, int k, int64_t L, uint64_t seed);
+/* N-thread baseline over n_parts partitions with their own k buckets each. */
+int ipls_oracle_updater_loop_partitions(int n_parts, const uint8_t *const *be_bufs, int k, int64_t L, int passes,
+                                        int threads, double *agg0);
 
 #ifdef __cplusplus
 }

@@ -389,6 +389,10 @@ def c_oracle():
         lib.ipls_oracle_updater_loop.argtypes = [D, ctypes.POINTER(U8), ctypes.c_int, i64, D]
         lib.ipls_oracle_updater_loop_parts.restype = ctypes.c_int
         lib.ipls_oracle_updater_loop_parts.argtypes = [ctypes.c_int, ctypes.POINTER(U8), ctypes.c_int, i64, D]
+        lib.ipls_oracle_synth_be_buckets.argtypes = [ctypes.POINTER(U8), ctypes.c_int, ctypes.c_int, i64, u64]
+        lib.ipls_oracle_updater_loop_partitions.restype = ctypes.c_int
+        lib.ipls_oracle_updater_loop_partitions.argtypes = [ctypes.c_int, ctypes.POINTER(U8), ctypes.c_int, i64,
+                                                            ctypes.c_int, ctypes.c_int, D]
         _C = lib
     return _C
 
@@ -456,6 +460,29 @@ def c_updater_loop_parts(be_bufs, L: int, n_parts: int):
     agg0 = np.zeros(L)
     arr = (U8 * len(be_bufs))(*[b.ctypes.data_as(U8) for b in be_bufs])
     t = lib.ipls_oracle_updater_loop_parts(n_parts, arr, len(be_bufs), L, _dp(agg0))
+    return agg0, t
+
+
+def c_synth_be_buckets(n_parts: int, k: int, L: int, seed: int = SEED) -> list[np.ndarray]:
+    """BE byte images of the synthetic buckets (p, j), p < n_parts, j < k
+    (partition-major), generated in C with OpenMP."""
+    U8 = ctypes.POINTER(ctypes.c_uint8)
+    bufs = [np.empty(8 * L, dtype=np.uint8) for _ in range(n_parts * k)]
+    arr = (U8 * len(bufs))(*[b.ctypes.data_as(U8) for b in bufs])
+    c_oracle().ipls_oracle_synth_be_buckets(arr, n_parts, k, L, seed)
+    return bufs
+
+
+def c_updater_loop_partitions(be_bufs, n_parts: int, k: int, L: int, passes: int, threads: int = 0):
+    """CPU baseline, N threads: n_parts partitions, each with its own k BE
+    buckets (be_bufs partition-major), one thread per partition running the
+    single-thread Updater loop, `passes` times.  Returns (partition 0 sum,
+    threads used)."""
+    lib = c_oracle()
+    U8 = ctypes.POINTER(ctypes.c_uint8)
+    agg0 = np.zeros(L)
+    arr = (U8 * len(be_bufs))(*[b.ctypes.data_as(U8) for b in be_bufs])
+    t = lib.ipls_oracle_updater_loop_partitions(n_parts, arr, k, L, passes, threads, _dp(agg0))
     return agg0, t
 
 
