@@ -9,8 +9,9 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1
-  echo "pytest rc=$?" >> $O/pytest_gpu.log
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
+  case $rc in 124|134|137|139) exit 10;; esac
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 11
 fi
 timeout -k 10 400 python bench.py "$@" > $O/bench.json 2> $O/bench.err || exit 12
