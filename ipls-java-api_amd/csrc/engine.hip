@@ -2214,7 +2214,7 @@ int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_
     dst = (unsigned char*)h->d_scratch;
   }
   const int64_t groups = (F + 23) / 24;
-  hipLaunchKernelGGL(k_b64url_encode_frame, dim3(std::max(1u, std::min<unsigned>(blocks_for(groups, kBlock), 8192))),
+  hipLaunchKernelGGL(k_b64url_encode_frame, dim3(std::max(1u, std::min<unsigned>(blocks_for(groups, kBlock), 16384))),
                      dim3(kBlock), 0, h->stream, fe, src, dst, groups, T);
   HIP_TRY(h, hipGetLastError());
   if (out_kind == IPLS_DEV_TEXT) {

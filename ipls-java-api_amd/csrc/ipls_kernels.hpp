@@ -879,18 +879,35 @@ __device__ __forceinline__ unsigned frame_byte(const FrameEnc& f, const unsigned
   return f.origin[q - 8 * f.n];
 }
 
+// Interior chars come from a 64-byte LDS table, one ds_read_u8 per char: the
+// branchy b64url_char mapping made the kernel VALU-bound (~400 integer ops
+// per lane for 24 bytes; 30.4 us for a 4M-double partition against 15.8 us
+// for a copy of the same bytes).  With the table: 18-20 us.  A 4-chars-per-
+// dword SWAR map (v_perm offsets) and staging the wave's input window through
+// LDS with coalesced 16-B loads were both slower (tools/publish_sweep.hip,
+// profiles/r02/publish_sweep.txt).
+__device__ __forceinline__ unsigned b64url_quad_lut(const unsigned char* tab, unsigned v) {
+  return (unsigned)tab[(v >> 18) & 63] | ((unsigned)tab[(v >> 12) & 63] << 8) | ((unsigned)tab[(v >> 6) & 63] << 16) |
+         ((unsigned)tab[v & 63] << 24);
+}
+
 __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, const unsigned long long* __restrict__ src,
                                                                unsigned char* __restrict__ out, int64_t groups,
                                                                int64_t text_len) {
-  // Each lane's 32 chars go through LDS so that every wave then stores its
-  // 2 KiB of text as two contiguous 1 KiB rows (lane-strided 16-B stores
-  // would leave every 128-B line half written per instruction).
+  // Each lane's 32 chars go through a wave-private LDS row so that every wave
+  // then stores its 2 KiB of text as two contiguous 1 KiB rows (lane-strided
+  // 16-B stores would leave every 128-B line half written per instruction).
+  // LDS ops of one wave complete in order: a compiler barrier suffices.
   __shared__ u4w stage[2 * kBlock];
+  __shared__ unsigned char tab[64];
+  if (threadIdx.x < 64) tab[threadIdx.x] = (unsigned char)b64url_char(threadIdx.x);
+  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   u4w* ws = stage + 128 * wv;
   const int64_t F = 14 + 8 * f.n + f.origin_len;   // frame bytes
   for (int64_t g0 = (int64_t)blockIdx.x * kBlock; g0 < groups; g0 += (int64_t)gridDim.x * kBlock) {
-    const int64_t g = g0 + threadIdx.x;
+    const int64_t gw = g0 + 64 * wv;                // this wave's first group
+    const int64_t g = gw + lane;
     const int64_t b0 = 24 * g;
     u4w c0 = {0u, 0u, 0u, 0u}, c1 = {0u, 0u, 0u, 0u};
     if (g < groups && g >= 1 && b0 + 24 <= 14 + 8 * f.n && src) {
@@ -905,14 +922,14 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
       const unsigned long long X0 = ((unsigned long long)O[0] << 32) | O[1];
       const unsigned long long X1 = ((unsigned long long)O[2] << 32) | O[3];
       const unsigned long long X2 = ((unsigned long long)O[4] << 32) | O[5];
-      c0.x = b64url_quad((unsigned)(X0 >> 40) & 0xFFFFFF);
-      c0.y = b64url_quad((unsigned)(X0 >> 16) & 0xFFFFFF);
-      c0.z = b64url_quad((unsigned)((X0 << 8) | (X1 >> 56)) & 0xFFFFFF);
-      c0.w = b64url_quad((unsigned)(X1 >> 32) & 0xFFFFFF);
-      c1.x = b64url_quad((unsigned)(X1 >> 8) & 0xFFFFFF);
-      c1.y = b64url_quad((unsigned)((X1 << 16) | (X2 >> 48)) & 0xFFFFFF);
-      c1.z = b64url_quad((unsigned)(X2 >> 24) & 0xFFFFFF);
-      c1.w = b64url_quad((unsigned)X2 & 0xFFFFFF);
+      c0.x = b64url_quad_lut(tab, (unsigned)(X0 >> 40) & 0xFFFFFF);
+      c0.y = b64url_quad_lut(tab, (unsigned)(X0 >> 16) & 0xFFFFFF);
+      c0.z = b64url_quad_lut(tab, (unsigned)((X0 << 8) | (X1 >> 56)) & 0xFFFFFF);
+      c0.w = b64url_quad_lut(tab, (unsigned)(X1 >> 32) & 0xFFFFFF);
+      c1.x = b64url_quad_lut(tab, (unsigned)(X1 >> 8) & 0xFFFFFF);
+      c1.y = b64url_quad_lut(tab, (unsigned)((X1 << 16) | (X2 >> 48)) & 0xFFFFFF);
+      c1.z = b64url_quad_lut(tab, (unsigned)(X2 >> 24) & 0xFFFFFF);
+      c1.w = b64url_quad_lut(tab, (unsigned)X2 & 0xFFFFFF);
     } else if (g < groups) {
       // header / tail lanes: byte by byte, '=' padding on the last unit
       unsigned q8[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -933,8 +950,8 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
     }
     ws[2 * lane] = c0;
     ws[2 * lane + 1] = c1;
-    __syncthreads();
-    const int64_t wbase = 32 * (g0 + 64 * wv);   // this wave's 2 KiB of text
+    __builtin_amdgcn_wave_barrier();
+    const int64_t wbase = 32 * gw;                  // this wave's 2 KiB of text
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const u4w v = ws[64 * h + lane];
@@ -946,7 +963,7 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
         for (int64_t c = 0; o + c < text_len; ++c) out[o + c] = (unsigned char)(w4[c >> 2] >> (8 * (c & 3)));
       }
     }
-    __syncthreads();   // the stage is rewritten by the next iteration
+    __builtin_amdgcn_wave_barrier();   // the row is rewritten by the next iteration
   }
 }
 

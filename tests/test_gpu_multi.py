@@ -231,7 +231,8 @@ def test_sharded_ingest_indirect_async_and_replicas(ipls, O):
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("L,origin", [(7, b""), (7, b"Q"), (7, b"Qm"),
                                       (100_000, b"QmPeerOrigin46charsxxxxxxxxxxxxxxxxxxxxxxxxxxx"),
-                                      (1_048_581, b"QmY"), (1_048_580, b"QmY")])
+                                      (1_048_581, b"QmY"), (1_048_580, b"QmY"),
+                                      (13_000_001, b"QmZ")])   # > 16384 blocks: grid-stride
 def test_publish_partial_matches_marshall_packet(ipls, O, L, origin):
     """ipls_agg_publish_partial = Base64.getUrlEncoder().encodeToString(frame)
     for the frame Marshall_Packet builds from Aggregated_Gradients[p]
