@@ -222,6 +222,58 @@ def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dic
             "pcie_ceiling": "~56 GB/s per direction measured (tools/h2d_bench.hip, profiles/r01/h2d_bench.txt)"}
 
 
+def e2e_multi(ipls, torch, dist, group, rank, world, local, L, K, reps, verify) -> dict:
+    """Config F's end-to-end leg at N > 1: every rank at once folds K peers'
+    big-endian byte buckets that start in pinned host memory (as pulled from
+    IPFS; zero-copy reads over its own PCIe link, one launch) and writes the
+    BE sum bytes back to pinned host memory (commit_update's update_file),
+    between host-side barriers.  Aggregate rate = all ranks' algorithmic
+    bytes / the slowest rank's time (the host's memory system and every
+    GPU's PCIe link are loaded together)."""
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L, device=local)
+    pinned = []
+    tmp = torch.empty(8 * L, dtype=torch.uint8, device="cuda")
+    for k in range(K):
+        ipls.synth_fill(ipls.DeviceBuffer(int(tmp.data_ptr()), L, big_endian=True), rank, k, ipls.SEED)
+        pb = ipls.PinnedBuffer(8 * L)
+        pb.view()[:] = tmp.cpu().numpy()
+        pinned.append(pb)
+    del tmp
+    sum_pinned = ipls.PinnedBuffer(8 * L)
+    row = [[ipls.DeviceBuffer(pb.ptr, L, big_endian=True) for pb in pinned]]
+
+    def one_round():
+        agg.reduce_batch(0, row, start_mode=ipls.START_ZERO, big_endian=True)
+        agg.AggregatePartition(0, sum_out=sum_pinned)
+
+    one_round()
+    dist.barrier(group=group)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one_round()
+    dt = time.perf_counter() - t0
+    times = [None] * world
+    dist.all_gather_object(times, dt, group=group)
+    ok = None
+    if verify and rank == 0:
+        from oracle import oracle as O   # checker only
+        ok = ipls.checksum_dev(ipls.DeviceBuffer(sum_pinned.ptr, L, big_endian=True)) == O.c_synth_sum_checksum(L, 0, K)
+    agg.close()
+    for pb in pinned:
+        pb.close()
+    sum_pinned.close()
+    per_rank = reps * (K + 1) * L * 8
+    return {"workload": f"F slice per GPU: 1 partition x {K} peers x {L} doubles of BE host bytes per rank, "
+                        f"all {world} ranks at once",
+            "GBps_total": round(world * per_rank / max(times) / 1e9, 2),
+            "GBps_per_gpu_min": round(per_rank / max(times) / 1e9, 2),
+            "GBps_per_gpu_max": round(per_rank / min(times) / 1e9, 2),
+            "verified_checksum_rank0": ok,
+            "note": "pinned host BE buckets read zero-copy by one launch per round + AggregatePartition with the BE "
+                    "sum written to pinned host memory; algorithmic bytes (K+1)*L*8 per rank per round; "
+                    "PCIe Gen5 x16 per GPU ~56 GB/s per direction"}
+
+
 def replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, reps, verify, backend="nccl") -> dict:
     """Config E (N > 1): a partition's contributors span GPUs.  Every rank owns
     its P partitions and folds their first K/2 peers; it is also the replica
@@ -887,7 +939,8 @@ def main():
     dog = None
     printed = []
     stage = ["replica_exchange"]
-    if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg and args.no_multi_leg):
+    if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg and args.no_multi_leg
+                                          and args.no_e2e):
         # the multi-rank side legs are extra measurements: a watchdog makes sure
         # a stuck exchange (or a teardown stuck behind a peer that failed in
         # it) can never cost the main line -- every rank exits
@@ -920,6 +973,19 @@ def main():
                 sl = {"error": f"{type(e).__name__}: {e}"}
             if out is not None:
                 out["strong_scaling_D"] = sl
+        if not args.no_e2e:
+            stage[0] = "host_inclusive_multi"
+            if "arena" in locals():
+                del arena, rows
+            torch.cuda.empty_cache()
+            _, LF, KF = CONFIGS["F"]
+            try:
+                el = e2e_multi(ipls, torch, dist, side_group, rank, world, local, LF // 4, KF, args.e2e_reps,
+                               not args.no_verify)
+            except Exception as e:                   # reported, never fatal to the main line
+                el = {"error": f"{type(e).__name__}: {e}"}
+            if out is not None:
+                out["host_inclusive_multi"] = el
         if not args.no_multi_leg:
             # rank 0 drives every GPU through ONE C-ABI handle (what a JVM would
             # do); the other ranks wait on a host-side (gloo) barrier, so no
