@@ -283,3 +283,52 @@ def test_publish_partial_rejects_bad_arguments(ipls):
     assert lib.ipls_agg_publish_partial(agg.handle, 0, N.TGT_AGG, 0, 0, 3, None, 0, out, need,
                                         N.HOST_F64) == N.IPLS_E_INVAL
     agg.close()
+
+
+# ---------------------------------------------------------------------------
+# Full-size BASELINE geometries through the multi-device handle
+# ---------------------------------------------------------------------------
+def test_config_e_geometry_full_size(ipls, O):
+    """Config E: -pa 64 sharded 16 per GPU over a
+    four-entry device list ([0, 0, 0, 0] on this one-GPU box), 4M doubles,
+    K = 32.  Round 1 (reduce_batch over all 64 partitions in one call, the
+    launch split over the four shards): per-partition checksums against the
+    C oracle at every shard boundary.  Round 2 (the replica exchange of
+    config E, IPLS.java:1402-1468): the owner folds peers [0, 16), the next
+    shard -- a replica aggregator of the same partitions -- folds peers
+    [16, 32) into its partials, the combine adds them to REP over the
+    cross-shard path, and W = AGG + (+0.0 + R) matches the oracle's replica
+    checksum (Updater.java:40-44, IPLS.java:1256)."""
+    P, L, K, G = 64, 4_194_304, 32, 4
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0] * G)
+    assert ipls.shard_plan(P, G) == [p // 16 for p in range(P)]
+    t, rows = dev_buckets(ipls, P, L, K)
+    check = [0, 15, 16, 31, 32, 47, 48, 63]
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    for p in check:
+        assert agg.checksum(p) == O.c_synth_sum_checksum(L, p, K), p
+    kh = K // 2
+    agg.reduce_batch(0, [r[:kh] for r in rows], start_mode=ipls.START_ZERO)
+    for s in range(G):                        # shard s replicates shard (s-1)'s partitions
+        o = (s - 1) % G
+        agg.reduce_partial(s, 16 * o, [r[kh:] for r in rows[16 * o:16 * o + 16]])
+    assert agg.combine_partials() == P
+    agg.AggregatePartition(ipls.ALL_PARTITIONS)
+    for p in check:
+        assert agg.checksum(p, ipls.TGT_WEIGHTS) == O.c_synth_replica_checksum(L, p, K, kh), p
+    agg.close()
+    del t
+
+
+def test_config_f_slice_full_size(ipls, O):
+    """One GPU's slice of config F: 16 partitions x 8M doubles x 64 peers
+    (69.8 GB of buckets resident), one reduce_batch, checksums of the first,
+    a middle and the last partition against the C oracle."""
+    P, L, K = 16, 8_388_608, 64
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    t, rows = dev_buckets(ipls, P, L, K)
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    for p in (0, 7, 15):
+        assert agg.checksum(p) == O.c_synth_sum_checksum(L, p, K), p
+    agg.close()
+    del t
