@@ -694,10 +694,49 @@ def publish_leg(ipls, torch, agg, stream, L: int, reps: int = 10, verify: bool =
         ok = (host == O.java_b64url_encode(O.frame_encode(agg.read(0, ipls.TGT_WEIGHTS), 7, 33, 3, origin)) and
               bytes(buf[:text_len].cpu().numpy()) == host)
     del buf
+    # a round's publish loop over all P partitions (IPLS.java:1423-1431): P
+    # single calls vs one ipls_agg_publish_partials launch, device text
+    P = agg.n_partitions
+    parts, bs = list(range(P)), [33] * P
+    total = 0
+    for _ in range(P):
+        total = (total + 63) // 64 * 64 + text_len
+    big = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    bptr = int(big.data_ptr())
+    lens, offs = agg.publish_partials(parts, 7, bs, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr)
+    agg.sync()
+    ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t_loop, t_batch = [], []
+    for _ in range(reps):
+        ev2[0].record(stream)
+        for p in parts:
+            agg.publish_partial(p, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr + offs[p])
+        ev2[1].record(stream)
+        agg.publish_partials(parts, 7, bs, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr)
+        ev2[2].record(stream)
+        agg.sync()
+        t_loop.append(ev2[0].elapsed_time(ev2[1]))
+        t_batch.append(ev2[1].elapsed_time(ev2[2]))
+    ok_all = None
+    if verify:
+        from oracle import oracle as O   # checker only
+        host_all = big.cpu().numpy().tobytes()
+        ok_all = all(host_all[offs[p]:offs[p] + lens[p]] ==
+                     O.java_b64url_encode(O.frame_encode(agg.read(p, ipls.TGT_WEIGHTS), 7, 33, 3, origin))
+                     for p in (0, P - 1))
+    del big
+    ms_loop, ms_batch = float(np.median(t_loop)), float(np.median(t_batch))
+    all_bytes = P * nbytes
+    all_parts = {"partitions": P, "loop_ms": round(ms_loop, 4), "batch_ms": round(ms_batch, 4),
+                 "batch_GBps": round(all_bytes / ms_batch / 1e6, 1),
+                 "batch_frac": round(all_bytes / ms_batch / 1e6 / HBM_PEAK_GBS, 4),
+                 "verified_first_last_vs_java_encoder": ok_all,
+                 "note": "the round's publish of every partition: P ipls_agg_publish_partial calls vs one "
+                         "ipls_agg_publish_partials launch (texts at 64-B aligned offsets), HIP events"}
     return {"partition_doubles": L, "text_bytes": text_len, "device_ms": round(ms, 4),
             "device_GBps": round(nbytes / ms / 1e6, 1), "device_frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4),
             "host_text_ms": round(dt * 1e3, 3), "host_text_GBps": round(text_len / dt / 1e9, 2),
-            "verified_vs_java_encoder": ok,
+            "verified_vs_java_encoder": ok, "all_partitions": all_parts,
             "note": "Marshall_Packet(W[0], origin, 7, 33, pid 3) -> base64url with padding; device_GBps counts "
                     "8L read + the text written; host_text: the same call with the text landing in pinned host "
                     "memory (C-ABI call wall time, D2H included)"}

@@ -377,6 +377,18 @@ int64_t ipls_agg_publish_partial(ipls_agg *h, int p, int target, int32_t a, int3
                                  const uint8_t *origin, int32_t origin_len, void *out, int64_t out_cap,
                                  int out_kind);
 
+/* The same for several partitions in one launch per GPU: the publish loop
+ * over Auth_List (IPLS.java:1423-1431), text i = Marshall_Packet(target[
+ * parts[i]], origin, a, b[i], pid) base64url-encoded.  Text i lands at
+ * out + offs[i] (offs are 64-byte multiples, texts in list order), lens[i]
+ * bytes.  lens/offs (n_parts entries, either may be NULL) are filled even
+ * when out == NULL.  Returns the bytes the buffer needs (offs[n-1] +
+ * lens[n-1]); b and origin may be NULL when out is (origin_len still counts).  IPLS_DEV_TEXT with partitions on several GPUs: out must be
+ * memory every owner device can write (its own or a peer's). */
+int64_t ipls_agg_publish_partials(ipls_agg *h, const int32_t *parts, int n_parts, int target, int32_t a,
+                                  const int32_t *b, int16_t pid, const uint8_t *origin, int32_t origin_len,
+                                  void *out, int64_t out_cap, int out_kind, int64_t *lens, int64_t *offs);
+
 /* ---- observability ----
  * What the last fold launch of a handle (of p's shard for multi-GPU handles:
  * the shard of the last call) ran: the kernel, the tile shape chosen by the

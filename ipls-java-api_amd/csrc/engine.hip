@@ -2227,6 +2227,77 @@ int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_
   return T;
 }
 
+// Several partitions' publish texts in one launch (the loop over Auth_List,
+// IPLS.java:1423-1431): text i of local partition parts[i] (field b = b[i])
+// lands at out + offs[i], lens[i] bytes; offs are 64-byte multiples (the
+// front lays them out).  HOST_TEXT: one D2H per text after the launch.
+int64_t dev_publish_many(ipls_dev* h, int n, const int* parts, int target, int32_t a, const int32_t* b, int16_t pid,
+                         const uint8_t* origin, int32_t origin_len, void* out, const int64_t* offs,
+                         const int64_t* lens, int out_kind) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  IPLS_LOCK(h);
+  if (n <= 0) return IPLS_OK;
+  if (origin_len < 0 || (origin_len > 0 && !origin)) return fail(h, IPLS_E_INVAL, "bad origin");
+  if (out_kind != IPLS_HOST_TEXT && out_kind != IPLS_DEV_TEXT) return fail(h, IPLS_E_INVAL, "out_kind HOST_TEXT/DEV_TEXT");
+  for (int i = 0; i < n; ++i) {
+    if (int rc = check_part(h, parts[i])) return rc;
+    if (target_off(h, parts[i], target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  }
+  HIP_TRY(h, hipSetDevice(h->device));
+  const unsigned char* dorig = nullptr;
+  if (origin_len > 0) {
+    void* d = nullptr;
+    if (int rc = upload_table(h, origin, (size_t)origin_len, &d)) return rc;
+    dorig = (const unsigned char*)d;
+  }
+  // texts land straight in a 16-B aligned device buffer; else in the scratch
+  // buffer at the same offsets, then copied out
+  const bool direct = out_kind == IPLS_DEV_TEXT && !((uintptr_t)out & 15);
+  int64_t span = 0;
+  for (int i = 0; i < n; ++i) span = std::max(span, offs[i] + lens[i]);
+  int64_t lo = span;
+  for (int i = 0; i < n; ++i) lo = std::min(lo, offs[i]);
+  unsigned char* base = (unsigned char*)out;
+  if (!direct) {
+    if (int rc = ensure_scratch(h, (size_t)(span - lo) + 64)) return rc;
+    base = (unsigned char*)h->d_scratch - lo;
+  }
+  std::vector<FrameJob> jobs(n);
+  int64_t max_groups = 1;
+  for (int i = 0; i < n; ++i) {
+    const int p = parts[i];
+    FrameJob& j = jobs[i];
+    j = FrameJob{};
+    const int64_t L = h->len[p];
+    const uint32_t hv[3] = {(uint32_t)L, (uint32_t)a, (uint32_t)b[i]};
+    j.f.hdr[0] = (unsigned char)((uint16_t)pid >> 8);   // putShort(0, pid)
+    j.f.hdr[1] = (unsigned char)pid;
+    for (int f = 0; f < 3; ++f)                         // putInt(2 | 6 | 10, ...)
+      for (int k = 0; k < 4; ++k) j.f.hdr[2 + 4 * f + k] = (unsigned char)(hv[f] >> (24 - 8 * k));
+    j.f.n = L;
+    j.f.origin_len = origin_len;
+    j.f.origin = dorig;
+    uint8_t* zf = zero_flag(h, p, target);
+    j.src = (zf && *zf) ? nullptr : (const unsigned long long*)(h->arena + target_off(h, p, target));
+    j.out = base + offs[i];
+    j.groups = (14 + 8 * L + origin_len + 23) / 24;
+    j.text_len = lens[i];
+    max_groups = std::max(max_groups, j.groups);
+  }
+  void* djobs = nullptr;
+  if (int rc = upload_table(h, jobs.data(), jobs.size() * sizeof(FrameJob), &djobs)) return rc;
+  const unsigned gx = std::max(1u, std::min<unsigned>(blocks_for(max_groups, kBlock), 16384));
+  hipLaunchKernelGGL(k_b64url_encode_frames, dim3(gx, (unsigned)n), dim3(kBlock), 0, h->stream,
+                     (const FrameJob*)djobs);
+  HIP_TRY(h, hipGetLastError());
+  if (direct) return IPLS_OK;                           // stream-ordered
+  const hipMemcpyKind kind = out_kind == IPLS_DEV_TEXT ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  for (int i = 0; i < n; ++i)
+    HIP_TRY(h, hipMemcpyAsync((unsigned char*)out + offs[i], base + offs[i], (size_t)lens[i], kind, h->stream));
+  if (out_kind == IPLS_HOST_TEXT) HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return IPLS_OK;
+}
+
 // ---- engine plumbing used by the multi-device front (ipls_agg.cpp) ----
 int dev_device(const ipls_dev* h) { return h ? h->device : -1; }
 

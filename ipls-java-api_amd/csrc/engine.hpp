@@ -62,5 +62,8 @@ int dev_checksum(ipls_dev* h, int p, int target, uint64_t* out);
 int64_t dev_commit_partial(ipls_dev* h, int p, int32_t workers, uint8_t* out, int64_t out_cap);
 int64_t dev_merge_files(ipls_dev* h, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
                         uint8_t* out, int64_t out_cap);
+int64_t dev_publish_many(ipls_dev* h, int n, const int* parts, int target, int32_t a, const int32_t* b, int16_t pid,
+                         const uint8_t* origin, int32_t origin_len, void* out, const int64_t* offs,
+                         const int64_t* lens, int out_kind);
 int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_t pid, const uint8_t* origin,
                     int32_t origin_len, void* out, int64_t out_cap, int out_kind);

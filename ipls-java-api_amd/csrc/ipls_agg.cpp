@@ -709,6 +709,61 @@ int64_t ipls_agg_publish_partial(ipls_agg* H, int p, int target, int32_t a, int3
   return fwd(H, s, dev_publish(H->sh[s], q, target, a, b, pid, origin, origin_len, out, out_cap, out_kind));
 }
 
+int64_t ipls_agg_publish_partials(ipls_agg* H, const int32_t* parts, int n_parts, int target, int32_t a,
+                                  const int32_t* b, int16_t pid, const uint8_t* origin, int32_t origin_len, void* out,
+                                  int64_t out_cap, int out_kind, int64_t* lens, int64_t* offs) {
+  if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
+  if (n_parts < 0 || (n_parts > 0 && (!parts || (out && !b)))) return ferr(H, IPLS_E_INVAL, "bad partition list");
+  if (origin_len < 0 || (out && origin_len > 0 && !origin)) return ferr(H, IPLS_E_INVAL, "bad origin");
+  if (out_kind != IPLS_HOST_TEXT && out_kind != IPLS_DEV_TEXT) return ferr(H, IPLS_E_INVAL, "out_kind HOST_TEXT/DEV_TEXT");
+  std::vector<int64_t> L(n_parts), O(n_parts);
+  int64_t total = 0;
+  for (int i = 0; i < n_parts; ++i) {
+    if (!part_ok(H, parts[i])) return range_err(H, parts[i]);
+    O[i] = (total + 63) / 64 * 64;                        // every text 64-B aligned
+    L[i] = ipls::pubsub::b64_enc_len(14 + 8 * H->len[parts[i]] + origin_len);
+    total = O[i] + L[i];
+  }
+  if (lens) std::copy(L.begin(), L.end(), lens);
+  if (offs) std::copy(O.begin(), O.end(), offs);
+  if (!out || n_parts == 0) return total;
+  if (out_cap < total) return ferr(H, IPLS_E_RANGE, "publish texts need %lld bytes", (long long)total);
+  // group by owner shard; each shard encodes its texts in one launch
+  std::vector<std::vector<int>> idx(H->S());
+  for (int i = 0; i < n_parts; ++i) idx[H->owner[parts[i]]].push_back(i);
+  for (int s = 0; s < H->S(); ++s) {
+    if (idx[s].empty()) continue;
+    if (out_kind == IPLS_DEV_TEXT) {
+      // the texts are written by shard s's device: out must be its memory or a peer's
+      hipPointerAttribute_t at{};
+      if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeDevice &&
+          at.device != H->devices[s]) {
+        int ok = 0;
+        for (int t = 0; t < H->S(); ++t)
+          if (H->devices[t] == at.device && H->peer[s][t]) ok = 1;
+        if (!ok)
+          return ferr(H, IPLS_E_DEVICE, "device %d cannot write the texts on device %d", H->devices[s], at.device);
+      }
+      (void)hipGetLastError();
+    }
+    std::vector<int> lp;
+    std::vector<int32_t> bb;
+    std::vector<int64_t> oo, ll;
+    for (int i : idx[s]) {
+      lp.push_back(parts[i] - H->lo[s]);
+      bb.push_back(b[i]);
+      oo.push_back(O[i]);
+      ll.push_back(L[i]);
+    }
+    H->last_shard = s;
+    if (int64_t rc = dev_publish_many(H->sh[s], (int)lp.size(), lp.data(), target, a, bb.data(), pid, origin,
+                                      origin_len, out, oo.data(), ll.data(), out_kind);
+        rc < 0)
+      return fwd(H, s, (int)rc);
+  }
+  return total;
+}
+
 // ---- replica slots across GPUs ----
 
 int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, const void* const* bufs, int k,

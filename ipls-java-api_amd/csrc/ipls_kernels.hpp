@@ -891,17 +891,15 @@ __device__ __forceinline__ unsigned b64url_quad_lut(const unsigned char* tab, un
          ((unsigned)tab[v & 63] << 24);
 }
 
-__global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, const unsigned long long* __restrict__ src,
-                                                               unsigned char* __restrict__ out, int64_t groups,
-                                                               int64_t text_len) {
+// One text: blocks [0, gridDim.x) of this job walk its groups grid-stride.
+// tab = the 64-char table in LDS, stage = 2 * kBlock 16-B rows of LDS.
+__device__ __forceinline__ void encode_frame_job(const FrameEnc& f, const unsigned long long* __restrict__ src,
+                                                 unsigned char* __restrict__ out, int64_t groups, int64_t text_len,
+                                                 const unsigned char* tab, u4w* stage) {
   // Each lane's 32 chars go through a wave-private LDS row so that every wave
   // then stores its 2 KiB of text as two contiguous 1 KiB rows (lane-strided
   // 16-B stores would leave every 128-B line half written per instruction).
   // LDS ops of one wave complete in order: a compiler barrier suffices.
-  __shared__ u4w stage[2 * kBlock];
-  __shared__ unsigned char tab[64];
-  if (threadIdx.x < 64) tab[threadIdx.x] = (unsigned char)b64url_char(threadIdx.x);
-  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   u4w* ws = stage + 128 * wv;
   const int64_t F = 14 + 8 * f.n + f.origin_len;   // frame bytes
@@ -965,6 +963,38 @@ __global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, cons
     }
     __builtin_amdgcn_wave_barrier();   // the row is rewritten by the next iteration
   }
+}
+
+__device__ __forceinline__ void init_b64url_table(unsigned char* tab) {
+  if (threadIdx.x < 64) tab[threadIdx.x] = (unsigned char)b64url_char(threadIdx.x);
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_b64url_encode_frame(FrameEnc f, const unsigned long long* __restrict__ src,
+                                                               unsigned char* __restrict__ out, int64_t groups,
+                                                               int64_t text_len) {
+  __shared__ u4w stage[2 * kBlock];
+  __shared__ unsigned char tab[64];
+  init_b64url_table(tab);
+  encode_frame_job(f, src, out, groups, text_len, tab, stage);
+}
+
+// Several partitions' texts in one launch (the publish loop over Auth_List,
+// IPLS.java:1423-1431): blockIdx.y = job.  Every text starts 16-B aligned.
+struct FrameJob {
+  FrameEnc f;
+  const unsigned long long* src;   // accumulator, or null = logically +0.0
+  unsigned char* out;
+  int64_t groups;
+  int64_t text_len;
+};
+
+__global__ __launch_bounds__(kBlock) void k_b64url_encode_frames(const FrameJob* __restrict__ jobs) {
+  __shared__ u4w stage[2 * kBlock];
+  __shared__ unsigned char tab[64];
+  init_b64url_table(tab);
+  const FrameJob& j = jobs[blockIdx.y];
+  encode_frame_job(j.f, j.src, j.out, j.groups, j.text_len, tab, stage);
 }
 
 // ---------------------------------------------------------------------------

@@ -129,6 +129,7 @@ SIGNATURES = {
     "ipls_agg_reduce_partial": (_i, [_vp, _i, _i, _i, _P(_vp), _i, _i, _i]),
     "ipls_agg_combine_partials": (_i, [_vp, _i, _i]),
     "ipls_agg_publish_partial": (_i64, [_vp, _i, _i, _i32, _i32, _i16, _vp, _i32, _vp, _i64, _i]),
+    "ipls_agg_publish_partials": (_i64, [_vp, _vp, _i, _i, _i32, _vp, _i16, _vp, _i32, _vp, _i64, _i, _vp, _vp]),
     "ipls_agg_last_launch": (_i, [_vp, _P(LaunchInfo)]),
 }
 

@@ -538,6 +538,41 @@ class Aggregator:
                                                      buf.ctypes.data, n, N.HOST_TEXT))
         return buf[:n].tobytes()
 
+    def publish_partials(self, partitions, a: int, b, *, pid: int = 3, origin: bytes = b"",
+                         target: int = N.TGT_AGG, out=None):
+        """The publish loop over Auth_List (IPLS.java:1423-1431) in one launch
+        per GPU: text i = Marshall_Packet(target[partitions[i]], origin, a,
+        b[i], pid) base64url-encoded.  Returns the list of texts (bytes), or,
+        when ``out`` is a device address / DeviceBuffer / PinnedBuffer, the
+        (lens, offs) of the texts written there (device: stream-ordered)."""
+        parts = np.ascontiguousarray(list(partitions), dtype=np.int32)
+        bb = np.ascontiguousarray(list(b), dtype=np.int32)
+        if bb.size != parts.size:
+            raise ValueError("one b value per partition")
+        o = np.frombuffer(bytes(origin), dtype=np.uint8)
+        op = o.ctypes.data if o.size else None
+        n = parts.size
+        lens = np.zeros(max(1, n), dtype=np.int64)
+        offs = np.zeros(max(1, n), dtype=np.int64)
+        total = self._chk(self._lib.ipls_agg_publish_partials(
+            self._h, parts.ctypes.data, n, target, a, bb.ctypes.data, pid, op, o.size, None, 0, N.HOST_TEXT,
+            lens.ctypes.data, offs.ctypes.data))
+        if out is not None:
+            if isinstance(out, PinnedBuffer):
+                ptr, cap, kind = out.ptr, out.nbytes, N.HOST_TEXT
+            else:
+                ptr = out.ptr if isinstance(out, DeviceBuffer) else int(out)
+                cap, kind = total, N.DEV_TEXT
+            self._chk(self._lib.ipls_agg_publish_partials(
+                self._h, parts.ctypes.data, n, target, a, bb.ctypes.data, pid, op, o.size, ptr, cap, kind,
+                None, None))
+            return lens[:n].tolist(), offs[:n].tolist()
+        buf = np.empty(max(1, total), dtype=np.uint8)
+        self._chk(self._lib.ipls_agg_publish_partials(
+            self._h, parts.ctypes.data, n, target, a, bb.ctypes.data, pid, op, o.size, buf.ctypes.data, total,
+            N.HOST_TEXT, None, None))
+        return [buf[offs[i]:offs[i] + lens[i]].tobytes() for i in range(n)]
+
     def last_launch(self) -> dict:
         """What the last fold launch ran (kernel, shape, lanes, vectors, SEQ code, map, grid)."""
         li = N.LaunchInfo()

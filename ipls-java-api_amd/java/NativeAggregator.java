@@ -202,6 +202,25 @@ public final class NativeAggregator implements AutoCloseable {
                           java.nio.charset.StandardCharsets.US_ASCII);
     }
 
+    /** The whole publish loop of a round (IPLS.java:1423-1431) in one launch per GPU:
+     *  text i = Marshall_Packet(Aggregated_Gradients[parts[i]], id, iteration,
+     *  workersPlusOne[i], 3) base64url-encoded. */
+    public String[] publishPartials(int[] parts, int iteration, int[] workersPlusOne, String originPeer) {
+        byte[] o = java.util.Arrays.copyOf(originPeer.getBytes(), originPeer.length());
+        long[] lens = new long[parts.length], offs = new long[parts.length];
+        long total = publishPartialsLayout(handle, parts, o.length, lens, offs);
+        ByteBuffer buf = ByteBuffer.allocateDirect((int) Math.max(1, total));
+        publishPartialsDirect(handle, parts, TGT_AGG, iteration, workersPlusOne, (short) 3, o, buf, 0, total);
+        String[] out = new String[parts.length];
+        for (int i = 0; i < parts.length; ++i) {
+            byte[] t = new byte[(int) lens[i]];
+            buf.position((int) offs[i]);
+            buf.get(t);
+            out[i] = new String(t, java.nio.charset.StandardCharsets.US_ASCII);
+        }
+        return out;
+    }
+
     /** Device-resident batches: n_parts x k device addresses, partition-major. */
     public void reduceBatch(int pFirst, int nParts, long[] devPtrs, int k, boolean bigEndian, int start, int target) {
         reduceBatchDevice(handle, pFirst, nParts, devPtrs, k, bigEndian ? 4 : 3, start, target);
@@ -231,6 +250,9 @@ public final class NativeAggregator implements AutoCloseable {
                                                    int kind, int start);
     private static native int combinePartials(long h, int pFirst, int nParts);
     private static native byte[] publishPartial(long h, int p, int target, int a, int b, short pid, byte[] origin);
+    private static native long publishPartialsLayout(long h, int[] parts, int originLen, long[] lens, long[] offs);
+    private static native void publishPartialsDirect(long h, int[] parts, int target, int a, int[] b, short pid,
+                                                     byte[] origin, ByteBuffer out, int pos, long cap);
     private static native void close(long h);
     private static native long partitionLen(long h, int p);
     private static native long partitionOffset(long h, int p);

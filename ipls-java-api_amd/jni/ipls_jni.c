@@ -554,3 +554,50 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_publishPartial(JNIEnv *env, j
     free(text);
     return res;
 }
+
+/* ipls_agg_publish_partials layout: total bytes; lens/offs of every text. */
+JNIEXPORT jlong JNICALL Java_NativeAggregator_publishPartialsLayout(JNIEnv *env, jclass c, jlong h, jintArray parts,
+                                                                    jint originLen, jlongArray lens, jlongArray offs) {
+    (void)c;
+    if (!parts) { throw_iae(env, "null partition list"); return -1; }
+    const jsize n = (*env)->GetArrayLength(env, parts);
+    if (!need_len(env, lens, n, "lens") || !need_len(env, offs, n, "offs")) return -1;
+    jint *pp = (*env)->GetIntArrayElements(env, parts, NULL);
+    jlong *l = (*env)->GetLongArrayElements(env, lens, NULL);
+    jlong *o = (*env)->GetLongArrayElements(env, offs, NULL);
+    int64_t total = -1;
+    if (pp && l && o)
+        total = ipls_agg_publish_partials(H(h), (const int32_t *)pp, n, IPLS_TGT_AGG, 0, NULL, 3, NULL, originLen, NULL,
+                                          0, IPLS_HOST_TEXT, (int64_t *)l, (int64_t *)o);
+    if (o) (*env)->ReleaseLongArrayElements(env, offs, o, 0);
+    if (l) (*env)->ReleaseLongArrayElements(env, lens, l, 0);
+    if (pp) (*env)->ReleaseIntArrayElements(env, parts, pp, JNI_ABORT);
+    if (total < 0) throw_for(env, (int)total, H(h));
+    return (jlong)total;
+}
+
+/* The publish loop over Auth_List (IPLS.java:1423-1431) in one launch per
+ * GPU: every text into the direct buffer at the layout's offsets. */
+JNIEXPORT void JNICALL Java_NativeAggregator_publishPartialsDirect(JNIEnv *env, jclass c, jlong h, jintArray parts,
+                                                                   jint tgt, jint a, jintArray b, jshort pid,
+                                                                   jbyteArray origin, jobject buf, jint pos,
+                                                                   jlong cap) {
+    (void)c;
+    if (!parts) { throw_iae(env, "null partition list"); return; }
+    const jsize n = (*env)->GetArrayLength(env, parts);
+    if (!need_len(env, b, n, "b (one value per partition)")) return;
+    void *dst = direct_span(env, buf, pos, cap);
+    if (!dst) return;
+    const jsize ol = origin ? (*env)->GetArrayLength(env, origin) : 0;
+    jint *pp = (*env)->GetIntArrayElements(env, parts, NULL);
+    jint *bb = (*env)->GetIntArrayElements(env, b, NULL);
+    jbyte *o = origin ? (*env)->GetByteArrayElements(env, origin, NULL) : NULL;
+    int64_t rc = IPLS_E_NOMEM;
+    if (pp && bb && (o || !origin))
+        rc = ipls_agg_publish_partials(H(h), (const int32_t *)pp, n, tgt, a, (const int32_t *)bb, pid,
+                                       (const uint8_t *)o, ol, dst, cap, IPLS_HOST_TEXT, NULL, NULL);
+    if (o) (*env)->ReleaseByteArrayElements(env, origin, o, JNI_ABORT);
+    if (bb) (*env)->ReleaseIntArrayElements(env, b, bb, JNI_ABORT);
+    if (pp) (*env)->ReleaseIntArrayElements(env, parts, pp, JNI_ABORT);
+    if (rc < 0) throw_for(env, (int)rc, H(h));
+}

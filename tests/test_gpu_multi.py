@@ -332,3 +332,54 @@ def test_config_f_slice_full_size(ipls, O):
         assert agg.checksum(p) == O.c_synth_sum_checksum(L, p, K), p
     agg.close()
     del t
+
+
+def test_publish_partials_batch_matches_single(ipls, O):
+    """ipls_agg_publish_partials: the publish loop over Auth_List
+    (IPLS.java:1423-1431) in one launch per GPU.  Model geometry with a short
+    last partition, partitions on both shards of [0, 0] in a mixed order, one
+    partition logically +0.0, a distinct b per text; every text equals the
+    single-partition call and Base64.getUrlEncoder(Marshall_Packet(...)), in
+    host memory, pinned memory and device memory (64-B aligned offsets)."""
+    M, P = 1_000_003, 5
+    agg = ipls.Aggregator(M, P, devices=[0, 0])
+    g = O.synth_bucket(M, 3, 1)
+    agg.UpdateGradient(g, auth_list=[0, 1, 3, 4])          # partition 2 stays logically +0.0
+    parts, bs = [4, 0, 2, 3, 1], [9, 2, 5, 7, 3]
+    origin = b"QmBatchOrigin"
+    texts = agg.publish_partials(parts, 12, bs, origin=origin)
+    for p, b, t in zip(parts, bs, texts):
+        want = O.java_b64url_encode(O.frame_encode(agg.read(p), 12, b, 3, origin))
+        assert t == want, p
+        assert t == agg.publish_partial(p, 12, b, origin=origin), p
+    lens = [len(t) for t in texts]
+    offs, pos = [], 0
+    for n in lens:
+        pos = (pos + 63) // 64 * 64
+        offs.append(pos)
+        pos += n
+    # device memory
+    dev = torch.zeros(pos + 64, dtype=torch.uint8, device="cuda")
+    assert agg.publish_partials(parts, 12, bs, origin=origin, out=int(dev.data_ptr())) == (lens, offs)
+    agg.sync()
+    host = dev.cpu().numpy().tobytes()
+    for i, t in enumerate(texts):
+        assert host[offs[i]:offs[i] + lens[i]] == t, parts[i]
+    # pinned host memory
+    pb = ipls.PinnedBuffer(pos)
+    assert agg.publish_partials(parts, 12, bs, origin=origin, out=pb) == (lens, offs)
+    v = pb.view()
+    for i, t in enumerate(texts):
+        assert v[offs[i]:offs[i] + lens[i]].tobytes() == t, parts[i]
+    pb.close()
+    # errors: a partition out of range, a buffer one byte short
+    with pytest.raises(ipls.IplsError):
+        agg.publish_partials([0, P], 1, [1, 1])
+    from ipls import _native as N
+    lib = N.lib()
+    pa = np.array(parts, dtype=np.int32)
+    ba = np.array(bs, dtype=np.int32)
+    buf = np.empty(pos, dtype=np.uint8)
+    assert lib.ipls_agg_publish_partials(agg.handle, pa.ctypes.data, len(parts), N.TGT_AGG, 12, ba.ctypes.data, 3,
+                                         None, 0, buf.ctypes.data, 10, N.HOST_TEXT, None, None) == N.IPLS_E_RANGE
+    agg.close()

@@ -324,5 +324,29 @@ def test_jni_devices_publish_and_device_batches(jvm, gpu, O):
         out = jvm.bytes_(b"\0" * (8 * Ls[q]))
         _, exc = jvm.call("finalizePartition", h, q, out)
         assert exc is None and jvm.data(out, np.uint8).tobytes() == O.be_encode(w)
+    # the round's publish loop in one call (publishPartials): layout, then the
+    # texts into a direct buffer; target Weights (what finalize left)
+    parts, bs = [3, 0, 2], [5, 9, 1]
+    lens, offs = jvm.longs([0] * 3), jvm.longs([0] * 3)
+    total, exc = jvm.call("publishPartialsLayout", h, jvm.ints(parts), 8, lens, offs, res=ctypes.c_int64)
+    assert exc is None
+    L_, O_ = jvm.data(lens, np.int64), jvm.data(offs, np.int64)
+    assert total == O_[-1] + L_[-1] and all(o % 64 == 0 for o in O_)
+    buf, mem = jvm.direct(int(total))
+    _, exc = jvm.call("publishPartialsDirect", h, jvm.ints(parts), 2, 7, jvm.ints(bs), 3, jvm.bytes_(b"QmOrigin"),
+                      buf, 0, ctypes.c_int64(int(total)))
+    assert exc is None
+    for i, q in enumerate(parts):
+        single, exc = jvm.call("publishPartial", h, q, 2, 7, bs[i], 3, jvm.bytes_(b"QmOrigin"), res=ctypes.c_void_p)
+        assert exc is None
+        assert mem[O_[i]:O_[i] + L_[i]].tobytes() == jvm.data(single, np.uint8).tobytes(), q
+    # a b[] shorter than the partition list, a buffer too small
+    _, exc = jvm.call("publishPartialsDirect", h, jvm.ints(parts), 2, 7, jvm.ints(bs[:2]), 3, None, buf, 0,
+                      ctypes.c_int64(int(total)))
+    assert exc == "java/lang/IllegalArgumentException"
+    small, _ = jvm.direct(16)
+    _, exc = jvm.call("publishPartialsDirect", h, jvm.ints(parts), 2, 7, jvm.ints(bs), 3, None, small, 0,
+                      ctypes.c_int64(16))
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
     jvm.call("close", h)
     del t
