@@ -87,6 +87,7 @@ struct PeerData {
   int port = 0;                         // -p
   bool secure_ipls = false;             // PeerData.java:62 (hard-coded false)
   int device = 0;                       // HIP device ordinal
+  std::vector<int32_t> devices;         // several GPUs: the -pa segments sharded over them (cfg.devices)
 };
 
 // ---- Middleware (Middleware.java) ------------------------------------------
@@ -180,6 +181,10 @@ class IPLS {
     c.partial_aggregation = pd.Partial_Aggregation;
     c.secure = pd.secure_ipls;
     c.device = pd.device;
+    if (!pd.devices.empty()) {
+      c.devices = pd.devices.data();
+      c.n_devices = (int32_t)pd.devices.size();
+    }
     ipls_agg* h = nullptr;
     const int rc = ipls_agg_open(&c, &h);   // init() -> InitializeWeights() (IPLS.java:1860)
     if (rc < 0) raise(rc, nullptr);
@@ -251,6 +256,33 @@ class IPLS {
     std::vector<uint8_t> out((size_t)n);
     const int64_t m = ipls_agg_commit_partial(h_.get(), Partition, workers, out.data(), n);
     if (m < 0) raise((int)m, h_.get());
+    return out;
+  }
+
+  // Wait_Client_Gradients' publish loop (IPLS.java:1423-1431, direct
+  // communication): for every partition i of Auth_List, ipfsClass.send(topic,
+  // Marshall_Packet(Aggregated_Gradients[i], id, middleware_iteration,
+  // workers[i].size() + 1, 3)) -- the texts, encoded on the GPU in one launch
+  // per device, in Auth_List order.
+  std::vector<std::string> Send_Partial_Updates(int32_t middleware_iteration,
+                                                const std::vector<int32_t>& workers_plus_one,
+                                                const std::string& id) {
+    const int n = (int)Auth_List.size();
+    if ((int)workers_plus_one.size() != n) throw IllegalArgumentException(IPLS_E_INVAL, "one workers count per partition");
+    std::vector<int64_t> lens((size_t)std::max(1, n)), offs((size_t)std::max(1, n));
+    const int64_t total = ipls_agg_publish_partials(h_.get(), Auth_List.data(), n, IPLS_TGT_AGG,
+                                                    middleware_iteration, workers_plus_one.data(), 3,
+                                                    (const uint8_t*)id.data(), (int32_t)id.size(), nullptr, 0,
+                                                    IPLS_HOST_TEXT, lens.data(), offs.data());
+    if (total < 0) raise((int)total, h_.get());
+    std::string buf((size_t)std::max<int64_t>(1, total), '\0');
+    const int64_t rc = ipls_agg_publish_partials(h_.get(), Auth_List.data(), n, IPLS_TGT_AGG, middleware_iteration,
+                                                 workers_plus_one.data(), 3, (const uint8_t*)id.data(),
+                                                 (int32_t)id.size(), buf.data(), total, IPLS_HOST_TEXT, nullptr,
+                                                 nullptr);
+    if (rc < 0) raise((int)rc, h_.get());
+    std::vector<std::string> out;
+    for (int i = 0; i < n; ++i) out.push_back(buf.substr((size_t)offs[i], (size_t)lens[i]));
     return out;
   }
 

@@ -147,6 +147,24 @@ int64_t ipls_oracle_frame_encode(const double *g, int32_t n, int32_t a, int32_t 
     return 14 + 8 * (int64_t)n + origin_len;
 }
 
+/* MyIPFSClass.java:1016 Base64.getUrlEncoder().encodeToString: every 3 input
+ * bytes -> 4 chars of A-Z a-z 0-9 - _, the last group padded with '=' */
+int64_t ipls_oracle_b64url_encode(const uint8_t *in, int64_t n, uint8_t *out) {
+    static const char A[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+    int64_t o = 0;
+    for (int64_t i = 0; i < n; i += 3) {
+        const int64_t r = n - i < 3 ? n - i : 3;
+        uint32_t v = (uint32_t)in[i] << 16;
+        if (r > 1) v |= (uint32_t)in[i + 1] << 8;
+        if (r > 2) v |= in[i + 2];
+        out[o++] = (uint8_t)A[(v >> 18) & 63];
+        out[o++] = (uint8_t)A[(v >> 12) & 63];
+        out[o++] = r > 1 ? (uint8_t)A[(v >> 6) & 63] : '=';
+        out[o++] = r > 2 ? (uint8_t)A[v & 63] : '=';
+    }
+    return o;
+}
+
 /* MyIPFSClass.java:1437-1459 (GET_GRADIENTS) / 1462-1481 (Get_Replica_Model) */
 int32_t ipls_oracle_frame_decode(const uint8_t *frame, int64_t len, int16_t *pid,
                                  int32_t *a, int32_t *b, double *g,

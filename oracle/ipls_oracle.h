@@ -81,6 +81,11 @@ int64_t ipls_oracle_frame_encode(const double *g, int32_t n, int32_t a, int32_t 
                                  int16_t pid, const uint8_t *origin, int32_t origin_len,
                                  uint8_t *out);
 
+/* java.util.Base64.getUrlEncoder().encodeToString(in) (MyIPFSClass.java:
+ * 1016): RFC 4648 URL-safe alphabet, '=' padding.  Returns chars written
+ * (4 * ceil(n / 3)). */
+int64_t ipls_oracle_b64url_encode(const uint8_t *in, int64_t n, uint8_t *out);
+
 /* GET_GRADIENTS / Get_Replica_Model after the pid short (MyIPFSClass.java:
  * 1437-1481).  Parses header, decodes n doubles into g (may be NULL).
  * Returns n, or -1 on a short buffer (BufferUnderflowException). */

@@ -120,6 +120,39 @@ int main(int argc, char** argv) {
 
   if (gpu) {
     // ---------------- device path ----------------
+    run("IPLS over two GPUs' shards: UpdateGradient + Send_Partial_Updates", [&] {
+      const int64_t M = 200003;
+      PeerData pd;
+      pd._MODEL_SIZE = M;
+      pd._PARTITIONS = 4;
+      pd.Min_Members = 2;
+      pd.devices = {0, 0};   // the one GPU of the test box, as two shards
+      IPLS ipls(pd, {3, 0, 1});
+      auto g = synth(M, 4, 4);
+      ipls.UpdateGradient(&g);
+      const std::vector<int32_t> w1 = {4, 2, 7};
+      auto texts = ipls.Send_Partial_Updates(11, w1, "QmPeer");
+      CHECK(texts.size() == 3, "one text per Auth_List partition");
+      for (int i = 0; i < 3; ++i) {
+        const int p = ipls.Auth_List[i];
+        auto part = organize(g, M, 4, p);
+        std::vector<double> agg(part.size());
+        for (size_t j = 0; j < part.size(); ++j) agg[j] = 0.0 + part[j];   // fresh accumulator + own bucket
+        std::vector<uint8_t> fr(14 + 8 * agg.size() + 6), want(4 * ((fr.size() + 2) / 3));
+        ipls_oracle_frame_encode(agg.data(), (int32_t)agg.size(), 11, w1[i], 3, (const uint8_t*)"QmPeer", 6,
+                                 fr.data());
+        ipls_oracle_b64url_encode(fr.data(), (int64_t)fr.size(), want.data());
+        CHECK(texts[i].size() == want.size() && std::memcmp(texts[i].data(), want.data(), want.size()) == 0,
+              "publish text == Base64.getUrlEncoder(Marshall_Packet(...))");
+      }
+      bool threw = false;
+      try {
+        ipls.Send_Partial_Updates(11, {1, 2}, "QmPeer");
+      } catch (const IllegalArgumentException&) {
+        threw = true;
+      }
+      CHECK(threw, "a workers list of the wrong length must throw");
+    });
     run("IPLS config A (ETHModel, -pa 3 -n 3)", [&] {
       const auto model = read_ethmodel(golden + "/ethmodel.f64be.gz");
       const int64_t M = (int64_t)model.size();

@@ -200,3 +200,23 @@ def test_c_synth_replica_checksum_matches_numpy(k, k_own):
     part = O.reduce([O.synth_bucket(L, p, j) for j in range(k_own, k)], L)
     W = own + O.reduce([part], L)
     assert O.c_synth_replica_checksum(L, p, k, k_own) == O.checksum(W)
+
+
+def test_c_b64url_encoder_matches_python_and_frames():
+    """The C oracle's Base64.getUrlEncoder restatement (MyIPFSClass.java:1016)
+    against Python's RFC 4648 urlsafe encoder (an independent implementation
+    of the same alphabet and '=' padding) over every length mod 3, and over
+    whole Marshall_Packet frames."""
+    import ctypes
+    lib = O.c_oracle()
+    lib.ipls_oracle_b64url_encode.restype = ctypes.c_int64
+    lib.ipls_oracle_b64url_encode.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    rng = np.random.default_rng(7)
+    cases = [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in (0, 1, 2, 3, 4, 5, 1000, 1001, 1002)]
+    cases += [O.frame_encode(O.synth_bucket(L, 1, 2), 7, 33, 3, origin)
+              for L, origin in ((5, b""), (6, b"Q"), (1001, b"QmOrigin"))]
+    for data in cases:
+        src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
+        out = np.zeros(4 * ((len(data) + 2) // 3) + 1, dtype=np.uint8)
+        n = lib.ipls_oracle_b64url_encode(src.ctypes.data, len(data), out.ctypes.data)
+        assert out[:n].tobytes() == O.java_b64url_encode(data), len(data)
