@@ -534,12 +534,46 @@ def config_a_leg(ipls, reps: int = 20) -> dict:
             out.append(O.c_divide(s))
         return np.concatenate(out)
 
+    # the same round the way INTEGRATION.md §4 wires it: the `ipfs cat` bytes
+    # and this peer's gradients land in pinned memory (direct ByteBuffers from
+    # hostAlloc), the kernels read them over PCIe (zero copy), and one fused
+    # launch does the folds + AggregatePartition(all) + GetPartitions into a
+    # pinned output (ipls_agg_aggregate_round): two C-ABI calls per round
+    pin_own = ipls.PinnedBuffer(8 * M)
+    pin_own.view()[:] = np.frombuffer(peers[0].tobytes(), dtype=np.uint8)
+    pin_be = [[None] * P for _ in range(3)]
+    for k in (1, 2):
+        for p in range(P):
+            pin_be[k][p] = ipls.PinnedBuffer(be[k][p].size)
+            pin_be[k][p].view()[:] = be[k][p]
+    pin_out = ipls.PinnedBuffer(8 * M)
+    own_dev = ipls.DeviceBuffer(pin_own.ptr, M)
+    rows = [[ipls.DeviceBuffer(pin_be[k][p].ptr, len(parts[0][p]), big_endian=True) for k in (1, 2)]
+            for p in range(P)]
+    out_dev = ipls.DeviceBuffer(pin_out.ptr, M)
+
+    def gpu_round_pinned():
+        agg.UpdateGradient(own_dev, auth_list=[0, 1, 2])
+        agg.aggregate_round(0, rows, big_endian=True, out=out_dev)
+        agg.sync()
+        return np.frombuffer(bytes(pin_out.view()[:8 * M]), dtype=np.float64)
+
     got, want = gpu_round(), cpu_round()
     same = bool(np.array_equal(got.view(np.int64), want.view(np.int64)))
+    got_p = gpu_round_pinned()
+    same_p = bool(np.array_equal(got_p.view(np.int64), want.view(np.int64)))
     t0 = time.perf_counter()
     for _ in range(reps):
         gpu_round()
     g_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        agg.UpdateGradient(own_dev, auth_list=[0, 1, 2])
+        agg.aggregate_round(0, rows, big_endian=True, out=out_dev)
+        agg.sync()
+    gp_ms = (time.perf_counter() - t0) / reps * 1e3
+    for b in [pin_own, pin_out] + [x for k in (1, 2) for x in pin_be[k]]:
+        b.close()
     t0 = time.perf_counter()
     for _ in range(reps):
         cpu_round()
@@ -548,6 +582,10 @@ def config_a_leg(ipls, reps: int = 20) -> dict:
     return {"workload": "A: ETHModel M=443,610, -pa 3 -n 3, 3 peers (host buffers in, averaged model out)",
             "gpu_round_ms": round(g_ms, 3), "cpu_port_round_ms": round(c_ms, 3), "cpu_port_cores": 1,
             "bit_identical": same,
+            "gpu_round_pinned_fused_ms": round(gp_ms, 3), "pinned_fused_bit_identical": same_p,
+            "pinned_fused_note": "buckets and own gradients in pinned host memory (direct ByteBuffers), read over "
+                                 "PCIe by the kernels; UpdateGradient + one ipls_agg_aggregate_round (folds + "
+                                 "AggregatePartition(all) + GetPartitions) writing the model to pinned memory",
             "note": f"wall time per round, mean of {reps}; GPU = Python caller through the C-ABI (H2D of 9 BE "
                     "buckets + own gradients, folds, AggregatePartition, divide, D2H of the model); CPU = the C "
                     "port of the Updater BE decode + fold and the GetPartitions divide"}

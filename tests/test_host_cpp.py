@@ -27,7 +27,8 @@ def test_host_mirror_on_gpu():
     _build()
     r = subprocess.run([str(BIN), "--gpu", str(GOLDEN)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "9 passed, 0 failed" in r.stdout, r.stdout
+    n_pass = r.stdout.count("PASS ")
+    assert n_pass >= 10 and f"{n_pass} passed, 0 failed" in r.stdout, r.stdout
 
 
 def test_partial_update_parser_under_asan():
