@@ -1376,8 +1376,9 @@ def test_full_ipls_round_four_peers(ipls, O):
         agg.close()
 
 
-@pytest.mark.parametrize("seed,group", [(1, 1), (2, 4), (3, 32), (4, 2), (5, 8)])
-def test_stateful_random_sequence(ipls, O, seed, group, P=4, L=5003):
+@pytest.mark.parametrize("seed,group,devices", [(1, 1, None), (2, 4, None), (3, 32, None), (4, 2, None), (5, 8, None),
+                                                (6, 4, [0, 0]), (7, 32, [0, 0, 0])])
+def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
     """A random sequence over the whole accumulator surface, checked step by
     step against a numpy model of the Java state (Aggregated_Gradients,
     Replicas_Gradients, Aggregated_Gradients_from_future, Weights): host and
@@ -1385,9 +1386,12 @@ def test_stateful_random_sequence(ipls, O, seed, group, P=4, L=5003):
     every start mode and byte order, AggregatePartition, resets, promotion of
     future gradients, the async blend, cache_partition, the fused round and
     GetPartitions.  Buckets include -0.0, subnormals and huge values so the
-    start-value and grouping rules show in the bits."""
+    start-value and grouping rules show in the bits.  ``devices``: the same
+    sequence through a multi-device handle (shards [0,2) | [2,4), and a
+    three-entry list whose last shard owns no partition), so the front's
+    routing of every call is checked against the same model."""
     rng = np.random.default_rng(seed)
-    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
     agg.set_coalesce(group)
     pool = []
     for k in range(10):
