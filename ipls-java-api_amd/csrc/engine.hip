@@ -303,6 +303,20 @@ bool is_pinned_host(const void* p, void** dev_alias = nullptr) {
   return true;
 }
 
+// Memory a kernel of this process may write at the address p itself: device
+// memory, or pinned host memory mapped at the same address (hipHostMalloc).
+// Pageable memory is rejected before any launch (a kernel store there faults).
+bool kernel_writable(const void* p) {
+  hipPointerAttribute_t a;
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return true;
+  void* alias = nullptr;
+  return a.type == hipMemoryTypeHost && is_pinned_host(p, &alias) && alias == p;
+}
+
 // Copy `bytes` of host memory (pinned or pageable) to device `dst` on the
 // handle's stream and wait for that copy only: the caller may reuse its buffer
 // on return, kernels queued behind the copy keep running.  HIP's own path for
@@ -2208,6 +2222,8 @@ int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_
   const unsigned long long* src =
       (zf && *zf) ? nullptr : (const unsigned long long*)(h->arena + target_off(h, p, target));
   unsigned char* dst = (unsigned char*)out;
+  if (out_kind == IPLS_DEV_TEXT && !kernel_writable(out))
+    return fail(h, IPLS_E_INVAL, "DEV_TEXT output is neither device memory nor pinned host memory");
   const bool dev_direct = out_kind == IPLS_DEV_TEXT && !((uintptr_t)out & 15);
   if (!dev_direct) {
     if (int rc = ensure_scratch(h, (size_t)T + 64)) return rc;
@@ -2244,6 +2260,8 @@ int64_t dev_publish_many(ipls_dev* h, int n, const int* parts, int target, int32
     if (target_off(h, parts[i], target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   }
   HIP_TRY(h, hipSetDevice(h->device));
+  if (out_kind == IPLS_DEV_TEXT && !kernel_writable(out))
+    return fail(h, IPLS_E_INVAL, "DEV_TEXT output is neither device memory nor pinned host memory");
   const unsigned char* dorig = nullptr;
   if (origin_len > 0) {
     void* d = nullptr;

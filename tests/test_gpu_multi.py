@@ -282,6 +282,13 @@ def test_publish_partial_rejects_bad_arguments(ipls):
                                         N.HOST_TEXT) == N.IPLS_E_RANGE
     assert lib.ipls_agg_publish_partial(agg.handle, 0, N.TGT_AGG, 0, 0, 3, None, 0, out, need,
                                         N.HOST_F64) == N.IPLS_E_INVAL
+    # device text into pageable host memory: rejected before any launch
+    assert lib.ipls_agg_publish_partial(agg.handle, 0, N.TGT_AGG, 0, 0, 3, None, 0, out, need,
+                                        N.DEV_TEXT) == N.IPLS_E_INVAL
+    import numpy as _np
+    parts, bs = _np.zeros(1, dtype=_np.int32), _np.ones(1, dtype=_np.int32)
+    assert lib.ipls_agg_publish_partials(agg.handle, parts.ctypes.data, 1, N.TGT_AGG, 0, bs.ctypes.data, 3, None, 0,
+                                         out, need, N.DEV_TEXT, None, None) == N.IPLS_E_INVAL
     agg.close()
 
 
