@@ -790,9 +790,14 @@ int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, con
   for (int q = 0; q < n_parts; ++q) {
     Partial& x = row[p_first + q];
     if (!x.d) {
-      if (hipMalloc(&x.d, (size_t)H->len[p_first + q] * 8) != hipSuccess ||
-          hipEventCreateWithFlags(&x.ready, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming) != hipSuccess) {
+      // an event is recorded only on a stream of the device it was created
+      // on: `ready` on the slot's stream, `consumed` on the owner's
+      const int od = H->devices[H->owner[p_first + q]];
+      const bool ok = hipMalloc(&x.d, (size_t)H->len[p_first + q] * 8) == hipSuccess &&
+                      hipEventCreateWithFlags(&x.ready, hipEventDisableTiming) == hipSuccess &&
+                      hipSetDevice(od) == hipSuccess &&
+                      hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming) == hipSuccess;
+      if (hipSetDevice(H->devices[slot]) != hipSuccess || !ok) {
         (void)hipGetLastError();
         return ferr(H, IPLS_E_NOMEM, "partial buffer of partition %d on device %d", p_first + q, H->devices[slot]);
       }
