@@ -163,8 +163,11 @@ def combine_replicas(agg, plan: ReplicaPlan, rank: int, *, device=None, mode: st
     if ops:
         for work in dist.batch_isend_irecv(ops):
             work.wait()
-    if landing:
-        _landed(landing[0][1])
+        # RCCL's wait() only orders torch's stream after the group: block the
+        # host on it, so received partials are visible to the aggregator's
+        # stream and a send buffer is not refilled by the next export while
+        # the send may still read it (a rank may only send)
+        _landed(ops[0].tensor)
     for p, buf in landing:                                # fold in (partition, replica) order
         agg.import_partial(p, buf)                        # REP[p] += R_r (Updater.java:40-44)
     if landing:
