@@ -506,15 +506,18 @@ struct FinDesc {
 };
 
 // 16-B vectors per lane of k_finalize / k_divide (tile = kBlock * 2 * kV doubles)
-constexpr int kFinV = 4, kDivV = 4;
+constexpr int kFinV = 8, kDivV = 4;   // tools/copy_sweep.hip, profiles/r02/s3/copy_sweep.txt
 constexpr int64_t kFinTile = (int64_t)kBlock * 2 * kFinV, kDivTile = (int64_t)kBlock * 2 * kDivV;
 
-template <bool REP_ZERO, bool ZERO_ACC>
-__global__ __launch_bounds__(kBlock) void k_finalize(const FinDesc* __restrict__ parts,
-                                                     double* __restrict__ arena,
-                                                     int tiles_per_part) {
-  // 16 B per lane per step (arena arrays are 256-B aligned), 4 steps per lane.
-  constexpr int kV = kFinV;
+//   BS, V: lanes per workgroup and 16-B vectors per lane (tile = BS * 2 * V
+//   doubles); the host launches the defaults (tools/copy_sweep.hip sweeps them)
+template <bool REP_ZERO, bool ZERO_ACC, int BS = kBlock, int V = kFinV>
+__global__ __launch_bounds__(BS) void k_finalize(const FinDesc* __restrict__ parts,
+                                                 double* __restrict__ arena,
+                                                 int tiles_per_part) {
+  // 16 B per lane per step (arena arrays are 256-B aligned), V steps per lane.
+  constexpr int kBlock = BS;
+  constexpr int kV = V;
   constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
   const int q = blockIdx.x / tiles_per_part;
   const int t = blockIdx.x - q * tiles_per_part;
@@ -575,18 +578,19 @@ struct DivDesc {
   int64_t out_off;
 };
 
-template <bool OUT_BE, bool SECURE>
-__global__ __launch_bounds__(kBlock) void k_divide(const DivDesc* __restrict__ parts,
-                                                   const double* __restrict__ arena,
-                                                   unsigned long long* __restrict__ out,
-                                                   int tiles_per_part) {
+template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV>
+__global__ __launch_bounds__(BS) void k_divide(const DivDesc* __restrict__ parts,
+                                               const double* __restrict__ arena,
+                                               unsigned long long* __restrict__ out,
+                                               int tiles_per_part) {
   // The flat output offset p*chunk is arbitrary, so the tiles are laid over
   // the OUTPUT: block 0 first writes the `head` elements up to the first 128-B
   // line boundary of this partition's output, then every wave stores whole
   // lines (64 lanes x 16 B = 8 lines), and each lane reads its two W values
   // with 8-B loads (W's alignment relative to the output is arbitrary; reads
   // of partial lines cost little, partial-line writes do).
-  constexpr int kV = kDivV;
+  constexpr int kBlock = BS;
+  constexpr int kV = V;
   constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
   const int q = blockIdx.x / tiles_per_part;
   const int t = blockIdx.x - q * tiles_per_part;

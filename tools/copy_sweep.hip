@@ -1,0 +1,159 @@
+// copy_sweep.hip -- dev tool: block shapes of the two copy-shaped kernels of a
+// round, k_finalize (AggregatePartition, W = AGG + REP, IPLS.java:1248-1274)
+// and k_divide (GetPartitions, IPLS.java:1159-1174), timed in one process
+// round-robin so every variant sees the same physical pages.
+// The fold found that the contiguous bytes each CU streams are the lever
+// (16 KiB -> 256 KiB: 67-85 % -> 84-89 %); this asks the same
+// of the copies, which ship at 256 lanes x 4 vectors = 16 KiB per block.
+//
+// Usage: copy_sweep P L REPS      (default: config C, 16 x 4194304, 20)
+// Algorithmic bytes: finalize 16 per element (read AGG, write W; REP
+// logically zero), divide 16 per output element (read W, write the model).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../ipls-java-api_amd/csrc/ipls_kernels.hpp"
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e = (x);                                                                \
+    if (e != hipSuccess) {                                                             \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+using namespace ipls;
+
+struct Var {
+  std::string name;
+  double bytes;
+  std::function<void(hipStream_t)> run;
+  std::vector<float> ms;
+};
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 16;
+  const int64_t L = argc > 2 ? atoll(argv[2]) : 4194304;
+  const int REPS = argc > 3 ? atoi(argv[3]) : 20;
+  // arena like the engine's: per partition AGG, REP, W, each 256-B aligned
+  const int64_t La = (L + 31) / 32 * 32;
+  double* arena;
+  CK(hipMalloc(&arena, (size_t)P * 3 * La * 8));
+  std::vector<FinDesc> fd(P);
+  std::vector<DivDesc> dd(P);
+  for (int p = 0; p < P; ++p) {
+    fd[p] = FinDesc{L, (int64_t)p * 3 * La, (int64_t)p * 3 * La + La, (int64_t)p * 3 * La + 2 * La};
+    dd[p] = DivDesc{L, fd[p].w_off, (int64_t)p * (L - 1)};   // flat model offsets p*chunk
+    hipLaunchKernelGGL(k_synth<false>, dim3(4096), dim3(kBlock), 0, 0,
+                       (unsigned long long*)(arena + fd[p].agg_off), L, 0x1B52026ULL ^ ((unsigned long long)p << 40));
+  }
+  unsigned long long* model;
+  CK(hipMalloc(&model, (size_t)P * (L - 1) * 8 + 256));
+  FinDesc* d_fd;
+  DivDesc* d_dd;
+  CK(hipMalloc(&d_fd, P * sizeof(FinDesc)));
+  CK(hipMalloc(&d_dd, P * sizeof(DivDesc)));
+  CK(hipMemcpy(d_fd, fd.data(), P * sizeof(FinDesc), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_dd, dd.data(), P * sizeof(DivDesc), hipMemcpyHostToDevice));
+  // W = AGG once, so the divide reads a real model (count slot = synth value)
+  hipLaunchKernelGGL((k_finalize<true, false>), dim3((unsigned)((L + kFinTile - 1) / kFinTile) * P), dim3(kBlock), 0,
+                     0, d_fd, arena, (int)((L + kFinTile - 1) / kFinTile));
+  CK(hipDeviceSynchronize());
+  const double fin_bytes = (double)P * L * 16, div_bytes = (double)P * (L - 1) * 16;
+
+  std::vector<Var> vars;
+#define FIN(BS, V)                                                                                          \
+  vars.push_back({"finalize BS=" #BS " V=" #V, fin_bytes, [=](hipStream_t s) {                              \
+                    const int64_t tile = (int64_t)BS * 2 * V;                                                \
+                    const int tpp = (int)((L + tile - 1) / tile);                                            \
+                    hipLaunchKernelGGL((k_finalize<true, false, BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
+                                       d_fd, arena, tpp);                                                    \
+                  }})
+#define DIV(BS, V)                                                                                          \
+  vars.push_back({"divide   BS=" #BS " V=" #V, div_bytes, [=](hipStream_t s) {                              \
+                    const int64_t tile = (int64_t)BS * 2 * V;                                                \
+                    const int tpp = (int)((L - 1 + tile - 1) / tile);                                        \
+                    hipLaunchKernelGGL((k_divide<false, false, BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
+                                       d_dd, (const double*)arena, model, tpp);                              \
+                  }})
+  FIN(256, 4);   // shipped
+  FIN(256, 8);
+  FIN(256, 16);
+  FIN(512, 8);
+  FIN(512, 16);
+  FIN(1024, 4);
+  FIN(1024, 8);
+  FIN(1024, 16);
+  DIV(256, 4);   // shipped
+  DIV(256, 8);
+  DIV(256, 16);
+  DIV(512, 8);
+  DIV(1024, 4);
+  DIV(1024, 8);
+  DIV(1024, 16);
+#undef FIN
+#undef DIV
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  // warm + check: each variant's whole output (W of every partition, or the
+  // flat model) after poisoning it must checksum like the shipped shape's
+  unsigned long long* d_sum;
+  CK(hipMalloc(&d_sum, 8));
+  unsigned long long want[2] = {0, 0};
+  bool all_ok = true;
+  for (auto& v : vars) {
+    const bool fin = v.name[0] == 'f';
+    if (fin)
+      for (int p = 0; p < P; ++p) CK(hipMemsetAsync(arena + fd[p].w_off, 0xA5, (size_t)L * 8, s));
+    else
+      CK(hipMemsetAsync(model, 0xA5, (size_t)P * (L - 1) * 8, s));
+    v.run(s);
+    unsigned long long sum = 0;
+    for (int p = 0; p < (fin ? P : 1); ++p) {
+      CK(hipMemsetAsync(d_sum, 0, 8, s));
+      const unsigned long long* x = fin ? (const unsigned long long*)(arena + fd[p].w_off) : model;
+      hipLaunchKernelGGL(k_checksum<false>, dim3(2048), dim3(kBlock), 0, s, x, fin ? L : (int64_t)P * (L - 1), d_sum);
+      unsigned long long c = 0;
+      CK(hipMemcpyAsync(&c, d_sum, 8, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      sum = sum * 31 + c;
+    }
+    unsigned long long& w = want[fin ? 0 : 1];
+    if (!w) w = sum;
+    if (sum != w) {
+      all_ok = false;
+      printf("MISMATCH %s\n", v.name.c_str());
+    }
+  }
+  printf("# outputs identical across shapes: %s\n", all_ok ? "yes" : "NO");
+  for (int r = 0; r < REPS; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(a, s));
+      v.run(s);
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      v.ms.push_back(ms);
+    }
+  CK(hipGetLastError());
+  printf("# P=%d L=%lld REPS=%d  finalize %.0f B, divide %.0f B per launch\n", P, (long long)L, REPS, fin_bytes,
+         div_bytes);
+  for (auto& v : vars) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2];
+    printf("%-24s median %8.4f ms  min %8.4f ms  %8.1f GB/s (median)  %5.1f%% of 8 TB/s\n", v.name.c_str(), med,
+           v.ms[0], v.bytes / (med * 1e-3) / 1e9, 100.0 * v.bytes / (med * 1e-3) / 8e12);
+  }
+  return 0;
+}
