@@ -411,12 +411,14 @@ inline bool fill(int64_t tiles) {
 template <bool BE_IN, int START, bool FIN = false>
 constexpr int big_r() { return START != kAccum ? 16 : 8; }
 // SEQ schedule of the big shape (0 = hipcc's own): big-endian input at R = 16
-// fences every 2 loads except among a peer's last 4 vectors (SEQF = 2 + 10*4),
-// which lets hipcc overlap the next peer's first loads with that tail:
-// +0.5 to +1.7 points over fencing all 16 in the same process, no spills
-// (profiles/r01/sweep_be_seqf*.txt, sweep_be_tail.txt).
+// loads, decodes and adds a peer's vectors three at a time with a fence after
+// each group (SEQF = 3; 118 VGPRs, no spills).  Round 2 swept fence periods
+// 1-8 with and without a free tail in one process (profiles/r02/s3/
+// sweep_be_tail{1,2}*.txt): 3 beats round 1's every-2-with-the-last-4-free
+// (SEQF = 42) by 0.7-1.6 points on C's and D's shapes, BE in and in + out;
+// periods >= 5, a free tail on period 3, and period 1 are all slower.
 template <bool BE_IN, int START>
-constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 42 : 0; }
+constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 3 : 0; }
 
 // C-ABI start mode -> kernel template start
 int kstart(int start_mode) {

@@ -3,7 +3,7 @@
 The fold kernel's dispatch picks a tile shape by how many tiles a batch fills
 (engine.hip launch_reduce_v: big = 1024 lanes x 16 vectors, mid = 256 lanes x
 16 vectors, small = 256 lanes x 8 peers in flight).  Big-endian input at
-R = 16 runs the hand-fenced SEQ schedule (SEQF = 42), START_ACCUM runs R = 8,
+R = 16 runs the hand-fenced SEQ schedule (SEQF = 3), START_ACCUM runs R = 8,
 partial last tiles run map 3.  Every case below asserts through
 ipls_agg_last_launch that it reached the shape it was written for, then
 compares with the oracle: bit for bit on whole partitions (C oracle,
@@ -87,7 +87,7 @@ def expect(li, ipls, kernel, shape, vectors, seqf, be_in, be_out, mapping=None):
 
 def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
     """Config D exactly: 64 partitions x 4,194,304 BE doubles x 32 peers, BE
-    sum bytes out -- the shipped big shape with the SEQF = 42 schedule
+    sum bytes out -- the shipped big shape with the SEQF = 3 schedule
     (2048 tiles, no partial tile), ZERO and FIRST start; then BE in with
     native doubles out into the accumulators, and ACCUM (R = 8) on top."""
     m = golden_meta["full"]["D"]
@@ -98,7 +98,7 @@ def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
     for start in (ipls.START_ZERO, ipls.START_FIRST):
         agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=True)
         li = agg.last_launch()
-        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 42, True, True, mapping=0)
+        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 3, True, True, mapping=0)
         assert li["block"] == 1024 and li["grid"] == P * L // (1024 * 2 * 16)
         agg.sync()
         got = [ipls.checksum_dev(ipls.DeviceBuffer(o, L, big_endian=True)) for o in pool.outs]
@@ -108,7 +108,7 @@ def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
         assert_bits_equal(pool.out_host(q, L, True), ref_sum(O, L, q, K), f"D partition {q}")
     # BE in, native doubles into AGG (GetParameters decode fused, Updater fold)
     agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ZERO, big_endian=True)
-    expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 42, True, False)
+    expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 3, True, False)
     assert [agg.checksum(q) for q in range(P)] == want
     # ACCUM: S + fold again, BE out (R = 8, compiler schedule)
     agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ACCUM, big_endian_in=True,
@@ -131,7 +131,7 @@ def test_be_big_shape_partial_tile(ipls, O, be_out):
     want = [O.c_synth_sum_checksum(L, q, K) for q in range(P)]
     for start in (ipls.START_ZERO, ipls.START_FIRST):
         agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=be_out)
-        expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 42, True, be_out, mapping=3)
+        expect(agg.last_launch(), ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 3, True, be_out, mapping=3)
         agg.sync()
         assert [ipls.checksum_dev(ipls.DeviceBuffer(o, L, big_endian=be_out)) for o in pool.outs] == want
     assert_bits_equal(pool.out_host(P - 1, L, be_out), ref_sum(O, L, P - 1, K), "partial-tile partition")
@@ -148,7 +148,7 @@ def test_be_big_shape_partial_tile(ipls, O, be_out):
 @pytest.mark.parametrize("P,L", [(1, 4_194_304 + 4099), (2, 2_100_003)])
 def test_be_mid_shape(ipls, O, P, L):
     """One or two partitions: too few big tiles, so the 256-lane mid shape
-    (SEQF = 42 for BE input) with a partial last tile."""
+    (SEQF = 3 for BE input) with a partial last tile."""
     K = 32
     pool = Pool(ipls, P, L, K, True, O.SEED)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
@@ -156,7 +156,7 @@ def test_be_mid_shape(ipls, O, P, L):
     for start in (ipls.START_ZERO, ipls.START_FIRST):
         agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=True)
         li = agg.last_launch()
-        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_MID, 16, 42, True, True, mapping=3)
+        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_MID, 16, 3, True, True, mapping=3)
         assert li["block"] == 256
         agg.sync()
         for q in range(P):
@@ -175,7 +175,7 @@ def test_be_mid_shape(ipls, O, P, L):
 
 def test_be_fused_round_config_c(ipls, O, golden_meta):
     """The fused round (k_round: fold + W = AGG + REP + GetPartitions divide)
-    on config C's shape with BE buckets: big shape, SEQF = 42; W and the
+    on config C's shape with BE buckets: big shape, SEQF = 3; W and the
     averages against the oracle's checksums."""
     m = golden_meta["full"]["C"]
     P, L, K = m["partitions"], m["bucket_len"], m["peers"]
@@ -183,7 +183,7 @@ def test_be_fused_round_config_c(ipls, O, golden_meta):
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     avg = torch.empty(P * (L - 1), dtype=torch.float64, device="cuda")
     agg.aggregate_round(0, pool.rows, big_endian=True, out=ipls.DeviceBuffer.from_tensor(avg))
-    expect(agg.last_launch(), ipls, ipls.KERNEL_ROUND, ipls.SHAPE_BIG, 16, 42, True, False)
+    expect(agg.last_launch(), ipls, ipls.KERNEL_ROUND, ipls.SHAPE_BIG, 16, 3, True, False)
     agg.sync()
     assert [agg.checksum(q, ipls.TGT_WEIGHTS) for q in range(P)] == m["sum_checksum"]
     base = int(avg.data_ptr())
@@ -210,7 +210,7 @@ def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
         agg.Update(rep[q], q, from_clients=False)          # Replicas_Gradients = +0.0 + R
     out = agg.aggregate_round(0, pool.rows, big_endian=True)
     li = agg.last_launch()
-    assert (li["kernel"], li["vectors"], li["seqf"], li["be_in"]) == (ipls.KERNEL_ROUND, 16, 42, 1), li
+    assert (li["kernel"], li["vectors"], li["seqf"], li["be_in"]) == (ipls.KERNEL_ROUND, 16, 3, 1), li
     assert li["shape"] == (ipls.SHAPE_BIG if P > 1 else ipls.SHAPE_MID) and li["map"] == 3, li
     for q in range(P):
         s = ref_sum(O, L, q, K)

@@ -306,6 +306,24 @@ int main(int argc, char** argv) {
     ADDS(16, 0, 44);
     ADDS(16, 0, 84);
   }
+  if (getenv("SWEEP_TAIL1")) {   // fence every 1 or 3 vectors with a free tail (SEQF = F + 10*T)
+    ADDS(16, 0, 42);
+    ADDS(16, 0, 41);
+    ADDS(16, 0, 71);
+    ADDS(16, 0, 91);
+    ADDS(16, 0, 3);
+    ADDS(16, 0, 43);
+    ADDS(16, 0, 73);
+  }
+  if (getenv("SWEEP_TAIL2")) {   // fence periods 3..8 around the SEQF=3 result
+    ADDS(16, 0, 42);
+    ADDS(16, 0, 3);
+    ADDS(16, 0, 13);
+    ADDS(16, 0, 5);
+    ADDS(16, 0, 6);
+    ADDS(16, 0, 7);
+    ADDS(16, 0, 8);
+  }
   if (quick) {             // fence interval of the SEQ schedule (0 = hipcc's own)
     ADDS(16, 0, 0);
     ADDS(16, 0, 1);
