@@ -270,6 +270,8 @@ JNIEXPORT jint JNICALL Java_NativeAggregator_ingestTexts(JNIEnv *env, jclass c, 
     jint *pp = NULL;
     int rc = IPLS_E_NOMEM;
     if (!arr || !ptr || !len || !st) goto out;
+    /* one local ref per text is live at once: more than the 16 a native frame is guaranteed */
+    if ((*env)->EnsureLocalCapacity(env, n + 8) < 0) { free(arr); free(ptr); free(len); free(st); return 0; }
     for (jsize i = 0; i < n; ++i) {
         arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, msgs, i);
         len[i] = arr[i] ? (*env)->GetArrayLength(env, arr[i]) : 0;
@@ -439,11 +441,13 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclas
     uint8_t *out = NULL;
     jsize got = 0;
     if (!arr || !ptrs || !lens) { throw_msg(env, "java/lang/OutOfMemoryError", "mergeFiles"); goto done; }
+    if ((*env)->EnsureLocalCapacity(env, k + 8) < 0) goto done;   /* OutOfMemoryError pending */
     for (; got < k; ++got) {   /* copies: several arrays cannot be held critical across a JNI call */
         arr[got] = (jbyteArray)(*env)->GetObjectArrayElement(env, files, got);
         if (!arr[got]) { throw_iae(env, "null file"); goto done; }
         lens[got] = (*env)->GetArrayLength(env, arr[got]);
         ptrs[got] = (const uint8_t *)(*env)->GetByteArrayElements(env, arr[got], NULL);
+        if (!ptrs[got]) { ++got; goto done; }   /* OutOfMemoryError pending */
     }
     int64_t cap = 8 * (lens[0] / 8);
     if (partial) {

@@ -41,6 +41,8 @@ static int g_critical;
 static int g_pinned;      /* Get*Elements not released yet */
 static int g_violations;
 static char g_last_violation[160];
+static jint g_local_cap = 16;   /* the JNI spec guarantees 16 local refs per native frame */
+static jint g_locals;              /* object-array element refs live (DeleteLocalRef releases) */
 
 static void violation(const char *what) {
     ++g_violations;
@@ -104,6 +106,7 @@ static jboolean JNICALL ExceptionCheck(JNIEnv *env) {
 static void JNICALL DeleteLocalRef(JNIEnv *env, jobject o) {
     (void)env; (void)o;
     plain_call("DeleteLocalRef");   /* local refs of object-array elements: the array owns them */
+    if (g_locals > 0) --g_locals;
 }
 
 static jsize JNICALL GetArrayLength(JNIEnv *env, jarray a) {
@@ -112,10 +115,18 @@ static jsize JNICALL GetArrayLength(JNIEnv *env, jarray a) {
     return a->n;
 }
 
+static jint JNICALL EnsureLocalCapacity(JNIEnv *env, jint cap) {
+    (void)env;
+    guarded_call("EnsureLocalCapacity");
+    if (cap > g_local_cap) g_local_cap = cap;
+    return 0;
+}
+
 static jobject JNICALL GetObjectArrayElement(JNIEnv *env, jobjectArray a, jsize i) {
     (void)env;
     guarded_call("GetObjectArrayElement");
     if (a->kind != K_OBJECTS || i < 0 || i >= a->n) { violation("GetObjectArrayElement index"); return NULL; }
+    if (++g_locals > g_local_cap) violation("local references beyond EnsureLocalCapacity");
     return ((jobject *)a->data)[i];
 }
 
@@ -234,7 +245,7 @@ static const struct JNINativeInterface_ g_table = {
     NewByteArray, NewIntArray, GetByteArrayElements, GetIntArrayElements, GetLongArrayElements,
     ReleaseByteArrayElements, ReleaseIntArrayElements, ReleaseLongArrayElements, SetByteArrayRegion,
     SetIntArrayRegion, GetPrimitiveArrayCritical, ReleasePrimitiveArrayCritical, NewDirectByteBuffer,
-    GetDirectBufferAddress, GetDirectBufferCapacity,
+    GetDirectBufferAddress, GetDirectBufferCapacity, EnsureLocalCapacity,
 };
 static JNIEnv g_env = &g_table;
 
@@ -271,4 +282,7 @@ JNIEXPORT void fj_clear(void) { g_exc = 0; g_exc_class[0] = 0; g_exc_msg[0] = 0;
 /* rule breaks since the last call, plus regions/elements left open */
 JNIEXPORT int fj_violations(void) { return g_violations + (g_critical != 0) + (g_pinned != 0); }
 JNIEXPORT const char *fj_last_violation(void) { return g_last_violation; }
-JNIEXPORT void fj_reset_violations(void) { g_violations = 0; g_critical = 0; g_pinned = 0; g_last_violation[0] = 0; }
+JNIEXPORT void fj_reset_violations(void) {
+    g_violations = 0; g_critical = 0; g_pinned = 0; g_last_violation[0] = 0;
+    g_local_cap = 16; g_locals = 0;   /* a new native frame */
+}

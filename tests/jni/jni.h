@@ -72,6 +72,7 @@ struct JNINativeInterface_ {
     jobject (JNICALL *NewDirectByteBuffer)(JNIEnv *env, void *address, jlong capacity);
     void *(JNICALL *GetDirectBufferAddress)(JNIEnv *env, jobject buf);
     jlong (JNICALL *GetDirectBufferCapacity)(JNIEnv *env, jobject buf);
+    jint (JNICALL *EnsureLocalCapacity)(JNIEnv *env, jint capacity);
 };
 
 #endif /* IPLS_TEST_JNI_H */

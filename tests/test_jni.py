@@ -162,6 +162,20 @@ def test_direct_buffer_checks_before_the_library(jvm):
         assert exc == "java/lang/IllegalArgumentException", (name, exc)
 
 
+def test_many_texts_and_files_reserve_local_refs(jvm):
+    """A native frame is guaranteed 16 local references; ingestTexts and
+    mergeFiles hold one per element at once, so they reserve the rest with
+    EnsureLocalCapacity first (the fake JVM counts live element refs against
+    the reserved capacity).  A null handle makes the library call fail after
+    the refs are taken, so this runs without a GPU."""
+    texts = jvm.objects([jvm.bytes_(b"AAAA")] * 40)
+    _, exc = jvm.call("ingestTexts", L64(0), 0, texts, 2, None, None, res=ctypes.c_int32)
+    assert exc == "java/lang/IllegalArgumentException"
+    files = jvm.objects([jvm.bytes_(b"\0" * 16)] * 24)
+    _, exc = jvm.call("mergeFiles", L64(0), files, 0, res=ctypes.c_void_p)
+    assert exc == "java/lang/IllegalArgumentException"
+
+
 def test_open_without_gpu_throws(jvm):
     torch = pytest.importorskip("torch")
     if torch.cuda.is_available():
