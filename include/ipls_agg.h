@@ -18,6 +18,10 @@
  *  - Calls with only device-resident operands are stream-ordered on the
  *    handle's HIP stream and may return before the GPU finishes; use
  *    ipls_agg_sync() before reading device results from another stream.
+ *    The handle's stream is non-blocking: device operands written on another
+ *    stream (the null stream included) must be complete, or ordered before
+ *    the call by an event the handle's stream waits on (ipls_agg_stream /
+ *    ipls_agg_partition_device give the stream).
  *  - A handle is internally serialised (one mutex): it may be called from
  *    the Updater thread and the daemon thread concurrently, as the Java code
  *    does under PeerData.mtx (PeerData.java:27).  Calls on one partition

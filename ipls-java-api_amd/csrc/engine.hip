@@ -419,6 +419,16 @@ constexpr int big_r() { return START != kAccum ? 16 : 8; }
 // periods >= 5, a free tail on period 3, and period 1 are all slower.
 template <bool BE_IN, int START>
 constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 3 : 0; }
+// The mid shape (256 lanes, one or two partitions: per-partition flushes, the
+// storage merge of one partition's files) with big-endian input runs 8
+// vectors per lane on hipcc's own schedule (100 VGPRs, no spills): one
+// partition of 4M x 32 peers at 83-86 % against 55-64 % for the big shape's
+// R = 16 SEQ schedules at 256 lanes (profiles/r02/s3/sweep_be_p1.txt, BE in
+// and BE in + out, two processes each).  Native doubles keep R = 16 (86-88 %).
+template <bool BE_IN, int START>
+constexpr int mid_r() { return BE_IN ? 8 : big_r<BE_IN, START>(); }
+template <bool BE_IN, int START>
+constexpr int mid_seqf() { return mid_r<BE_IN, START>() > 8 ? big_seqf<BE_IN, START>() : 0; }
 
 // C-ABI start mode -> kernel template start
 int kstart(int start_mode) {
@@ -447,10 +457,11 @@ template <bool BE_IN, bool BE_OUT, int START, bool FIN = false>
 ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, const unsigned long long* const* bufs,
                                  const PartDesc* parts, int k, int secure = 0, const double* cnts = nullptr) {
   constexpr int R = big_r<BE_IN, START, FIN>();
+  constexpr int RM = mid_r<BE_IN, START>();
   constexpr int KER = FIN ? IPLS_KERNEL_ROUND : IPLS_KERNEL_REDUCE;
   const int64_t big_tile = (int64_t)kBigBS * 2 * R;
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
-  const int64_t mid_tile = (int64_t)kMidBS * 2 * R;
+  const int64_t mid_tile = (int64_t)kMidBS * 2 * RM;
   const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
   if (fill(big_tpp * n_parts)) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
@@ -477,17 +488,17 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
 #define MID(MAP)                                                                                          \
     do {                                                                                                  \
       if constexpr (FIN)                                                                                  \
-        hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, R, MAP, kMidBS, big_seqf<BE_IN, START>()>), grid, \
+        hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, RM, MAP, kMidBS, mid_seqf<BE_IN, START>()>), grid, \
                            dim3(kMidBS), 0, st, bufs, parts, k, (int)mid_tpp, n_parts, secure, cnts);     \
       else                                                                                                \
-        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, R, true, MAP, kMidBS,                   \
-                                     big_seqf<BE_IN, START>()>),                                          \
+        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, RM, true, MAP, kMidBS,                  \
+                                     mid_seqf<BE_IN, START>()>),                                          \
                            grid, dim3(kMidBS), 0, st, bufs, parts, k, (int)mid_tpp, n_parts);             \
     } while (0)
     if (partial) MID(3);
     else MID(kBigMap);
 #undef MID
-    return launch_info(KER, IPLS_SHAPE_MID, kMidBS, R, big_seqf<BE_IN, START>(), partial ? 3 : kBigMap, grid.x,
+    return launch_info(KER, IPLS_SHAPE_MID, kMidBS, RM, mid_seqf<BE_IN, START>(), partial ? 3 : kBigMap, grid.x,
                        BE_IN, BE_OUT, START);
   } else {
     const int64_t tile = (int64_t)kBlock * 2 * kSmallR;

@@ -367,6 +367,7 @@ def test_publish_partials_batch_matches_single(ipls, O):
         pos += n
     # device memory
     dev = torch.zeros(pos + 64, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()   # torch's stream; the handle's stream does not order after it
     assert agg.publish_partials(parts, 12, bs, origin=origin, out=int(dev.data_ptr())) == (lens, offs)
     agg.sync()
     host = dev.cpu().numpy().tobytes()

@@ -545,6 +545,7 @@ def test_export_import_partial(ipls, O):
     assert_bits_equal(s, O.reduce(own_b, L) + O.reduce(R, L), "replica combine")
     # replace_agg: the partial becomes AGG exactly (FIRST start keeps -0.0)
     neg = torch.full((L,), -0.0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()   # torch's stream; the handle's stream does not order after it
     owner.import_partial(0, neg, replace_agg=True)
     assert np.signbit(owner.read(0)).all()
     for a in [owner, *reps]:
@@ -887,6 +888,7 @@ def test_aggregate_round_big_shape_device_out(ipls, O, shift):
         for k in range(K):
             ipls.synth_fill(rows[p][k], p, k, O.SEED)
     out = torch.full((P * (L - 1) + 2,), 7.0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()   # fills and the poison ran on the null stream; the handle's is non-blocking
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     agg.Update(O.synth_bucket(L, 3, 77), 3, from_clients=False)    # one partition with REP
     agg.aggregate_round(0, rows, out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1)))
@@ -1095,6 +1097,8 @@ def test_maximum_sizes(ipls, O, P, L, K):
     for p in range(P):
         for k in range(K):
             ipls.synth_fill(rows[p][k], p, k, O.SEED)
+    # the fills ran on the null stream; the handle's stream is non-blocking
+    torch.cuda.synchronize()
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
     ref = [O.c_synth_sum_checksum(L, p, K) for p in range(P)]

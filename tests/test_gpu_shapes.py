@@ -2,8 +2,9 @@
 
 The fold kernel's dispatch picks a tile shape by how many tiles a batch fills
 (engine.hip launch_reduce_v: big = 1024 lanes x 16 vectors, mid = 256 lanes x
-16 vectors, small = 256 lanes x 8 peers in flight).  Big-endian input at
-R = 16 runs the hand-fenced SEQ schedule (SEQF = 3), START_ACCUM runs R = 8,
+16 vectors (8 for big-endian input), small = 256 lanes x 8 peers in flight).
+Big-endian input at R = 16 runs the hand-fenced SEQ schedule (SEQF = 3),
+START_ACCUM runs R = 8,
 partial last tiles run map 3.  Every case below asserts through
 ipls_agg_last_launch that it reached the shape it was written for, then
 compares with the oracle: bit for bit on whole partitions (C oracle,
@@ -148,7 +149,7 @@ def test_be_big_shape_partial_tile(ipls, O, be_out):
 @pytest.mark.parametrize("P,L", [(1, 4_194_304 + 4099), (2, 2_100_003)])
 def test_be_mid_shape(ipls, O, P, L):
     """One or two partitions: too few big tiles, so the 256-lane mid shape
-    (SEQF = 3 for BE input) with a partial last tile."""
+    (8 vectors per lane on hipcc's schedule for BE input) with a partial last tile."""
     K = 32
     pool = Pool(ipls, P, L, K, True, O.SEED)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
@@ -156,7 +157,7 @@ def test_be_mid_shape(ipls, O, P, L):
     for start in (ipls.START_ZERO, ipls.START_FIRST):
         agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=start, big_endian_in=True, big_endian_out=True)
         li = agg.last_launch()
-        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_MID, 16, 3, True, True, mapping=3)
+        expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_MID, 8, 0, True, True, mapping=3)
         assert li["block"] == 256
         agg.sync()
         for q in range(P):
@@ -210,8 +211,10 @@ def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
         agg.Update(rep[q], q, from_clients=False)          # Replicas_Gradients = +0.0 + R
     out = agg.aggregate_round(0, pool.rows, big_endian=True)
     li = agg.last_launch()
-    assert (li["kernel"], li["vectors"], li["seqf"], li["be_in"]) == (ipls.KERNEL_ROUND, 16, 3, 1), li
-    assert li["shape"] == (ipls.SHAPE_BIG if P > 1 else ipls.SHAPE_MID) and li["map"] == 3, li
+    big = P > 1
+    assert (li["kernel"], li["vectors"], li["seqf"], li["be_in"]) == \
+        (ipls.KERNEL_ROUND, 16 if big else 8, 3 if big else 0, 1), li
+    assert li["shape"] == (ipls.SHAPE_BIG if big else ipls.SHAPE_MID) and li["map"] == 3, li
     for q in range(P):
         s = ref_sum(O, L, q, K)
         w = s + (0.0 + rep[q])                             # AggregatePartition, IPLS.java:1256

@@ -265,6 +265,23 @@ int main(int argc, char** argv) {
                        },
                        alg, {}});
   }
+  if (getenv("SWEEP_MID")) {   // the mid shape (256 lanes, 1-2 partitions) under the SEQ schedules
+    ADDSB(16, 256, 42);
+    ADDSB(16, 256, 3);
+    ADDSB(16, 256, 2);
+    ADDSB(16, 1024, 42);
+    ADDSB(16, 1024, 3);
+  }
+  if (getenv("SWEEP_P1")) {   // one partition (per-partition flushes, the storage merge): shapes that fill 256 CUs
+    ADDSB(8, 1024, 0);
+    ADDSB(16, 512, 2);
+    ADDSB(16, 512, 3);
+    ADDSB(8, 512, 0);
+    ADDSB(16, 256, 2);
+    ADDSB(16, 256, 3);
+    ADDSB(8, 256, 0);
+    ADDSB(16, 256, 0);
+  }
   if (getenv("SWEEP_BS")) {   // block size / fence interval of the big-endian fold
     ADDSB(16, 1024, 2);
     ADDSB(16, 512, 2);
