@@ -419,6 +419,14 @@ constexpr int big_r() { return START != kAccum ? 16 : 8; }
 // periods >= 5, a free tail on period 3, and period 1 are all slower.
 template <bool BE_IN, int START>
 constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 3 : 0; }
+// Block order of the big shape over whole tiles: partition-major (map 0),
+// except big-endian input on grids of at most 4096 tiles, which runs
+// XCD-chunked (map 2: each XCD walks one contiguous eighth of the work).  With
+// SEQF = 3, map 2 measured +2 to +3.6 points at 2-4 partitions of 4M x 32,
+// +0.2 to +0.6 at 16, and -3.6 at 64 (config D, 8192 tiles); native doubles
+// gain nothing from it (profiles/r02/s3/sweep_be_map.txt, sweep_map_fewp.txt).
+template <bool BE_IN>
+inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMap; }
 // The mid shape (256 lanes, one or two partitions: per-partition flushes, the
 // storage merge of one partition's files) with big-endian input runs 8
 // vectors per lane on hipcc's own schedule (100 VGPRs, no spills): one
@@ -464,9 +472,10 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
   const int64_t mid_tile = (int64_t)kMidBS * 2 * RM;
   const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
   if (fill(big_tpp * n_parts)) {
-    const dim3 grid((unsigned)grid_blocks(kBigMap, big_tpp * n_parts));
     // partial last tiles are scheduled first (map 3, ipls_kernels.hpp map_block)
     const bool partial = big_tpp > 1 && maxL % big_tile != 0;
+    const int map = partial ? 3 : big_map<BE_IN>(big_tpp * n_parts);
+    const dim3 grid((unsigned)grid_blocks(map, big_tpp * n_parts));
 #define BIG(MAP)                                                                                          \
     do {                                                                                                  \
       if constexpr (FIN)                                                                                  \
@@ -477,11 +486,11 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
                                      big_seqf<BE_IN, START>()>),                                          \
                            grid, dim3(kBigBS), 0, st, bufs, parts, k, (int)big_tpp, n_parts);             \
     } while (0)
-    if (partial) BIG(3);
+    if (map == 3) BIG(3);
+    else if (map == 2) BIG(2);
     else BIG(kBigMap);
 #undef BIG
-    return launch_info(KER, IPLS_SHAPE_BIG, kBigBS, R, big_seqf<BE_IN, START>(), partial ? 3 : kBigMap, grid.x,
-                       BE_IN, BE_OUT, START);
+    return launch_info(KER, IPLS_SHAPE_BIG, kBigBS, R, big_seqf<BE_IN, START>(), map, grid.x, BE_IN, BE_OUT, START);
   } else if (fill(mid_tpp * n_parts)) {
     const dim3 grid((unsigned)grid_blocks(kBigMap, mid_tpp * n_parts));
     const bool partial = mid_tpp > 1 && maxL % mid_tile != 0;

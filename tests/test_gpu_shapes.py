@@ -89,7 +89,7 @@ def expect(li, ipls, kernel, shape, vectors, seqf, be_in, be_out, mapping=None):
 def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
     """Config D exactly: 64 partitions x 4,194,304 BE doubles x 32 peers, BE
     sum bytes out -- the shipped big shape with the SEQF = 3 schedule
-    (2048 tiles, no partial tile), ZERO and FIRST start; then BE in with
+    (8192 tiles, no partial tile: partition-major order), ZERO and FIRST start; then BE in with
     native doubles out into the accumulators, and ACCUM (R = 8) on top."""
     m = golden_meta["full"]["D"]
     P, L, K = m["partitions"], m["bucket_len"], m["peers"]
@@ -119,6 +119,31 @@ def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
     for q in (0, 37):
         s = ref_sum(O, L, q, K)
         assert_bits_equal(pool.out_host(q, L, True), ref_sum(O, L, q, K, O.START_ACCUM, s), f"D accum {q}")
+    agg.close()
+    pool.free()
+
+
+def test_be_big_shape_xcd_order(ipls, O):
+    """Big-endian input on a grid of at most 4096 whole tiles runs the big
+    shape XCD-chunked (map 2): 2 x 4M x 32 = 256 tiles, the fold with BE
+    bytes out and the fused round, against the oracle."""
+    P, L, K = 2, 4_194_304, 32
+    pool = Pool(ipls, P, L, K, True, O.SEED)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    refs = [ref_sum(O, L, q, K) for q in range(P)]
+    agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ZERO, big_endian_in=True,
+                         big_endian_out=True)
+    li = agg.last_launch()
+    expect(li, ipls, ipls.KERNEL_REDUCE, ipls.SHAPE_BIG, 16, 3, True, True, mapping=2)
+    assert li["grid"] == P * L // (1024 * 2 * 16), li
+    agg.sync()
+    for q in range(P):
+        assert_bits_equal(pool.out_host(q, L, True), refs[q], f"map 2 partition {q}")
+    out = agg.aggregate_round(0, pool.rows, big_endian=True)
+    expect(agg.last_launch(), ipls, ipls.KERNEL_ROUND, ipls.SHAPE_BIG, 16, 3, True, False, mapping=2)
+    for q in range(P):
+        assert_bits_equal(agg.read(q, ipls.TGT_WEIGHTS), refs[q] + 0.0, f"map 2 W[{q}]")
+        assert_bits_equal(out[q * (L - 1):(q + 1) * (L - 1)], O.c_divide(refs[q] + 0.0), f"map 2 avg[{q}]")
     agg.close()
     pool.free()
 

@@ -332,6 +332,11 @@ int main(int argc, char** argv) {
     ADDS(16, 0, 43);
     ADDS(16, 0, 73);
   }
+  if (getenv("SWEEP_MAP3")) {   // block order under the shipped SEQF = 3 schedule
+    ADDS(16, 0, 3);
+    ADDS(16, 2, 3);
+    ADDS(16, 1, 3);
+  }
   if (getenv("SWEEP_TAIL2")) {   // fence periods 3..8 around the SEQF=3 result
     ADDS(16, 0, 42);
     ADDS(16, 0, 3);
