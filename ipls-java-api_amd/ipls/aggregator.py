@@ -40,7 +40,12 @@ from . import _native as N
 
 @dataclass
 class DeviceBuffer:
-    """A device-resident operand: address, element count, big-endian or not."""
+    """A device-resident operand: address, element count, big-endian or not.
+
+    The handle's HIP stream is non-blocking (include/ipls_agg.h): bytes
+    written by torch or the null stream must be complete before the call
+    that reads them (``torch.cuda.synchronize()``, or an event the handle's
+    stream ``Aggregator.stream`` waits on)."""
     ptr: int
     n: int
     big_endian: bool = False
