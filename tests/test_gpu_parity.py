@@ -1382,7 +1382,7 @@ def test_full_ipls_round_four_peers(ipls, O):
 
 @pytest.mark.parametrize("seed,group,devices", [(1, 1, None), (2, 4, None), (3, 32, None), (4, 2, None), (5, 8, None),
                                                 (6, 4, [0, 0]), (7, 32, [0, 0, 0])])
-def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
+def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, steps=300, shapes=None):
     """A random sequence over the whole accumulator surface, checked step by
     step against a numpy model of the Java state (Aggregated_Gradients,
     Replicas_Gradients, Aggregated_Gradients_from_future, Weights): host and
@@ -1393,7 +1393,9 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
     start-value and grouping rules show in the bits.  ``devices``: the same
     sequence through a multi-device handle (shards [0,2) | [2,4), and a
     three-entry list whose last shard owns no partition), so the front's
-    routing of every call is checked against the same model."""
+    routing of every call is checked against the same model.  ``shapes``: a
+    set that collects the (kernel, shape, map) of every batched launch, for
+    callers that must show which production shapes a sequence reached."""
     rng = np.random.default_rng(seed)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
     agg.set_coalesce(group)
@@ -1419,7 +1421,7 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
     gbuf = np.zeros(L)          # the Updater's one Gradient_Buff (synthetic geometry: L doubles)
     store = {}                  # Other_Replica_Gradients
     msgs = [O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmS")) for g in pool]
-    for step in range(300):
+    for step in range(steps):
         op = int(rng.integers(0, 17))
         p = int(rng.integers(0, P))
         k = int(rng.integers(0, len(pool)))
@@ -1447,6 +1449,9 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
             tg = [ipls.TGT_AGG, ipls.TGT_REP][int(rng.integers(0, 2))]
             agg.reduce_batch(p, [[(DB if be else D)[j] for j in row] for row in ks], start_mode=mode, target=tg,
                              big_endian=be)
+            if shapes is not None:
+                li = agg.last_launch()
+                shapes.add((li["kernel"], li["shape"], li["map"], be))
             for q, row in enumerate(ks):
                 bufs = [pool[j] for j in row]
                 M[T[tg]][p + q] = O.reduce(bufs, L, mode, acc=M[T[tg]][p + q])
@@ -1483,6 +1488,9 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
             kk = int(rng.integers(0, 3))
             ks = [[int(x) for x in rng.integers(0, len(pool), kk)] for _ in range(n)]
             avg = agg.aggregate_round(p, [[D[j] for j in row] for row in ks])
+            if shapes is not None and kk:
+                li = agg.last_launch()
+                shapes.add((li["kernel"], li["shape"], li["map"], False))
             exp = []
             for q, row in enumerate(ks):
                 a = O.reduce([pool[j] for j in row], L, ipls.START_ACCUM, acc=M["agg"][p + q]) if row \
@@ -1526,3 +1534,20 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003):
         for tg in T:
             check(p, tg, "end")
     agg.close()
+
+
+@pytest.mark.parametrize("seed,P,L", [(23, 4, 4 * 1048576 + 5), (22, 1, 4 * 1048576 + 3)])
+def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
+    """The random sequence at config-C bucket lengths (ragged, so every batch
+    ends in a partial tile), so that its batched folds and fused rounds run
+    the production launch shapes -- the big 1024-lane R = 16 / R = 8 tiles
+    and the 256-lane mid shape, native and big-endian, every start mode --
+    interleaved with every other call on the same state.  Four partitions
+    reach the big shape (batches of 2-4 partitions) and the mid one (single
+    partitions); one partition reaches the mid shape only."""
+    shapes = set()
+    test_stateful_random_sequence(ipls, O, seed, 32, None, P=P, L=L, steps=300, shapes=shapes)
+    reduce_shapes = {(s, be) for k, s, _, be in shapes if k == ipls.KERNEL_REDUCE}
+    assert (ipls.SHAPE_MID, False) in reduce_shapes and (ipls.SHAPE_MID, True) in reduce_shapes, shapes
+    if P == 4:
+        assert (ipls.SHAPE_BIG, False) in reduce_shapes and (ipls.SHAPE_BIG, True) in reduce_shapes, shapes
