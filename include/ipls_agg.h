@@ -26,6 +26,8 @@
  *    the Updater thread and the daemon thread concurrently, as the Java code
  *    does under PeerData.mtx (PeerData.java:27).  Calls on one partition
  *    take effect in call order -- the reference's arrival order.
+ *  - Every ipls_agg_* call returns with the calling thread's current HIP
+ *    device unchanged, whichever GPUs the handle's shards live on.
  *  - Arithmetic is IEEE binary64 with no contraction and no reassociation:
  *    each element is folded over the peers in the order given, starting from
  *    +0.0 (or from the first bucket), so results are bit-identical to the

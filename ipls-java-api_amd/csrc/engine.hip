@@ -759,6 +759,18 @@ const char* dev_last_error(const ipls_dev* h) {
 // ipls_agg_last_error(NULL) reads.
 void dev_set_thread_error(const char* msg) { g_tls_err = msg ? msg : ""; }
 
+namespace {
+thread_local int t_dev = -1;   // this thread's current device inside a C-ABI call, -1 = unknown
+}
+hipError_t dev_use(int device) {
+  if (t_dev == device) return hipSuccess;
+  const hipError_t e = hipSetDevice(device);
+  t_dev = e == hipSuccess ? device : -1;
+  return e;
+}
+void dev_track(int device) { t_dev = device; }
+int dev_tracked() { return t_dev; }
+
 int dev_geometry(const ipls_agg_cfg* cfg, std::vector<int64_t>& len, std::vector<int64_t>& off, int64_t& chunk,
                  std::string& why) {
   return partition_geometry(cfg, len, off, chunk, why);
@@ -814,7 +826,7 @@ int dev_open(const ipls_agg_cfg* cfg, int device, int p_lo, int p_hi, ipls_dev**
     dev_close(h);
     return code;
   };
-  if (hipSetDevice(h->device) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipSetDevice(%d) failed", h->device));
+  if (dev_use(h->device) != hipSuccess) return cleanup(fail(nullptr, IPLS_E_DEVICE, "dev_use(%d) failed", h->device));
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(nullptr, IPLS_E_DEVICE, "hipStreamCreate failed"));
   if (h->arena_elems > 0 && hipMalloc(&h->arena, (size_t)h->arena_elems * 8) != hipSuccess) {
@@ -835,7 +847,7 @@ int dev_open(const ipls_agg_cfg* cfg, int device, int p_lo, int p_hi, ipls_dev**
 
 int dev_close(ipls_dev* h) {
   if (!h) return IPLS_OK;
-  hipSetDevice(h->device);
+  dev_use(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   for (auto& s : h->ring) {
     if (s.host) hipHostFree(s.host);
@@ -966,7 +978,7 @@ int end_batch(ipls_dev* h) {
 // batch kernel's table is [partition][peer]).
 int flush_pending(ipls_dev* h) {
   if (h->pend_keys.empty()) return IPLS_OK;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   int rc = IPLS_OK;
   std::vector<int>& keys = h->pend_keys;
   std::sort(keys.begin(), keys.end());   // (target, p) ascending
@@ -1007,7 +1019,7 @@ int dev_reduce_batch(ipls_dev* h, int p_first, int n_parts, const void* const* b
   if (start_mode < IPLS_START_ACCUM || start_mode > IPLS_START_FIRST) return fail(h, IPLS_E_INVAL, "bad start mode");
   if (target_off(h, 0, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (k < 0 || (k > 0 && !bufs)) return fail(h, IPLS_E_INVAL, "bad bucket list");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, target);
 }
 
@@ -1017,7 +1029,7 @@ int dev_accumulate(ipls_dev* h, int p, int target, const void* src, int64_t n, i
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (!src) return IPLS_OK;  // Gradient == null: the Updater loops do nothing (Updater.java:115)
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const int64_t L = h->len[p];
   const void* dptr = nullptr;
   bool be = false, staged = false;
@@ -1125,7 +1137,7 @@ int dev_accumulate_async(ipls_dev* h, int p, int target, const void* src, int64_
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (int rc = host_decode_count(src_kind, n, h->len[p], h)) return rc;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const void* bl[1] = {alias};   // zero copy: the kernel reads the pinned bucket over PCIe
   if (int rc = reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target, nullptr, false, nullptr,
                           true))
@@ -1179,7 +1191,7 @@ int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const int64_t G = h->gbuf_len;
   bool zero_copy = false;
   if (int rc = gbuf_load(h, bytes, n_bytes, &zero_copy)) return rc;
@@ -1201,7 +1213,7 @@ int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** 
   if (!h || !gbuf || !glen) return fail(h, IPLS_E_INVAL, "null argument");
   IPLS_LOCK(h);
   if (n_bytes < 0 || (n_bytes > 0 && !bytes)) return fail(h, IPLS_E_INVAL, "bad byte buffer");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   bool zero_copy = false;
   if (int rc = gbuf_load(h, bytes, n_bytes, &zero_copy)) return rc;
   if (zero_copy) HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -1243,7 +1255,7 @@ int dev_device_ptr(ipls_dev* h, int p, int target, void** ptr) {
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (int rc = materialize(h, p, target)) return rc;
   *ptr = h->arena + target_off(h, p, target);
   return IPLS_OK;
@@ -1256,7 +1268,7 @@ int dev_read(ipls_dev* h, int p, int target, void* dst, int64_t n, int dst_kind)
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   const int64_t L = h->len[p];
   if (n < L) return fail(h, IPLS_E_RANGE, "output of %lld < partition length %lld", (long long)n, (long long)L);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (int rc = materialize(h, p, target)) return rc;
   const double* srcd = h->arena + target_off(h, p, target);
   switch (dst_kind) {
@@ -1287,7 +1299,7 @@ int dev_checksum(ipls_dev* h, int p, int target, uint64_t* out) {
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (int rc = materialize(h, p, target)) return rc;
   HIP_TRY(h, hipMemsetAsync(h->d_sum, 0, 8, h->stream));
   const int64_t L = h->len[p];
@@ -1374,7 +1386,7 @@ int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_ou
   // AGG/REP logically zero, so a rejected call must not get that far
   if (sum_out && sum_kind != IPLS_HOST_F64 && sum_kind != IPLS_HOST_BE)
     return fail(h, IPLS_E_INVAL, "sum_kind must be HOST_F64 or HOST_BE");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (int rc = finalize_range(h, p0, np)) return rc;
 
   if (np == 1 && (sum_out || avg_out)) {
@@ -1419,7 +1431,7 @@ int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind
     if (nd < L)
       return fail(h, IPLS_E_RANGE, "frame payload of %lld doubles < length %lld (IPLS.java:498)", (long long)nd,
                   (long long)L);
-    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, dev_use(h->device));
     if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
     if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
     hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
@@ -1432,7 +1444,7 @@ int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind
   // more than arr.length -> ArrayIndexOutOfBoundsException.
   if (n > L) return fail(h, IPLS_E_RANGE, "downloaded partition of %lld doubles > length %lld", (long long)n, (long long)L);
   if (n <= 0) return IPLS_OK;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   double* w = h->arena + h->w_off[p];
   switch (src_kind) {
     case IPLS_HOST_F64:
@@ -1488,7 +1500,7 @@ int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, i
   if (n < 0 || (n > 0 && !src)) return fail(h, IPLS_E_INVAL, "bad bucket");
   if ((src_kind == IPLS_DEV_F64 || src_kind == IPLS_DEV_BE) && ((uintptr_t)src & 7))
     return fail(h, IPLS_E_INVAL, "device bucket not 8-byte aligned");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   auto key = std::make_pair(p, aggregator);
   auto it = h->other.find(key);
   const bool first = it == h->other.end();
@@ -1524,7 +1536,7 @@ int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, i
 int dev_collect_replicas(ipls_dev* h, int32_t* participants) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   // REP[p] is a double[L_p]: a longer stored array overruns it (IPLS.java:1225).
   for (auto& kv : h->other)
     if (kv.second.n > h->len[kv.first.first])
@@ -1559,7 +1571,7 @@ int dev_load_model(ipls_dev* h, const void* src, int64_t n, int src_kind) {
   IPLS_LOCK(h);
   if (n < h->flat_total)
     return fail(h, IPLS_E_RANGE, "model of %lld values < model size %lld", (long long)n, (long long)h->flat_total);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const unsigned long long* d;
   bool be;
   // only this engine's segment [flat_base, flat_total) of the model
@@ -1600,7 +1612,7 @@ int dev_split(ipls_dev* h, const void* flat, int64_t n, int src_kind, int p, voi
   if (int rc = check_part(h, p)) return rc;
   int64_t ncopy;
   if (int rc = split_bounds(h, p, n, &ncopy)) return rc;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const int64_t L = h->len[p];
   const unsigned long long* d;
   bool be_in;
@@ -1651,7 +1663,7 @@ int dev_update_gradient(ipls_dev* h, const void* flat, int64_t n, int src_kind, 
   for (int i = 0; i < n_owned; ++i)
     if (int rc = check_part(h, owned[i])) return rc;
   if (n_owned == 0) return IPLS_OK;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const unsigned long long* d;
   bool be;
   // only this engine's segment of the gradient vector (flat_base on)
@@ -1685,7 +1697,7 @@ int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind) {
   if (n < M) return fail(h, IPLS_E_RANGE, "output of %lld < model size %lld", (long long)n, (long long)M);
   if (out_kind != IPLS_HOST_F64 && out_kind != IPLS_HOST_BE_CANON && out_kind != IPLS_DEV_F64)
     return fail(h, IPLS_E_INVAL, "bad out_kind %d", out_kind);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   unsigned long long* d_out;
   if (out_kind == IPLS_DEV_F64) {
     if ((uintptr_t)out & 7) return fail(h, IPLS_E_INVAL, "device output not 8-byte aligned");
@@ -1756,7 +1768,7 @@ int dev_reduce_batch_out(ipls_dev* h, int p_first, int n_parts, const void* cons
     return fail(h, IPLS_E_INVAL, "reduce_batch_out writes device buffers (DEV_F64/DEV_BE)");
   if (start_mode < IPLS_START_ACCUM || start_mode > IPLS_START_FIRST) return fail(h, IPLS_E_INVAL, "bad start mode");
   if (!dst || k < 0 || (k > 0 && !bufs)) return fail(h, IPLS_E_INVAL, "bad bucket/destination list");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   return reduce_dev(h, p_first, n_parts, bufs, k, src_kind == IPLS_DEV_BE, start_mode, IPLS_TGT_AGG, dst,
                     dst_kind == IPLS_DEV_BE);
 }
@@ -1772,7 +1784,7 @@ int dev_aggregate_round(ipls_dev* h, int p_first, int n_parts, const void* const
   if (avg_out && avg_kind != IPLS_DEV_F64 && avg_kind != IPLS_HOST_F64)
     return fail(h, IPLS_E_INVAL, "avg_kind must be DEV_F64 or HOST_F64");
   if (k < 0 || (k > 0 && !bufs)) return fail(h, IPLS_E_INVAL, "bad bucket list");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const int p_last = p_first + n_parts - 1;
   const int64_t n_avg = h->flat_off[p_last] + h->len[p_last] - 1 - h->flat_off[p_first];
   unsigned long long* d_avg = nullptr;
@@ -1833,7 +1845,7 @@ int dev_ingest_pubsub(ipls_dev* h, int target, const uint8_t* const* msgs, const
   if (layers < 1 || layers > 2) return fail(h, IPLS_E_INVAL, "layers must be 1 or 2");
   if (target_off(h, 0, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   if (n_msgs == 0) return 0;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
 
   // 1. host: tail rules, frame header, routing (GET_GRADIENTS, MyIPFSClass.java:1437-1459).
   //    post[i] = the status if the device finds no invalid char; decode[i] = needs the device.
@@ -1901,7 +1913,7 @@ int dev_ingest_pubsub(ipls_dev* h, int target, const uint8_t* const* msgs, const
     std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[n_dec]);   // 0 pending, 1 recorded, <0 error
     for (int j = 0; j < n_dec; ++j) ready[j].store(0);
     auto copier = [&](int t) {
-      hipSetDevice(h->device);
+      dev_use(h->device);
       for (int j = t; j < n_dec; j += T) {
         const int i = order[j];
         hipError_t e = hipMemcpyAsync(base + text_off[i], msgs[i], lens[i], hipMemcpyHostToDevice, h->copy_stream[t]);
@@ -1965,7 +1977,7 @@ int dev_blend(ipls_dev* h, int p, int target, const void* src, int64_t n, int sr
   if (!src) return IPLS_OK;
   const int64_t L = h->len[p];
   if (n < L) return fail(h, IPLS_E_RANGE, "bucket of %lld doubles shorter than partition length %lld", (long long)n, (long long)L);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   const void* d = src;
   bool be = src_kind == IPLS_HOST_BE || src_kind == IPLS_DEV_BE;
   if (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE) {
@@ -1989,7 +2001,7 @@ int dev_scale(ipls_dev* h, int p, int dst_target, int src_target, double c) {
   IPLS_LOCK(h);
   if (int rc = check_part(h, p)) return rc;
   if (target_off(h, p, dst_target) < 0 || target_off(h, p, src_target) < 0) return fail(h, IPLS_E_INVAL, "bad target");
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (int rc = materialize(h, p, src_target)) return rc;
   if (uint8_t* f = zero_flag(h, p, dst_target)) *f = 0;
   const int64_t L = h->len[p];
@@ -2098,7 +2110,7 @@ int64_t dev_commit_partial(ipls_dev* h, int p, int32_t workers, uint8_t* out, in
   const int64_t hl = javaser::pair_header_len(), total = hl + 8 * L + javaser::pair_trailer_len();
   if (!out) return total;
   if (out_cap < total) return fail(h, IPLS_E_RANGE, "partial update needs %lld bytes", (long long)total);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   javaser::write_pair_header(out, workers, (int32_t)L);
   if (h->agg_zero[p]) {
     std::memset(out + hl, 0, (size_t)L * 8);   // +0.0 in any byte order
@@ -2140,7 +2152,7 @@ int64_t dev_merge_files(ipls_dev* h, const uint8_t* const* files, const int64_t*
   const int64_t n0 = nd[0];
   if (out_cap < 8 * n0 || (!out && n0 > 0)) return fail(h, IPLS_E_RANGE, "merge output needs %lld bytes", (long long)(8 * n0));
   if (n0 == 0) return 0;
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (h->merge_cap < n0) {
     if (h->d_merge) {
       HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -2225,7 +2237,7 @@ int64_t dev_publish(ipls_dev* h, int p, int target, int32_t a, int32_t b, int16_
   const int64_t T = pubsub::b64_enc_len(F);
   if (!out) return T;
   if (out_cap < T) return fail(h, IPLS_E_RANGE, "publish text needs %lld bytes", (long long)T);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   FrameEnc fe{};
   const uint32_t hv[3] = {(uint32_t)n, (uint32_t)a, (uint32_t)b};
   fe.hdr[0] = (unsigned char)((uint16_t)pid >> 8);   // putShort(0, pid)
@@ -2281,7 +2293,7 @@ int64_t dev_publish_many(ipls_dev* h, int n, const int* parts, int target, int32
     if (int rc = check_part(h, parts[i])) return rc;
     if (target_off(h, parts[i], target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
   }
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   if (out_kind == IPLS_DEV_TEXT && !kernel_writable(out))
     return fail(h, IPLS_E_INVAL, "DEV_TEXT output is neither device memory nor pinned host memory");
   const unsigned char* dorig = nullptr;
@@ -2355,7 +2367,7 @@ int dev_reduce_ext(ipls_dev* h, int n, const int64_t* lens, const void* const* b
                    int start_mode, void* const* dst) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
-  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, dev_use(h->device));
   return reduce_dev(h, 0, n, bufs, k, be_in, start_mode, IPLS_TGT_AGG, dst, false, nullptr, false, lens);
 }
 

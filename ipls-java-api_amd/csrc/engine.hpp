@@ -11,12 +11,23 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../include/ipls_agg.h"
 
 struct ipls_dev;
 
 const char* dev_last_error(const ipls_dev* h);
 void dev_set_thread_error(const char* msg);
+// The calling thread's current HIP device, tracked while a C-ABI call runs so
+// that switching to a device that is already current costs no HIP call:
+// dev_use(d) makes d current (hipSetDevice only when the tracked device
+// differs); dev_track(d) records what the thread's device is (-1: unknown,
+// every dev_use then sets it); dev_tracked() returns the record.  Every device
+// switch on a calling thread goes through dev_use, so the record stays exact.
+hipError_t dev_use(int device);
+void dev_track(int device);
+int dev_tracked();
 int dev_geometry(const ipls_agg_cfg* cfg, std::vector<int64_t>& len, std::vector<int64_t>& off, int64_t& chunk,
                  std::string& why);
 int dev_open(const ipls_agg_cfg* cfg, int device, int p_lo, int p_hi, ipls_dev** out);

@@ -103,6 +103,27 @@ T fwd(ipls_agg* H, int s, T rc) {
   return rc;
 }
 
+// Every entry point leaves the calling thread's current HIP device as it
+// found it: the engines switch devices internally (one per shard), and a
+// caller that also drives the GPU (torch, another library) must not find its
+// device changed behind its back.
+struct KeepDevice {
+  int d = -1;
+  KeepDevice() {
+    if (hipGetDevice(&d) != hipSuccess) {
+      (void)hipGetLastError();
+      d = -1;
+    }
+    dev_track(d);
+  }
+  ~KeepDevice() {
+    if (d >= 0 && dev_tracked() != d && hipSetDevice(d) != hipSuccess) (void)hipGetLastError();
+    dev_track(-1);   // outside a call the caller may switch devices on its own
+  }
+  KeepDevice(const KeepDevice&) = delete;
+  KeepDevice& operator=(const KeepDevice&) = delete;
+};
+
 bool part_ok(const ipls_agg* H, int p) { return p >= 0 && p < H->P; }
 
 int range_err(ipls_agg* H, int p) { return ferr(H, IPLS_E_RANGE, "partition %d out of range [0,%d)", p, H->P); }
@@ -149,8 +170,8 @@ int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
 // Order shard b's stream after the work queued so far on shard a's stream.
 int order_after(ipls_agg* H, int a, int b) {
   if (a == b) return IPLS_OK;
-  if (hipSetDevice(H->devices[a]) != hipSuccess || hipEventRecord(H->xev[a], (hipStream_t)dev_stream(H->sh[a])) != hipSuccess ||
-      hipSetDevice(H->devices[b]) != hipSuccess ||
+  if (dev_use(H->devices[a]) != hipSuccess || hipEventRecord(H->xev[a], (hipStream_t)dev_stream(H->sh[a])) != hipSuccess ||
+      dev_use(H->devices[b]) != hipSuccess ||
       hipStreamWaitEvent((hipStream_t)dev_stream(H->sh[b]), H->xev[a], 0) != hipSuccess) {
     (void)hipGetLastError();
     return ferr(H, IPLS_E_DEVICE, "cross-shard stream ordering failed");
@@ -191,6 +212,7 @@ int ipls_shard_plan(int32_t n_partitions, int32_t n_shards, int32_t* owner) {
 }
 
 int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
+  KeepDevice keep_device;
   if (!cfg || !out) return ferr(nullptr, IPLS_E_INVAL, "null cfg/out");
   *out = nullptr;
   if (cfg->n_partitions <= 0) return ferr(nullptr, IPLS_E_INVAL, "n_partitions must be > 0 (-pa)");
@@ -238,7 +260,7 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
       destroy(H);
       return ferr(nullptr, rc, "shard %d (device %d): %s", s, devs[s], m.c_str());
     }
-    if (hipSetDevice(devs[s]) != hipSuccess || hipEventCreateWithFlags(&H->xev[s], hipEventDisableTiming) != hipSuccess) {
+    if (dev_use(devs[s]) != hipSuccess || hipEventCreateWithFlags(&H->xev[s], hipEventDisableTiming) != hipSuccess) {
       (void)hipGetLastError();
       destroy(H);
       return ferr(nullptr, IPLS_E_DEVICE, "event creation on device %d failed", devs[s]);
@@ -253,7 +275,7 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
       int can = 0;
       if (hipDeviceCanAccessPeer(&can, devs[a], devs[b]) != hipSuccess) can = 0;
       if (can) {
-        hipSetDevice(devs[a]);
+        dev_use(devs[a]);
         const hipError_t e = hipDeviceEnablePeerAccess(devs[b], 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) can = 0;
       }
@@ -265,6 +287,7 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
 }
 
 int ipls_agg_close(ipls_agg* h) {
+  KeepDevice keep_device;
   if (!h) return IPLS_OK;
   destroy(h);
   return IPLS_OK;
@@ -287,6 +310,7 @@ int ipls_agg_partition_offset(const ipls_agg* h, int p, int64_t* off) {
 }
 
 int ipls_agg_partition_device(ipls_agg* H, int p, int32_t* device, void** stream) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   const int s = H->owner[p];
@@ -298,6 +322,7 @@ int ipls_agg_partition_device(ipls_agg* H, int p, int32_t* device, void** stream
 void* ipls_agg_stream(ipls_agg* H) { return H ? dev_stream(H->sh[0]) : nullptr; }
 
 int ipls_agg_sync(ipls_agg* H) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   std::vector<int> all(H->S());
   for (int s = 0; s < H->S(); ++s) all[s] = s;
@@ -305,6 +330,7 @@ int ipls_agg_sync(ipls_agg* H) {
 }
 
 int ipls_agg_flush(ipls_agg* H) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   for (int s = 0; s < H->S(); ++s)
     if (int rc = fwd(H, s, dev_flush(H->sh[s]))) return rc;
@@ -312,6 +338,7 @@ int ipls_agg_flush(ipls_agg* H) {
 }
 
 int ipls_agg_set_coalesce(ipls_agg* H, int max_group) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   for (int s = 0; s < H->S(); ++s)
     if (int rc = fwd(H, s, dev_set_coalesce(H->sh[s], max_group))) return rc;
@@ -319,11 +346,13 @@ int ipls_agg_set_coalesce(ipls_agg* H, int max_group) {
 }
 
 int ipls_agg_last_launch(ipls_agg* H, ipls_launch_info* out) {
+  KeepDevice keep_device;
   if (!H || !out) return ferr(H, IPLS_E_INVAL, "null argument");
   return dev_last_launch(H->sh[H->last_shard], out);
 }
 
 int ipls_agg_load_model(ipls_agg* H, const void* src, int64_t n, int src_kind) {
+  KeepDevice keep_device;
   if (!H || !src) return ferr(H, IPLS_E_INVAL, "null argument");
   if (H->S() == 1) return fwd(H, 0, dev_load_model(H->sh[0], src, n, src_kind));
   if (n < H->flat_total)
@@ -332,6 +361,7 @@ int ipls_agg_load_model(ipls_agg* H, const void* src, int64_t n, int src_kind) {
 }
 
 int ipls_agg_split(ipls_agg* H, const void* flat, int64_t n, int src_kind, int p, void* dst, int dst_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -341,6 +371,7 @@ int ipls_agg_split(ipls_agg* H, const void* flat, int64_t n, int src_kind, int p
 
 int ipls_agg_update_gradient(ipls_agg* H, const void* flat, int64_t n, int src_kind, const int32_t* owned,
                              int n_owned) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_update_gradient(H->sh[0], flat, n, src_kind, owned, n_owned));
   if (!flat) return IPLS_OK;   // Gradients == null (IPLS.java:1708-1713)
@@ -366,6 +397,7 @@ int ipls_agg_update_gradient(ipls_agg* H, const void* flat, int64_t n, int src_k
 }
 
 int ipls_agg_accumulate(ipls_agg* H, int p, int target, const void* src, int64_t n, int src_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -375,6 +407,7 @@ int ipls_agg_accumulate(ipls_agg* H, int p, int target, const void* src, int64_t
 
 int ipls_agg_accumulate_async(ipls_agg* H, int p, int target, const void* src, int64_t n, int src_kind,
                               uint64_t* ticket) {
+  KeepDevice keep_device;
   if (!H || !ticket) return ferr(H, IPLS_E_INVAL, "null argument");
   if (H->S() == 1) return fwd(H, 0, dev_accumulate_async(H->sh[0], p, target, src, n, src_kind, ticket));
   if (!part_ok(H, p)) return range_err(H, p);
@@ -399,6 +432,7 @@ int ipls_agg_accumulate_async(ipls_agg* H, int p, int target, const void* src, i
 }
 
 int ipls_agg_wait(ipls_agg* H, uint64_t ticket) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_wait(H->sh[0], ticket));
   std::vector<std::pair<int, uint64_t>> w;   // (shard, newest engine ticket issued at or before `ticket`)
@@ -420,6 +454,7 @@ int ipls_agg_wait(ipls_agg* H, uint64_t ticket) {
 }
 
 int ipls_agg_update_indirect(ipls_agg* H, int p, int target, const void* bytes, int64_t n_bytes) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -439,6 +474,7 @@ int ipls_agg_update_indirect(ipls_agg* H, int p, int target, const void* bytes, 
 }
 
 int ipls_agg_other_replica(ipls_agg* H, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -447,6 +483,7 @@ int ipls_agg_other_replica(ipls_agg* H, int p, int32_t aggregator, const void* s
 }
 
 int ipls_agg_collect_replicas(ipls_agg* H, int32_t* participants) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_collect_replicas(H->sh[0], participants));
   const std::vector<int> ss = nonempty_shards(H);
@@ -471,6 +508,7 @@ int ipls_agg_collect_replicas(ipls_agg* H, int32_t* participants) {
 
 int ipls_agg_reduce_batch(ipls_agg* H, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                           int start_mode, int target) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_reduce_batch(H->sh[0], p_first, n_parts, bufs, k, src_kind, start_mode, target));
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > H->P)
@@ -488,6 +526,7 @@ int ipls_agg_reduce_batch(ipls_agg* H, int p_first, int n_parts, const void* con
 
 int ipls_agg_reduce_batch_out(ipls_agg* H, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                               int start_mode, void* const* dst, int dst_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1)
     return fwd(H, 0, dev_reduce_batch_out(H->sh[0], p_first, n_parts, bufs, k, src_kind, start_mode, dst, dst_kind));
@@ -506,6 +545,7 @@ int ipls_agg_reduce_batch_out(ipls_agg* H, int p_first, int n_parts, const void*
 
 int ipls_agg_aggregate_round(ipls_agg* H, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                              void* avg_out, int avg_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1)
     return fwd(H, 0, dev_aggregate_round(H->sh[0], p_first, n_parts, bufs, k, src_kind, avg_out, avg_kind));
@@ -529,6 +569,7 @@ int ipls_agg_aggregate_round(ipls_agg* H, int p_first, int n_parts, const void* 
 
 int ipls_agg_ingest_pubsub(ipls_agg* H, int target, const uint8_t* const* msgs, const int64_t* lens, int n_msgs,
                            int layers, const int32_t* parts, int32_t* status) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_ingest_pubsub(H->sh[0], target, msgs, lens, n_msgs, layers, parts, status));
   if (n_msgs < 0 || (n_msgs > 0 && (!msgs || !lens))) return ferr(H, IPLS_E_INVAL, "bad message list");
@@ -581,6 +622,7 @@ int ipls_agg_ingest_pubsub(ipls_agg* H, int target, const uint8_t* const* msgs, 
 }
 
 int ipls_agg_blend(ipls_agg* H, int p, int target, const void* src, int64_t n, int src_kind, double a, double b) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -589,6 +631,7 @@ int ipls_agg_blend(ipls_agg* H, int p, int target, const void* src, int64_t n, i
 }
 
 int ipls_agg_scale(ipls_agg* H, int p, int dst_target, int src_target, double c) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -597,6 +640,7 @@ int ipls_agg_scale(ipls_agg* H, int p, int dst_target, int src_target, double c)
 }
 
 int ipls_agg_finalize(ipls_agg* H, int p, void* sum_out, int sum_kind, double* avg_out) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_finalize(H->sh[0], p, sum_out, sum_kind, avg_out));
   if (p == IPLS_ALL_PARTITIONS) {
@@ -612,6 +656,7 @@ int ipls_agg_finalize(ipls_agg* H, int p, void* sum_out, int sum_kind, double* a
 }
 
 int ipls_agg_set_weights(ipls_agg* H, int p, const void* src, int64_t n, int src_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -620,6 +665,7 @@ int ipls_agg_set_weights(ipls_agg* H, int p, const void* src, int64_t n, int src
 }
 
 int ipls_agg_get_partitions(ipls_agg* H, void* out, int64_t n, int out_kind) {
+  KeepDevice keep_device;
   if (!H || !out) return ferr(H, IPLS_E_INVAL, "null argument");
   if (H->S() == 1) return fwd(H, 0, dev_get_partitions(H->sh[0], out, n, out_kind));
   if (n < H->flat_total)
@@ -634,6 +680,7 @@ int ipls_agg_get_partitions(ipls_agg* H, void* out, int64_t n, int out_kind) {
 }
 
 int ipls_agg_read(ipls_agg* H, int p, int target, void* dst, int64_t n, int dst_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -642,6 +689,7 @@ int ipls_agg_read(ipls_agg* H, int p, int target, void* dst, int64_t n, int dst_
 }
 
 int ipls_agg_promote_future(ipls_agg* H, const int32_t* parts, int n_parts) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_promote_future(H->sh[0], parts, n_parts));
   if (n_parts < 0 || (n_parts > 0 && !parts)) return ferr(H, IPLS_E_INVAL, "bad partition list");
@@ -656,6 +704,7 @@ int ipls_agg_promote_future(ipls_agg* H, const int32_t* parts, int n_parts) {
 }
 
 int ipls_agg_reset(ipls_agg* H, int p) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (H->S() == 1) return fwd(H, 0, dev_reset(H->sh[0], p));
   if (p == IPLS_ALL_PARTITIONS) {
@@ -670,6 +719,7 @@ int ipls_agg_reset(ipls_agg* H, int p) {
 }
 
 int ipls_agg_device_ptr(ipls_agg* H, int p, int target, void** ptr) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -678,6 +728,7 @@ int ipls_agg_device_ptr(ipls_agg* H, int p, int target, void** ptr) {
 }
 
 int ipls_agg_checksum(ipls_agg* H, int p, int target, uint64_t* out) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -686,6 +737,7 @@ int ipls_agg_checksum(ipls_agg* H, int p, int target, uint64_t* out) {
 }
 
 int64_t ipls_agg_commit_partial(ipls_agg* H, int p, int32_t workers, uint8_t* out, int64_t out_cap) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -695,6 +747,7 @@ int64_t ipls_agg_commit_partial(ipls_agg* H, int p, int32_t workers, uint8_t* ou
 
 int64_t ipls_agg_merge_files(ipls_agg* H, const uint8_t* const* files, const int64_t* lens, int k, int file_kind,
                              uint8_t* out, int64_t out_cap) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   return fwd(H, 0, dev_merge_files(H->sh[0], files, lens, k, file_kind, out, out_cap));
 }
@@ -702,6 +755,7 @@ int64_t ipls_agg_merge_files(ipls_agg* H, const uint8_t* const* files, const int
 int64_t ipls_agg_publish_partial(ipls_agg* H, int p, int target, int32_t a, int32_t b, int16_t pid,
                                  const uint8_t* origin, int32_t origin_len, void* out, int64_t out_cap,
                                  int out_kind) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
@@ -712,6 +766,7 @@ int64_t ipls_agg_publish_partial(ipls_agg* H, int p, int target, int32_t a, int3
 int64_t ipls_agg_publish_partials(ipls_agg* H, const int32_t* parts, int n_parts, int target, int32_t a,
                                   const int32_t* b, int16_t pid, const uint8_t* origin, int32_t origin_len, void* out,
                                   int64_t out_cap, int out_kind, int64_t* lens, int64_t* offs) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (n_parts < 0 || (n_parts > 0 && (!parts || (out && !b)))) return ferr(H, IPLS_E_INVAL, "bad partition list");
   if (origin_len < 0 || (out && origin_len > 0 && !origin)) return ferr(H, IPLS_E_INVAL, "bad origin");
@@ -768,6 +823,7 @@ int64_t ipls_agg_publish_partials(ipls_agg* H, const int32_t* parts, int n_parts
 
 int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, const void* const* bufs, int k,
                             int src_kind, int start_mode) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (slot < 0 || slot >= H->S()) return ferr(H, IPLS_E_INVAL, "slot %d not in [0,%d)", slot, H->S());
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > H->P)
@@ -783,7 +839,7 @@ int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, con
   auto& row = H->part[slot];
   if (row.empty()) row.resize(H->P);
   hipStream_t st = (hipStream_t)dev_stream(H->sh[slot]);
-  if (hipSetDevice(H->devices[slot]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
+  if (dev_use(H->devices[slot]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
   std::vector<void*> dst(n_parts);
   std::vector<int64_t> lens(n_parts);
   int n_live = 0;
@@ -795,9 +851,9 @@ int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, con
       const int od = H->devices[H->owner[p_first + q]];
       const bool ok = hipMalloc(&x.d, (size_t)H->len[p_first + q] * 8) == hipSuccess &&
                       hipEventCreateWithFlags(&x.ready, hipEventDisableTiming) == hipSuccess &&
-                      hipSetDevice(od) == hipSuccess &&
+                      dev_use(od) == hipSuccess &&
                       hipEventCreateWithFlags(&x.consumed, hipEventDisableTiming) == hipSuccess;
-      if (hipSetDevice(H->devices[slot]) != hipSuccess || !ok) {
+      if (dev_use(H->devices[slot]) != hipSuccess || !ok) {
         (void)hipGetLastError();
         return ferr(H, IPLS_E_NOMEM, "partial buffer of partition %d on device %d", p_first + q, H->devices[slot]);
       }
@@ -824,7 +880,7 @@ int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, con
   if (int rc = fwd(H, slot, dev_reduce_ext(H->sh[slot], n_parts, lens.data(), bufs, k, src_kind == IPLS_DEV_BE, start,
                                            dst.data())))
     return rc;
-  if (hipSetDevice(H->devices[slot]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
+  if (dev_use(H->devices[slot]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
   for (int q = 0; q < n_parts; ++q) {
     Partial& x = row[p_first + q];
     if (hipEventRecord(x.ready, st) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipEventRecord failed");
@@ -834,6 +890,7 @@ int ipls_agg_reduce_partial(ipls_agg* H, int slot, int p_first, int n_parts, con
 }
 
 int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
+  KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > H->P)
     return ferr(H, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, H->P);
@@ -857,7 +914,7 @@ int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
     }
     if (!slots.empty()) {
       hipStream_t ost = (hipStream_t)dev_stream(H->sh[o]);
-      if (hipSetDevice(H->devices[o]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
+      if (dev_use(H->devices[o]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
       const int k = (int)slots.size();
       std::vector<const void*> ptrs((size_t)(e - p) * k);
       for (int q = p; q < e; ++q)
@@ -876,7 +933,7 @@ int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
       if (int rc = fwd(H, o, dev_reduce_batch(H->sh[o], p - H->lo[o], e - p, ptrs.data(), k, IPLS_DEV_F64,
                                               IPLS_START_ACCUM, IPLS_TGT_REP)))
         return rc;
-      if (hipSetDevice(H->devices[o]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
+      if (dev_use(H->devices[o]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
       for (int q = p; q < e; ++q)
         for (int s : slots) {
           Partial& x = H->part[s][q];

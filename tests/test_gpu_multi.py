@@ -391,3 +391,29 @@ def test_publish_partials_batch_matches_single(ipls, O):
     assert lib.ipls_agg_publish_partials(agg.handle, pa.ctypes.data, len(parts), N.TGT_AGG, 12, ba.ctypes.data, 3,
                                          None, 0, buf.ctypes.data, 10, N.HOST_TEXT, None, None) == N.IPLS_E_RANGE
     agg.close()
+
+
+def test_calls_keep_the_callers_current_device(ipls, O):
+    """Every C-ABI call returns with the caller's current HIP device as it
+    found it (include/ipls_agg.h conventions): a handle whose shards live on
+    other GPUs must not switch a torch caller's device.  On a one-GPU box the
+    handle runs over [0, 0] (shards still switch devices internally); with
+    two or more GPUs the handle lives on the last device while the caller
+    stays on device 0."""
+    n = torch.cuda.device_count()
+    devs = [0, 0] if n < 2 else [n - 1, n - 1]
+    torch.cuda.set_device(0)
+    before = torch.cuda.current_device()
+    P, L, K = 4, 5003, 3
+    with ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devs) as agg:
+        assert torch.cuda.current_device() == before
+        g = O.synth_bucket(L, 0, 0)
+        agg.Update(g, 0, from_clients=True)
+        agg.Update(O.be_encode(g), P - 1, from_clients=True)
+        agg.AggregatePartition(ipls.ALL_PARTITIONS)
+        avg = agg.GetPartitions()
+        agg.sync()
+        assert torch.cuda.current_device() == before
+    assert torch.cuda.current_device() == before
+    ref = O.get_partitions([O.reduce([g], L) if p in (0, P - 1) else np.zeros(L) for p in range(P)])
+    assert_bits_equal(avg, ref, "model")
