@@ -125,7 +125,10 @@ int ipls_agg_open(const ipls_agg_cfg *cfg, ipls_agg **out);
 /* Free everything.  NULL is accepted. */
 int ipls_agg_close(ipls_agg *h);
 
-/* Message of the last failure on h (h == NULL: last failure of this thread). */
+/* Message of the last failure on h (h == NULL: last failure of this thread).
+ * Right after a call fails, ipls_agg_last_error(NULL) is that call's message
+ * even while other threads use the same handle.  The string belongs to the
+ * calling thread and stays valid until its next ipls_agg_last_error call. */
 const char *ipls_agg_last_error(const ipls_agg *h);
 
 /* Partition length incl. the count slot: IPLS.java:1019-1028. */

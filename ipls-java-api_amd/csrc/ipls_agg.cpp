@@ -53,7 +53,7 @@ struct Partial {
 
 struct ipls_agg {
   std::mutex mu;       // front bookkeeping only (tickets, partials); never held across a host wait
-  std::mutex err_mu;
+  mutable std::mutex err_mu;
   std::string err;
   int P = 0;
   int64_t chunk = 0, flat_total = 0;
@@ -91,15 +91,20 @@ int ferr(ipls_agg* H, int code, const char* fmt, ...) {
   return code;
 }
 
-// An engine call's failure becomes the handle's last error.
-template <class T>
-T fwd(ipls_agg* H, int s, T rc) {
-  if (rc < 0) {
-    const char* m = dev_last_error(H->sh[s]);
+// An engine call's failure becomes the handle's last error.  The engine left
+// its message in this thread's slot (the engine's own copy may already hold
+// another caller's failure on the same shard).
+void set_err(ipls_agg* H, const std::string& m) {
+  {
     std::lock_guard<std::mutex> lk(H->err_mu);
     H->err = m;
-    dev_set_thread_error(m);
   }
+  dev_set_thread_error(m.c_str());
+}
+template <class T>
+T fwd(ipls_agg* H, int s, T rc) {
+  (void)s;
+  if (rc < 0) set_err(H, dev_last_error(nullptr));
   return rc;
 }
 
@@ -158,12 +163,21 @@ int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
     return IPLS_OK;
   }
   std::vector<int> rc(ss.size(), 0);
+  std::vector<std::string> msg(ss.size());   // a worker's message lives in the worker's thread slot
   std::vector<std::thread> th;
-  for (size_t i = 1; i < ss.size(); ++i) th.emplace_back([&, i] { rc[i] = fn(ss[i]); });
+  for (size_t i = 1; i < ss.size(); ++i)
+    th.emplace_back([&, i] {
+      rc[i] = fn(ss[i]);
+      if (rc[i] < 0) msg[i] = dev_last_error(nullptr);
+    });
   rc[0] = fn(ss[0]);
+  if (rc[0] < 0) msg[0] = dev_last_error(nullptr);
   for (auto& t : th) t.join();
   for (size_t i = 0; i < ss.size(); ++i)
-    if (rc[i] < 0) return fwd(H, ss[i], rc[i]);
+    if (rc[i] < 0) {
+      set_err(H, msg[i]);
+      return rc[i];
+    }
   return IPLS_OK;
 }
 
@@ -200,8 +214,15 @@ extern "C" {
 int ipls_agg_abi_version(void) { return IPLS_AGG_ABI_VERSION; }
 
 const char* ipls_agg_last_error(const ipls_agg* h) {
-  if (h) return h->err.c_str();
-  return dev_last_error(nullptr);
+  if (!h) return dev_last_error(nullptr);
+  // a snapshot per calling thread: another thread's failure on the same handle
+  // may replace h->err while this caller still reads the returned string
+  thread_local std::string snap;
+  {
+    std::lock_guard<std::mutex> lk(h->err_mu);
+    snap = h->err;
+  }
+  return snap.c_str();
 }
 
 int ipls_shard_plan(int32_t n_partitions, int32_t n_shards, int32_t* owner) {

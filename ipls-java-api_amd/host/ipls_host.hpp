@@ -58,7 +58,8 @@ IPLS_HOST_EXC(DeviceError, "ipls.DeviceError")
 #undef IPLS_HOST_EXC
 
 [[noreturn]] inline void raise(int rc, const ipls_agg* h) {
-  const std::string msg = ipls_agg_last_error(h);
+  (void)h;
+  const std::string msg = ipls_agg_last_error(nullptr);   // this thread's failure
   switch (rc) {
     case IPLS_E_RANGE: throw ArrayIndexOutOfBoundsException(rc, msg);
     case IPLS_E_NEGSIZE: throw NegativeArraySizeException(rc, msg);
@@ -471,7 +472,7 @@ class UpdaterThread {
             lk.unlock();
             const int rc = ipls_agg_flush(ipls_.handle());
             lk.lock();
-            if (rc < 0) failures_.push_back(ipls_agg_last_error(ipls_.handle()));
+            if (rc < 0) failures_.push_back(ipls_agg_last_error(nullptr));
           }
           cv_.wait(lk, ready);
         }
@@ -508,7 +509,7 @@ class UpdaterThread {
         const int rc = ipls_agg_flush(ipls_.handle());
         std::lock_guard<std::mutex> lk(mu_);
         ++hint_flushes_;
-        if (rc < 0) failures_.push_back(ipls_agg_last_error(ipls_.handle()));
+        if (rc < 0) failures_.push_back(ipls_agg_last_error(nullptr));
       }
       {
         std::lock_guard<std::mutex> lk(mu_);

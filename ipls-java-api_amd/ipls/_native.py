@@ -161,5 +161,6 @@ def last_error(h=None) -> str:
 
 def check(rc: int, h=None) -> int:
     if rc < 0:
-        raise IplsError(rc, last_error(h))
+        # this thread's failure: another thread may already have failed on h since
+        raise IplsError(rc, last_error(None))
     return rc

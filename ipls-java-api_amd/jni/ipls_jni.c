@@ -38,7 +38,8 @@ static void throw_for(JNIEnv *env, int rc, ipls_agg *h) {
         case IPLS_E_NOMEM: cls = "java/lang/OutOfMemoryError"; break;
         default: break;
     }
-    throw_msg(env, cls, ipls_agg_last_error(h));
+    (void)h;
+    throw_msg(env, cls, ipls_agg_last_error(NULL));   /* this thread's failure */
 }
 
 static void throw_iae(JNIEnv *env, const char *what) {

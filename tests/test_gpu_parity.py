@@ -1207,6 +1207,51 @@ def test_async_device_coalesced(ipls, O, group):
     pb.close()
 
 
+def test_concurrent_failures_keep_their_messages(ipls, O):
+    """Two threads fail on one handle over and over with different errors (a
+    bucket shorter than its partition, Updater.java:115; an out-of-range
+    partition), a third folds correctly in between.  Each exception must carry
+    its own call's message (the failing thread's, include/ipls_agg.h), never
+    the other thread's, and the good folds must still be exact."""
+    import threading
+    P, L = 4, 4099
+    with ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0, 0]) as agg:
+        short = O.synth_bucket(L, 1, 0)[:L - 7]
+        good = O.synth_bucket(L, 1, 1)
+        wrong = []
+
+        def short_bucket():
+            for _ in range(300):
+                try:
+                    agg.Update(short, 1, from_clients=True)
+                    wrong.append("short bucket accepted")
+                except ipls.IplsError as e:
+                    if "shorter than partition length" not in str(e):
+                        wrong.append(f"short: {e}")
+
+        def bad_partition():
+            for _ in range(300):
+                try:
+                    agg.checksum(P + 3)
+                    wrong.append("partition P+3 read")
+                except ipls.IplsError as e:
+                    if "out of range" not in str(e) or "shorter" in str(e):
+                        wrong.append(f"range: {e}")
+
+        def folds():
+            for _ in range(50):
+                agg.Update(good, 3, from_clients=True)
+
+        th = [threading.Thread(target=f) for f in (short_bucket, bad_partition, folds)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not wrong, wrong[:5]
+        assert_bits_equal(agg.read(3), O.reduce([good] * 50, L), "partition 3 after 50 folds")
+        assert_bits_equal(agg.read(1), np.zeros(L), "partition 1 untouched by rejected buckets")
+
+
 def test_concurrent_callers_one_handle(ipls, O):
     """The reference's producer threads, Updater thread and daemon thread all
     reach the accumulators (serialised by PeerData.mtx, PeerData.java:27).
