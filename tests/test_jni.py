@@ -364,3 +364,56 @@ def test_jni_devices_publish_and_device_batches(jvm, gpu, O):
     assert exc == "java/lang/ArrayIndexOutOfBoundsException"
     jvm.call("close", h)
     del t
+
+
+# Java parameter / return type -> the JNI C type the shim must declare
+JNI_TYPES = {"void": "void", "boolean": "jboolean", "byte": "jbyte", "char": "jchar", "short": "jshort",
+             "int": "jint", "long": "jlong", "float": "jfloat", "double": "jdouble",
+             "boolean[]": "jbooleanArray", "byte[]": "jbyteArray", "short[]": "jshortArray", "int[]": "jintArray",
+             "long[]": "jlongArray", "float[]": "jfloatArray", "double[]": "jdoubleArray",
+             "String": "jstring", "Class": "jclass"}
+
+
+def _jni_type(t):
+    t = t.strip()
+    if t in JNI_TYPES:
+        return JNI_TYPES[t]
+    return "jobjectArray" if t.endswith("[]") else "jobject"   # byte[][], ByteBuffer, any other object
+
+
+def test_natives_match_the_shim_signatures():
+    """Every `native` of NativeAggregator.java has a C definition in the shim
+    with the JNI types a JVM will pass: (JNIEnv*, jclass) for a static native,
+    then one C parameter per Java parameter of the matching JNI type, and the
+    matching return type.  A JVM binds non-overloaded natives by name only, so
+    a type mismatch here would not be caught at link time -- it would read
+    the wrong registers at run time."""
+    import re
+    java = (ROOT / "ipls-java-api_amd" / "java" / "NativeAggregator.java").read_text()
+    shim = (ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c").read_text()
+    decls = re.findall(r"private\s+static\s+native\s+([\w\[\]<>.]+)\s+(\w+)\s*\(([^)]*)\)\s*;", java)
+    assert len(decls) == len(set(re.findall(r"\bnative\s+[\w\[\]<>.]+\s+(\w+)\s*\(", java))), "unparsed natives"
+    defs = {m.group(2): (m.group(1), m.group(3)) for m in
+            re.finditer(r"JNIEXPORT\s+(\w+)\s+JNICALL\s+Java_NativeAggregator_(\w+)\s*\(([^)]*)\)", shim)}
+    bad = []
+    for ret, name, params in decls:
+        if name not in defs:
+            bad.append(f"{name}: no C definition")
+            continue
+        cret, cparams = defs[name]
+        cps = [" ".join(p.split()) for p in cparams.split(",")]
+        if cret != _jni_type(ret):
+            bad.append(f"{name}: returns {cret}, Java {ret} needs {_jni_type(ret)}")
+        if len(cps) < 2 or not cps[0].startswith("JNIEnv *") or not cps[1].startswith("jclass"):
+            bad.append(f"{name}: must start (JNIEnv *env, jclass cls), has {cps[:2]}")
+            continue
+        jps = [p for p in (x.strip() for x in params.split(",")) if p]
+        if len(jps) != len(cps) - 2:
+            bad.append(f"{name}: {len(jps)} Java parameters, {len(cps) - 2} C parameters")
+            continue
+        for jp, cp in zip(jps, cps[2:]):
+            jt = jp.rsplit(None, 1)[0]
+            ct = cp.rsplit(None, 1)[0].replace(" *", "*")
+            if ct != _jni_type(jt):
+                bad.append(f"{name}: Java '{jp}' passed as C '{cp}' (needs {_jni_type(jt)})")
+    assert not bad, bad
