@@ -140,3 +140,77 @@ def test_shard_plan_rejects_bad_arguments():
         ipls.shard_plan(0, 2)
     with pytest.raises(ipls.IplsError):
         ipls.shard_plan(4, 0)
+
+
+def _prototypes():
+    """name -> (return C type, [parameter C types]) of every function include/ipls_agg.h declares."""
+    text = (ROOT / "include" / "ipls_agg.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"#.*", "", text)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(ipls_\w+)\s*\(([^)]*)\)\s*;", text):
+        ret = " ".join(m.group(1).split())
+        params = [" ".join(p.split()) for p in m.group(3).split(",")]
+        params = [] if params == ["void"] else params
+        out[m.group(2)] = (ret, params)
+    return out
+
+
+def _ctype_of(c, N):
+    """The ctypes type a C type must be bound with (pointers: None = any pointer type is checked separately)."""
+    c = c.replace("const ", "").strip()
+    scalars = {"int": ctypes.c_int, "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64, "uint64_t": ctypes.c_uint64,
+               "int16_t": ctypes.c_int16, "size_t": ctypes.c_size_t, "double": ctypes.c_double}
+    if "*" not in c:
+        return scalars[c]
+    return None
+
+
+def _pointee(c):
+    c = c.replace("const", " ")
+    base, stars = c.split("*", 1)[0].strip(), c.count("*")
+    return base.split()[-1] if base else base, stars
+
+
+def test_ctypes_signatures_match_the_header():
+    """Every prototype in include/ipls_agg.h against its ctypes binding in
+    ipls/_native.py: same parameter count, the same scalar types (an int64_t
+    bound as c_int would truncate lengths above 2^31), pointers bound as
+    pointers of the right element type, and the same return type."""
+    from ipls import _native as N
+    protos = _prototypes()
+    assert set(protos) == set(N.SIGNATURES), set(protos) ^ set(N.SIGNATURES)
+    elem = {"double": ctypes.c_double, "int32_t": ctypes.c_int32, "int64_t": ctypes.c_int64,
+            "uint64_t": ctypes.c_uint64, "int16_t": ctypes.c_int16, "ipls_agg_cfg": N.AggCfg,
+            "ipls_launch_info": N.LaunchInfo}
+    bad = []
+    for name, (ret, params) in sorted(protos.items()):
+        res, args = N.SIGNATURES[name]
+        # return type
+        if "*" in ret:
+            want = ctypes.c_char_p if "char" in ret else ctypes.c_void_p
+            if res is not want:
+                bad.append(f"{name}: returns {ret}, bound {res}")
+        elif res is not _ctype_of(ret, N):
+            bad.append(f"{name}: returns {ret}, bound {res}")
+        if len(args) != len(params):
+            bad.append(f"{name}: {len(params)} parameters, {len(args)} bound")
+            continue
+        for i, (c, a) in enumerate(zip(params, args)):
+            ctype = re.sub(r"\b\w+$", "", c).strip() if re.search(r"[*\s]\w+$", c) else c   # drop the name
+            if "*" not in ctype:
+                if a is not _ctype_of(ctype, N):
+                    bad.append(f"{name} arg {i}: C '{c}' bound {a.__name__}")
+                continue
+            base, stars = _pointee(ctype)
+            if a in (ctypes.c_void_p, ctypes.c_char_p):
+                continue                                    # any pointer may travel as void*
+            inner = getattr(a, "_type_", None)
+            if inner is None:
+                bad.append(f"{name} arg {i}: C '{c}' bound {a}")
+            elif stars >= 2:
+                if inner not in (ctypes.c_void_p, ctypes.c_char_p):
+                    bad.append(f"{name} arg {i}: C '{c}' (pointer to pointer) bound POINTER({inner.__name__})")
+            elif base in elem and inner is not elem[base]:
+                bad.append(f"{name} arg {i}: C '{c}' bound POINTER({inner.__name__})")
+    assert not bad, bad
