@@ -417,3 +417,24 @@ def test_natives_match_the_shim_signatures():
             if ct != _jni_type(jt):
                 bad.append(f"{name}: Java '{jp}' passed as C '{cp}' (needs {_jni_type(jt)})")
     assert not bad, bad
+
+
+def test_shim_under_asan():
+    """The shim's own host work (array pinning and release, length and
+    direct-buffer checks, local-reference reservation, exception mapping)
+    under AddressSanitizer + UndefinedBehaviorSanitizer: tests/jni/asan_driver.c
+    with the fake JVM and the shim instrumented, linked to the uninstrumented
+    libipls_agg.so (host code only: no device compute, a GPU-less open fails
+    as expected)."""
+    import os
+    BUILD.mkdir(parents=True, exist_ok=True)
+    exe = BUILD / "asan_driver"
+    subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-Wall", "-Wextra", "-Werror",
+                    "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all",
+                    f"-I{ROOT / 'tests' / 'jni'}", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "jni" / "asan_driver.c"), str(ROOT / "tests" / "jni" / "fake_jvm.c"),
+                    str(ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c"),
+                    f"-L{AGG}", "-lipls_agg", f"-Wl,-rpath,{AGG}", "-o", str(exe)], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "0 failure(s)" in r.stdout, r.stdout + r.stderr[-2000:]
