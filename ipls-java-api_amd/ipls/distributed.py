@@ -141,41 +141,75 @@ def combine_replicas(agg, plan: ReplicaPlan, rank: int, *, device=None, mode: st
                 filled.append(p)
         return filled
 
-    # All of this rank's sends and receives go out as ONE batch
-    # (batch_isend_irecv: one RCCL group), so partials to and from every
-    # peer GPU move at once, each pair over its own xGMI link.  The ops are
-    # listed in the global (partition, replica) order on every rank.
+    return finish_exchange(start_exchange(agg, plan, rank, device=device, group=group))
+
+
+@dataclass
+class Exchange:
+    """A replica exchange in flight (start_exchange -> finish_exchange)."""
+    agg: object
+    works: list
+    ops: list
+    landing: list
+    filled: list
+
+
+def start_exchange(agg, plan: ReplicaPlan, rank: int, *, device=None, group=None) -> Exchange:
+    """First half of the fixed-order replica exchange: export this rank's
+    replica partials and post every send and receive, without waiting.
+
+    All of this rank's sends and receives go out as ONE batch
+    (batch_isend_irecv: one RCCL group), so partials to and from every peer
+    GPU move at once, each pair over its own xGMI link.  The ops are listed in
+    the global (partition, replica) order on every rank.  The transfers run on
+    RCCL's stream: work queued on the aggregator's own stream before
+    finish_exchange (the owner's own folds, which the exchange never reads or
+    writes) overlaps them."""
+    import torch.distributed as dist
+
     ops, landing, filled = [], [], []
     bufs = getattr(agg, "transport_buffers", None)
-    for p, owner, others in exchanges:
+    for p, owner, others in plan.exchanges():
         if rank == owner:
             L = agg.lengths[p]
             for r in others:
-                buf = bufs(("in", p, r), L) if bufs else torch.empty(L, dtype=torch.float64, device=device)
+                buf = bufs(("in", p, r), L) if bufs else _empty(L, device)
                 ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
                 landing.append((p, buf))
             filled.append(p)
         elif rank in others:
             L = agg.lengths[p]
-            buf = bufs(("out", p, rank), L) if bufs else torch.empty(L, dtype=torch.float64, device=device)
+            buf = bufs(("out", p, rank), L) if bufs else _empty(L, device)
             agg.export_partial(p, buf)                    # AGG[p] -> the published partial
             ops.append(dist.P2POp(dist.isend, buf, owner, group=group))
-    if ops:
-        for work in dist.batch_isend_irecv(ops):
-            work.wait()
+    works = dist.batch_isend_irecv(ops) if ops else []
+    return Exchange(agg, works, ops, landing, filled)
+
+
+def finish_exchange(ex: Exchange) -> list[int]:
+    """Second half: wait for the transfers, then fold the landed partials into
+    REP strictly in (partition, replica) order."""
+    for work in ex.works:
+        work.wait()
+    if ex.ops:
         # RCCL's wait() only orders torch's stream after the group: block the
         # host on it, so received partials are visible to the aggregator's
         # stream and a send buffer is not refilled by the next export while
         # the send may still read it (a rank may only send)
-        _landed(ops[0].tensor)
-    for p, buf in landing:                                # fold in (partition, replica) order
-        agg.import_partial(p, buf)                        # REP[p] += R_r (Updater.java:40-44)
-    if landing:
+        _landed(ex.ops[0].tensor)
+    for p, buf in ex.landing:                             # fold in (partition, replica) order
+        ex.agg.import_partial(p, buf)                     # REP[p] += R_r (Updater.java:40-44)
+    if ex.landing:
         # the folds above are queued on the aggregator's stream and read the
         # transport buffers, which the next round's irecv (on RCCL's stream)
         # overwrites: wait for them before the buffers are handed out again
-        agg.sync()
-    return filled
+        ex.agg.sync()
+    return ex.filled
+
+
+def _empty(L, device):
+    import torch
+    return torch.empty(L, dtype=torch.float64, device=device)
 
 
 class RankShard:

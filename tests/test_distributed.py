@@ -61,17 +61,29 @@ def bucket(p, k, L):
 def worker(rank, world, port, P, L, K, replicas, mode, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from ipls.distributed import ReplicaPlan, combine_replicas
+    from ipls.distributed import ReplicaPlan, combine_replicas, finish_exchange, owner_of, start_exchange
     plan = ReplicaPlan.build(P, world, replicas)
     agg = NumpyAggregator(P, L)
+
     # each holder of partition p folds its own peers' buckets: holder h gets peers k with k % len == idx
-    for p, hs in plan.holders.items():
-        if rank in hs:
-            idx = hs.index(rank)
-            for k in range(K):
-                if k % len(hs) == idx:
-                    agg.Update(bucket(p, k, L), p)
-    filled = combine_replicas(agg, plan, rank, device="cpu", mode=mode)
+    def fold(owned):
+        for p, hs in plan.holders.items():
+            if rank in hs and (owner_of(p, P, world) == rank) == owned:
+                idx = hs.index(rank)
+                for k in range(K):
+                    if k % len(hs) == idx:
+                        agg.Update(bucket(p, k, L), p)
+    if mode == "overlapped":
+        # the replica partials first; the owner's own folds run while the
+        # exchange is in flight (start_exchange ... finish_exchange)
+        fold(owned=False)
+        ex = start_exchange(agg, plan, rank, device="cpu")
+        fold(owned=True)
+        filled = finish_exchange(ex)
+    else:
+        fold(owned=False)
+        fold(owned=True)
+        filled = combine_replicas(agg, plan, rank, device="cpu", mode=mode)
     res = {p: agg.finalize(p) for p in filled}
     q.put((rank, res))
     dist.barrier()
@@ -94,16 +106,21 @@ def expected(P, L, K, world, replicas):
     return out
 
 
-@pytest.mark.parametrize("world,replicas", [
-    (2, {0: [1], 3: [0]}),
-    (4, {0: [1, 2, 3], 5: [0, 3], 6: [1]}),
+@pytest.mark.parametrize("world,replicas,mode", [
+    (2, {0: [1], 3: [0]}, "fixed_order"),
+    (4, {0: [1, 2, 3], 5: [0, 3], 6: [1]}, "fixed_order"),
+    (4, {0: [1, 2, 3], 5: [0, 3], 6: [1]}, "overlapped"),
 ])
-def test_replica_exchange_fixed_order(world, replicas):
+def test_replica_exchange_fixed_order(world, replicas, mode):
+    """fixed_order: combine_replicas after every fold.  overlapped: the
+    exchange is started right after the replica partials are folded, the
+    owners fold their own buckets while it is in flight, then it finishes --
+    the same bits."""
     P, L, K = 8, 1031, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, P, L, K, replicas, "fixed_order", q))
+    procs = [ctx.Process(target=worker, args=(r, world, port, P, L, K, replicas, mode, q))
              for r in range(world)]
     for pr in procs:
         pr.start()
