@@ -267,23 +267,25 @@ __device__ __forceinline__ void reduce_tiles(
     }
     }  // !SEQ
     if constexpr (FIN) {
+      // W = fold + REP (AggregatePartition, IPLS.java:1256), and the averages'
+      // R stores before W's: two runs of stores per wave instead of
+      // alternating between the two streams every vector
+      // (tools/round_epilogue_sweep.hip, profiles/r02/s4/round_epilogue.txt)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        d2 w = acc[r];
         if (rep) {
           const d2 y = decode2<false>(ld16<true>(rep + off[r]));
-          w.x = w.x + y.x;
-          w.y = w.y + y.y;
+          acc[r].x = acc[r].x + y.x;
+          acc[r].y = acc[r].y + y.y;
         } else {
-          w.x = w.x + 0.0;   // AGG + REP with REP == +0.0, as AggregatePartition computes it
-          w.y = w.y + 0.0;
+          acc[r].x = acc[r].x + 0.0;   // AGG + REP with REP == +0.0, as AggregatePartition computes it
+          acc[r].y = acc[r].y + 0.0;
         }
-        __builtin_nontemporal_store(encode2<false>(w), (gu2)(dst + off[r]));
         if (avg) {
           // averages of elements e, e+1 (e + 1 may be the count slot L-1, which is not output)
           const int64_t e = off[r];
-          const double ax = cnt == 0.0 ? w.x : w.x / den;
-          const double ay = cnt == 0.0 ? w.y : w.y / den;
+          const double ax = cnt == 0.0 ? acc[r].x : acc[r].x / den;
+          const double ay = cnt == 0.0 ? acc[r].y : acc[r].y / den;
           if (avg_aligned) {
             if (e + 1 < L - 1) __builtin_nontemporal_store(encode2<false>(d2{ax, ay}), (gu2)(avg + e));
             else st8(avg + e, __builtin_bit_cast(unsigned long long, ax));
@@ -298,6 +300,8 @@ __device__ __forceinline__ void reduce_tiles(
           }
         }
       }
+#pragma unroll
+      for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<false>(acc[r]), (gu2)(dst + off[r]));
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) __builtin_nontemporal_store(encode2<BE_OUT>(acc[r]), (gu2)(dst + off[r]));
