@@ -12,6 +12,10 @@
 //   5 W only (no averages): the cost of the third stream
 //   6 averages at 256-B aligned offsets (q*L) instead of p*(L-1): the cost of
 //     the 8-mod-16 placement
+//   7 as 2 (averages first), and for 8-mod-16 averages no single 8-B stores
+//     inside a tile: each wave's last W value goes through LDS to the next
+//     wave piece, whose lane 63 stores the pair (previous y, its lane 0's x),
+//     so every lane stores one 16-B pair (singles only at the tile's ends)
 // Every variant that writes the real layout is checked bit-identical to the
 // shipped k_round (W and averages).
 // Usage: round_epilogue_sweep P L K REPS    (L a multiple of 32768)
@@ -129,6 +133,41 @@ __global__ __launch_bounds__(1024) void k_ep(const u64* const* __restrict__ bufs
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) st16<true>(dst + off[r], acc[r]);
+  } else if constexpr (V == 7) {
+    __shared__ double ylast[16][R];   // W value of lane 63 of wave w at vector r
+    const int w = tid >> 6;
+    if (lane == 63)
+#pragma unroll
+      for (int r = 0; r < R; ++r) ylast[w][r] = acc[r].y;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      double ax, ay;
+      A(r, ax, ay);
+      const int64_t e = off[r];
+      if (aligned) {
+        if (e + 1 < L - 1) st16<true>(avg + e, d2{ax, ay});
+        else st8(avg + e, __builtin_bit_cast(u64, ax));
+        continue;
+      }
+      const double nx = __shfl_down(ax, 1);
+      const double x0 = __shfl(ax, 0);
+      const bool first = (w == 0 && r == 0), last = (w == 15 && r == R - 1);
+      if (lane < 63) {
+        st16<true>(avg + e + 1, d2{ay, nx});
+      } else {
+        // the pair just before this wave piece: (predecessor's y, lane 0's x)
+        if (!first) {
+          const double py = w > 0 ? ylast[w - 1][r] : ylast[15][r - 1];
+          const double pa = cnt == 0.0 ? py : py / den;
+          st16<true>(avg + e - 127, d2{pa, x0});
+        }
+        if (last && e + 1 < L - 1) st8(avg + e + 1, __builtin_bit_cast(u64, ay));
+      }
+      if (first && lane == 0) st8(avg + e, __builtin_bit_cast(u64, ax));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) st16<true>(dst + off[r], acc[r]);
   } else {  // 5: W only
 #pragma unroll
     for (int r = 0; r < R; ++r) st16<true>(dst + off[r], acc[r]);
@@ -187,10 +226,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&o.d, P * sizeof(PartDesc)));
     CK(hipMemcpy(o.d, pd.data(), P * sizeof(PartDesc), hipMemcpyHostToDevice));
   };
-  Out ship, red, v[7];
+  Out ship, red, v[8];
   make(ship, L - 1, true);
   make(red, L - 1, false);
-  for (int i = 0; i < 7; ++i) make(v[i], i == 6 ? dl : L - 1, i != 5);
+  for (int i = 0; i < 8; ++i) make(v[i], i == 6 ? dl : L - 1, i != 5);
 
   struct Var {
     std::string name;
@@ -208,21 +247,21 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_round<false, kZero, 1, 16, 0, 1024>), dim3(tpp * P), dim3(1024), 0, 0, bp,
                                        ship.d, K, tpp, P, 0, d_cnt);
                   }, {}, round_b});
-  const char* names[7] = {"0 tool copy: W[r], avg[r]", "1 all W, then all avg", "2 all avg, then all W",
+  const char* names[8] = {"0 tool copy: W[r], avg[r]", "1 all W, then all avg", "2 all avg, then all W",
                           "3 W plain stores, avg nt", "4 W nt, avg plain stores", "5 W only (no averages)",
-                          "6 averages 256-B aligned"};
+                          "6 averages 256-B aligned", "7 avg first, LDS pair at wave ends"};
 #define V(I)                                                                                                 \
   vars.push_back({names[I], [&] {                                                                            \
                     hipLaunchKernelGGL((k_ep<I>), dim3(tpp * P), dim3(1024), 0, 0, bp, v[I].d, K, tpp, d_cnt); \
                   }, {}, I == 5 ? red_b : round_b});
-  V(0) V(1) V(2) V(3) V(4) V(5) V(6)
+  V(0) V(1) V(2) V(3) V(4) V(5) V(6) V(7)
 #undef V
 
   for (auto& x : vars) x.run();
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned char> a(na), b(na);
-    for (int i = 0; i <= 4; ++i) {
+    for (int i : {0, 1, 2, 3, 4, 7}) {
       CK(hipMemcpy(a.data(), ship.a, na, hipMemcpyDeviceToHost));
       CK(hipMemcpy(b.data(), v[i].a, na, hipMemcpyDeviceToHost));
       const bool avg_ok = !memcmp(a.data(), b.data(), na);
