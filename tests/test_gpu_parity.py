@@ -908,6 +908,46 @@ def test_aggregate_round_big_shape_device_out(ipls, O, shift):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("shift,accum,secure", [(0, False, False), (1, True, False), (0, True, True)])
+def test_aggregate_round_whole_tiles(ipls, O, shift, accum, secure):
+    """Partitions of whole 1024-lane tiles (config C's shape class, no
+    partial tile anywhere) through the fused round's big shape: every
+    partition's W and averages compared in full (odd and even partitions,
+    averages buffer 16-B aligned or 8 mod 16, i.e. both store paths of the
+    averages-before-W epilogue), with AGG started from a previous arrival
+    (ACCUM) or zero, and the secure divide."""
+    P, L, K = 4, 2097152, 3
+    arena = torch.empty(P * K * (L + 32), dtype=torch.float64, device="cuda")
+    base = (int(arena.data_ptr()) + 255) // 256 * 256
+    rows = [[ipls.DeviceBuffer(base + 8 * (p * K + k) * (L + 32), L) for k in range(K)] for p in range(P)]
+    for p in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[p][k], p, k, O.SEED)
+    out = torch.full((P * (L - 1) + 2,), 7.0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, secure=secure)
+    first = [O.synth_bucket(L, p, 50) for p in range(P)]
+    if accum:
+        for p in range(P):
+            agg.Update(first[p], p, from_clients=True)
+    agg.aggregate_round(0, rows, out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1)))
+    li = agg.last_launch()
+    assert li["kernel"] == ipls.KERNEL_ROUND and li["shape"] == ipls.SHAPE_BIG and li["map"] != 3, li
+    torch.cuda.synchronize()
+    full = out.cpu().numpy()
+    got = full[shift:shift + P * (L - 1)]
+    assert full[:shift].tolist() == [7.0] * shift and full[shift + P * (L - 1):].tolist() == [7.0] * (2 - shift)
+    for p in range(P):
+        bk = [O.synth_bucket(L, p, k) for k in range(K)]
+        S = O.reduce(bk, L, ipls.START_ACCUM, acc=first[p]) if accum else O.reduce(bk, L)
+        S = S + 0.0
+        assert_bits_equal(agg.read(p, ipls.TGT_WEIGHTS), S, f"W[{p}]")
+        assert_bits_equal(got[p * (L - 1):(p + 1) * (L - 1)], O.divide(S, secure=secure), f"avg[{p}]")
+    agg.close()
+    del arena, out
+    torch.cuda.empty_cache()
+
+
 def test_aggregate_round_edges(ipls, O, golden):
     """k = 0 (W = AGG + REP), a zero count slot (values pass through),
     special values, a sub-range of partitions, 8-B aligned buckets (unfused
