@@ -80,6 +80,12 @@ def parse():
                     help="N=1: run the single-handle multi-GPU leg over two shards of GPU 0 (a functional "
                          "rehearsal of the cross-GPU code path; the numbers measure one GPU)")
     ap.add_argument("--replica-timeout", type=float, default=240.0)
+    ap.add_argument("--be-schedule-ab", action="store_true",
+                    help="N=1: after the headline, A/B config D's big-endian schedules in one process on the same "
+                         "buckets (needs make -C ipls-java-api_amd variants)")
+    ap.add_argument("--watchdog-selftest", action="store_true",
+                    help="CPU only: run the N>1 watchdog over a gloo exchange that never completes "
+                         "(tests/test_bench_watchdog.py); exits with Watchdog.EXIT_CODE")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearsal of the N>1 code on one GPU (ranks share cuda:0, partials "
                          "travel through host memory); numbers are not a measurement")
@@ -522,6 +528,64 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
             "verified_checksum_p0": verified}
 
 
+def be_schedule_ab(ipls, torch, device: int, rounds: int = 4, steps: int = 5, verify: bool = True) -> dict:
+    """Config D's big-endian schedules A/B'd in ONE process on the SAME
+    buckets: the shipped library (R = 16, a fence after
+    every 3 vectors) against round 1's R = 16 fence-every-2-last-4-free
+    (IPLS_BE_SEQF=42) and hipcc's own schedule at R = 8, each a build of the
+    same sources (make -C ipls-java-api_amd variants) loaded beside the
+    shipped one.  64 x 4M x 32 BE buckets in, BE sums out; the variants'
+    launches are interleaved round by round so the layout is
+    common to all three; HIP events on each handle's stream."""
+    from ipls import _native as N
+    P, L, K = CONFIGS["D"]
+    ab = N.PKG_ROOT / "lib" / "ab"
+    libs = {"shipped_seqf3": None, "seqf42": N.load(ab / "libipls_agg_seqf42.so"),
+            "r8_compiler": N.load(ab / "libipls_agg_r8.so")}
+    elem = L + 32
+    arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
+    base = (int(arena.data_ptr()) + 255) // 256 * 256
+    rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L, big_endian=True) for k in range(K)] for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[q][k], q, k, ipls.SEED)
+    out_arena = torch.empty(P * elem + 32, dtype=torch.float64, device="cuda")
+    obase = (int(out_arena.data_ptr()) + 255) // 256 * 256
+    dsts = [obase + 8 * q * elem for q in range(P)]
+    torch.cuda.synchronize()
+    nbytes = P * (K + 1) * L * 8
+    aggs = {nm: ipls.Aggregator(n_partitions=P, bucket_len=L, device=device, library=lb) for nm, lb in libs.items()}
+    res = {nm: {"ms": [], "launch": None, "verified_checksum_p0": None} for nm in libs}
+    for r in range(rounds):
+        for nm, agg in aggs.items():
+            stream = torch.cuda.ExternalStream(agg.stream, device=torch.device("cuda", device))
+            agg.reduce_batch_out(0, rows, dsts, start_mode=ipls.START_ZERO, big_endian_in=True, big_endian_out=True)
+            agg.sync()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+            ev[0].record(stream)
+            for i in range(steps):
+                agg.reduce_batch_out(0, rows, dsts, start_mode=ipls.START_ZERO, big_endian_in=True,
+                                     big_endian_out=True)
+                ev[i + 1].record(stream)
+            agg.sync()
+            res[nm]["ms"].append(round(float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])), 4))
+            if r == 0:
+                res[nm]["launch"] = agg.last_launch()
+                if verify:
+                    from oracle import oracle as O   # checker only
+                    res[nm]["verified_checksum_p0"] = (
+                        ipls.checksum_dev(ipls.DeviceBuffer(dsts[0], L, big_endian=True)) ==
+                        O.c_synth_sum_checksum(L, 0, K))
+    for nm, agg in aggs.items():
+        agg.close()
+        ms = float(np.median(res[nm]["ms"]))
+        res[nm].update(median_ms=round(ms, 4), frac=round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4))
+    del arena, out_arena, rows
+    torch.cuda.empty_cache()
+    return {"workload": f"D: {P} x {L} x {K}, BE in + BE out", "rounds": rounds, "steps_per_round": steps,
+            "algorithmic_bytes_per_launch": nbytes, "variants": res}
+
+
 def config_a_leg(ipls, reps: int = 20) -> dict:
     """BASELINE configs[0], the reference's own CPU-runnable case: ETHModel
     (M = 443,610, tests/golden/ethmodel.f64be.gz), -pa 3 -n 3, three peers.
@@ -740,12 +804,12 @@ def publish_leg(ipls, torch, agg, stream, L: int, reps: int = 10, verify: bool =
     text_len = 4 * -(-(14 + 8 * L + len(origin)) // 3)
     buf = torch.empty(text_len + 64, dtype=torch.uint8, device="cuda")
     ptr = int(buf.data_ptr())
-    agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=ptr)
+    agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=ptr, out_cap=text_len + 64)
     agg.sync()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     ev[0].record(stream)
     for i in range(reps):
-        agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=ptr)
+        agg.publish_partial(0, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=ptr, out_cap=text_len + 64)
         ev[i + 1].record(stream)
     agg.sync()
     ms = float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]))
@@ -773,16 +837,17 @@ def publish_leg(ipls, torch, agg, stream, L: int, reps: int = 10, verify: bool =
         total = (total + 63) // 64 * 64 + text_len
     big = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
     bptr = int(big.data_ptr())
-    lens, offs = agg.publish_partials(parts, 7, bs, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr)
+    lens, offs = agg.publish_partials(parts, 7, bs, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr, out_cap=total + 64)
     agg.sync()
     ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     t_loop, t_batch = [], []
     for _ in range(reps):
         ev2[0].record(stream)
         for p in parts:
-            agg.publish_partial(p, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr + offs[p])
+            agg.publish_partial(p, 7, 33, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr + offs[p],
+                                  out_cap=total + 64 - offs[p])
         ev2[1].record(stream)
-        agg.publish_partials(parts, 7, bs, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr)
+        agg.publish_partials(parts, 7, bs, origin=origin, target=ipls.TGT_WEIGHTS, out=bptr, out_cap=total + 64)
         ev2[2].record(stream)
         agg.sync()
         t_loop.append(ev2[0].elapsed_time(ev2[1]))
@@ -859,22 +924,131 @@ def strong_leg(ipls, torch, dist, rank: int, world: int, local: int, steps: int 
             "GBps_per_gpu": round(total / dt / 1e9 / world, 1), "verified_checksum_p0": ok}
 
 
-def pmc_traffic(workload_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass for this
-    workload (profiles/pmc_traffic.json), or None."""
+def pmc_traffic(workload_key: str, build: dict):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes for this
+    workload (profiles/pmc_traffic.json), tied to the code that was profiled:
+    every entry carries the build record (ipls.build_info()) of the process the
+    counters came from.  Returns (traffic or None, provenance).  The traffic is
+    reported only when the entry was taken on this very library (same .so
+    sha256), or on a library built from the same kernel sources (kernel-source
+    sha256 of ipls_kernels.hpp + engine.hip; the .so differs in host code only);
+    otherwise None with traffic_stale = True."""
     f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None
+    prov = {"source": "profiles/pmc_traffic.json", "entry": workload_key, "traffic_stale": True, "match": None}
     try:
-        d = json.loads(f.read_text())
-        e = d.get(workload_key)
-        return None if e is None else e.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+        e = json.loads(f.read_text()).get(workload_key)
+    except (OSError, ValueError):
+        e = None
+    if e is None:
+        prov["why"] = "no PMC entry for this workload"
+        return None, prov
+    eb = e.get("build") or {}
+    prov.update(entry_git_rev=eb.get("git_rev"), entry_so_sha256=eb.get("so_sha256"), profile=e.get("source"))
+    if eb.get("so_sha256") and eb.get("so_sha256") == build.get("so_sha256"):
+        prov.update(traffic_stale=False, match="so_sha256")
+    elif eb.get("kernel_src_sha256") and eb.get("kernel_src_sha256") == build.get("kernel_src_sha256"):
+        prov.update(traffic_stale=False, match="kernel_src_sha256")
+    else:
+        prov["why"] = "the PMC entry was taken on another build of the kernels"
+        return None, prov
+    return e.get("hbm_bytes_per_launch"), prov
+
+
+class Watchdog:
+    """Bounds the N>1 side legs (replica exchange, strong-scaling D, the
+    all-ranks host-inclusive leg, the single-handle C-ABI leg).  On expiry it
+    records the leg that was running as {"error": "timed out ..."} in the JSON
+    line, prints the line (rank 0, once) and ends the process with EXIT_CODE:
+    a stuck RCCL/xGMI exchange must show up as a failed run, never as rc 0."""
+    EXIT_CODE = 3
+
+    def __init__(self, timeout: float, out):
+        import threading
+        self.timeout = timeout
+        self.out = out                 # rank 0's line (None on other ranks)
+        self.stage = ["replica_exchange"]
+        self._lock = threading.Lock()
+        self._state = "running"        # -> "finished" (main prints) or "expired" (the dog prints and exits)
+        self._t = threading.Timer(timeout, self.expire)
+        self._t.daemon = True
+
+    def start(self):
+        self._t.start()
+
+    def cancel(self):
+        """The legs are done: True if the main thread may print the line.  If
+        the dog already fired, this thread parks until its os._exit ends it."""
+        with self._lock:
+            if self._state == "running":
+                self._state = "finished"
+                self._t.cancel()
+                return True
+        time.sleep(3600)
+        return False
+
+    def expire(self):
+        with self._lock:
+            if self._state != "running":
+                return
+            self._state = "expired"
+        msg = f"timed out after {self.timeout} s (watchdog; exit code {self.EXIT_CODE})"
+        if self.out is not None:
+            self.out[self.stage[0]] = {"error": msg}
+            self.out["watchdog"] = {"expired": True, "stage": self.stage[0], "exit_code": self.EXIT_CODE}
+            print(json.dumps(self.out), flush=True)
+        print(f"bench.py: side leg {self.stage[0]} {msg}", file=sys.stderr, flush=True)
+        os._exit(self.EXIT_CODE)
+
+
+def rccl_record(torch, dist, group, rank: int, local: int, build: dict) -> dict:
+    """What the process group saw after init_process_group: the backend, its
+    world size, and per rank the HIP device it drives (ordinal, name, PCI bus
+    and the library build it loaded), gathered over the host-side group."""
+    me = {"rank": rank, "local_rank": local, "device": None, "name": None, "pci_bus_id": None,
+          "so_sha256": build.get("so_sha256")}
+    try:
+        d = torch.cuda.current_device()
+        pr = torch.cuda.get_device_properties(d)
+        me.update(device=d, name=pr.name)
+        bus = getattr(pr, "pci_bus_id", None)
+        if bus is not None:
+            me["pci_bus_id"] = f"{getattr(pr, 'pci_domain_id', 0):04x}:{bus:02x}:{getattr(pr, 'pci_device_id', 0):02x}"
+    except Exception as e:   # noqa: BLE001 -- the record never costs the run
+        me["error"] = f"{type(e).__name__}: {e}"
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me, group=group)
+    buses = [r.get("pci_bus_id") for r in ranks]
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks,
+            "distinct_devices": len(set(buses)) if all(buses) else None}
+
+
+def watchdog_selftest(args) -> None:
+    """CPU rehearsal of the N>1 watchdog (no GPU): every rank joins a gloo
+    group, then gets stuck in a point-to-point exchange that never completes
+    (each rank waits to receive from the next one; nobody sends) -- the shape of
+    a hung replica exchange.  The watchdog must print rank 0's line with the
+    stuck leg's error and end every rank with Watchdog.EXIT_CODE."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "selftest": "watchdog"} \
+        if rank == 0 else None
+    dog = Watchdog(args.replica_timeout, out)
+    dog.start()
+    dog.stage[0] = "replica_exchange"
+    buf = torch.zeros(1)
+    dist.recv(buf, src=(rank + 1) % world)     # never sent: stuck until the watchdog fires
+    if dog.cancel() and out is not None:       # not reached
+        print(json.dumps(out), flush=True)
 
 
 def main():
     args = parse()
+    if args.watchdog_selftest:
+        return watchdog_selftest(args)
     import torch
     import torch.distributed as dist
 
@@ -897,6 +1071,8 @@ def main():
         side_group = dist.new_group(backend="gloo")   # host-side barriers of the side legs
 
     import ipls
+    build = ipls.build_info()   # the code every number below was measured on
+    rccl = rccl_record(torch, dist, side_group, rank, local, build) if world > 1 else None
     P, L, K = CONFIGS[args.config]
     if args.strong:
         if P % world:
@@ -983,7 +1159,7 @@ def main():
     if rank == 0:
         achieved = bytes_step / (kern_ms / 1e3) / 1e9
         wkey = f"{args.config}{'-be' if args.be else ''}"
-        traffic = pmc_traffic(wkey)
+        traffic, traffic_prov = pmc_traffic(wkey, build)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -1012,11 +1188,15 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_provenance": traffic_prov,
                 "algorithmic_bytes_per_launch": bytes_step,
                 "kernel_ms": round(kern_ms, 4),
             },
             "verified_checksum_p0": verified,
+            "build": build,
         }
+        if rccl is not None:
+            out["rccl"] = rccl
         if round_info:
             out["round"] = round_info
         def side(fn, *a, **kw):
@@ -1047,24 +1227,21 @@ def main():
                 _, LF, KF = CONFIGS["F"]
                 out["other_configs"]["F"]["host_inclusive"] = side(host_inclusive, ipls, ipls.Aggregator, LF, KF, 2,
                                                                    local)
+    if world == 1 and args.be_schedule_ab and out is not None:
+        if "arena" in locals():
+            del arena, rows
+        torch.cuda.empty_cache()
+        out["be_schedule_ab"] = side(be_schedule_ab, ipls, torch, local, verify=not args.no_verify)
     dog = None
-    printed = []
-    stage = ["replica_exchange"]
     if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg and args.no_multi_leg
                                           and args.no_e2e):
-        # the multi-rank side legs are extra measurements: a watchdog makes sure
-        # a stuck exchange (or a teardown stuck behind a peer that failed in
-        # it) can never cost the main line -- every rank exits
-        import threading
-
-        def expire():
-            if out is not None and not printed:
-                out[stage[0]] = {"error": f"timed out after {args.replica_timeout} s"}
-                print(json.dumps(out), flush=True)
-            os._exit(0)
-        dog = threading.Timer(args.replica_timeout, expire)
-        dog.daemon = True
+        # the multi-rank side legs are extra measurements: a watchdog ends a
+        # stuck exchange (or a teardown stuck behind a peer that failed in it)
+        # -- the line is printed with the stuck leg's error and every rank exits
+        # NON-zero, so a hang is never recorded as a clean run
+        dog = Watchdog(args.replica_timeout, out)
         dog.start()
+        stage = dog.stage
         if not args.no_replica_leg:
             stage[0] = "replica_exchange"
             try:
@@ -1122,14 +1299,14 @@ def main():
         out["c_abi_multi_gpu"] = side(c_abi_multi_gpu, ipls, torch, [local, local], P_m // 2, L_m, K_m,
                                       verify=not args.no_verify)
         out["c_abi_multi_gpu"]["note"] = "rehearsal: two shards of one GPU (same code path, no xGMI)"
+    if dog is not None:
+        dog.cancel()          # every leg finished: the line is printed once, here
+                              # (if the dog fired first, it printed and exits)
     if out is not None:
-        printed.append(True)
         print(json.dumps(out), flush=True)
     agg.close()
     if world > 1:
         dist.destroy_process_group()
-    if dog is not None:
-        dog.cancel()
 
 
 if __name__ == "__main__":

@@ -368,7 +368,14 @@ int ipls_agg_reduce_partial(ipls_agg *h, int slot, int p_first, int n_parts, con
 /* For every partition of [p_first, p_first+n_parts): REP[p] += the partial of
  * every slot that folded into p since the last combine, slots ascending, in
  * one launch per owner shard that reads the partials over xGMI; the partials
- * are then logically +0.0 again.  Returns the number of partials folded. */
+ * are then logically +0.0 again.  Returns the number of partials folded.
+ * A pair of devices without peer access is not an error: such a partial is
+ * first copied into an owner-side buffer (hipMemcpyPeerAsync on the owner's
+ * stream) and the same fold reads that copy, in the same slot order, so the
+ * result is bit-identical.  Setting IPLS_PEER_STAGED=1 in the environment
+ * before ipls_agg_open forces this path for every cross-shard read (the
+ * combine and the Gradient_Buff of ipls_agg_update_indirect) -- a test
+ * switch; ipls_launch_info.staged counts the staged partials. */
 int ipls_agg_combine_partials(ipls_agg *h, int p_first, int n_parts);
 
 /* ---- publish-side codec (a9) ----
@@ -413,7 +420,9 @@ int64_t ipls_agg_publish_partials(ipls_agg *h, const int32_t *parts, int n_parts
 typedef struct ipls_launch_info {
     int32_t kernel, shape, block, vectors, seqf, map;
     int64_t grid;
-    int32_t be_in, be_out, start, reserved;
+    int32_t be_in, be_out, start;
+    int32_t staged;   /* partials the handle's last ipls_agg_combine_partials copied to the owner
+                         first (no xGMI peer access, or IPLS_PEER_STAGED=1) instead of peer loads */
 } ipls_launch_info;
 int ipls_agg_last_launch(ipls_agg *h, ipls_launch_info *out);
 

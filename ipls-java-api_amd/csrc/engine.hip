@@ -408,8 +408,17 @@ inline bool fill(int64_t tiles) {
 // reduce_tiles (hipcc's own schedule hoisted the loads around the bswap and
 // spilled 184 B).  The ACCUM start keeps 8 (at 16 it still spills around
 // the loop -- checked with -Rpass-analysis=kernel-resource-usage).
+// IPLS_BE_BIG_R / IPLS_BE_SEQF rebuild the big-endian big shape with another
+// schedule for same-process A/B runs (make -C ipls-java-api_amd variants,
+// bench.py --be-schedule-ab); the shipped library uses the defaults.
+#ifndef IPLS_BE_BIG_R
+#define IPLS_BE_BIG_R 16
+#endif
+#ifndef IPLS_BE_SEQF
+#define IPLS_BE_SEQF 3
+#endif
 template <bool BE_IN, int START, bool FIN = false>
-constexpr int big_r() { return START != kAccum ? 16 : 8; }
+constexpr int big_r() { return START != kAccum ? (BE_IN ? IPLS_BE_BIG_R : 16) : 8; }
 // SEQ schedule of the big shape (0 = hipcc's own): big-endian input at R = 16
 // loads, decodes and adds a peer's vectors three at a time with a fence after
 // each group (SEQF = 3; 118 VGPRs, no spills).  Round 2 swept fence periods
@@ -418,7 +427,7 @@ constexpr int big_r() { return START != kAccum ? 16 : 8; }
 // (SEQF = 42) by 0.7-1.6 points on C's and D's shapes, BE in and in + out;
 // periods >= 5, a free tail on period 3, and period 1 are all slower.
 template <bool BE_IN, int START>
-constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? 3 : 0; }
+constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? IPLS_BE_SEQF : 0; }
 // Block order of the big shape over whole tiles: partition-major (map 0),
 // except big-endian input on grids of at most 4096 tiles, which runs
 // XCD-chunked (map 2: each XCD walks one contiguous eighth of the work).  With

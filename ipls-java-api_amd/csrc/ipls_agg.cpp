@@ -23,11 +23,16 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -47,6 +52,66 @@ struct Partial {
   hipEvent_t ready = nullptr;      // recorded on the slot's stream after its last fold
   hipEvent_t consumed = nullptr;   // recorded on the owner's stream after the combine read it
   bool consumed_pending = false;
+  double* stage = nullptr;         // owner-side copy, when the owner cannot load d over xGMI
+};
+
+// Persistent host workers, one per shard after the first: a call that waits
+// on host memory (sync, get_partitions into host memory, collect_replicas,
+// ingest ...) hands each shard's part to that shard's worker instead of
+// spawning a thread per shard per call.  A worker only ever drives its own
+// shard's GPU, so after its first call its device is current and every
+// dev_use on it is free.
+class ShardPool {
+ public:
+  explicit ShardPool(int n) : w_(n) {
+    for (int s = 1; s < n; ++s) {
+      w_[s] = std::make_unique<W>();
+      w_[s]->th = std::thread([w = w_[s].get()] { run(w); });
+    }
+  }
+  ~ShardPool() {
+    for (auto& w : w_)
+      if (w) {
+        {
+          std::lock_guard<std::mutex> lk(w->m);
+          w->stop = true;
+        }
+        w->cv.notify_one();
+        w->th.join();
+      }
+  }
+  bool has(int s) const { return s > 0 && s < (int)w_.size() && w_[s]; }
+  void post(int s, std::function<void()> fn) {
+    W* w = w_[s].get();
+    {
+      std::lock_guard<std::mutex> lk(w->m);
+      w->q.push_back(std::move(fn));
+    }
+    w->cv.notify_one();
+  }
+
+ private:
+  struct W {
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    bool stop = false;
+  };
+  static void run(W* w) {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(w->m);
+        w->cv.wait(lk, [w] { return w->stop || !w->q.empty(); });
+        if (w->q.empty()) return;   // stop requested and drained
+        fn = std::move(w->q.front());
+        w->q.pop_front();
+      }
+      fn();
+    }
+  }
+  std::vector<std::unique_ptr<W>> w_;
 };
 
 }  // namespace
@@ -63,8 +128,17 @@ struct ipls_agg {
   std::vector<int> lo;               // shard s owns partitions [lo[s], lo[s+1])
   std::vector<int> owner;            // partition -> shard
   std::vector<std::vector<char>> peer;   // peer[a][b]: shard a's device reads shard b's memory
-  std::vector<hipEvent_t> xev;       // per shard: cross-shard ordering point
-  int last_shard = 0;
+  bool force_staged = false;         // IPLS_PEER_STAGED=1: stage every cross-device read (test switch)
+  std::vector<hipEvent_t> xev;       // per shard: cross-shard ordering point (used under gbuf_mu)
+  // the handle's ONE Gradient_Buff lives on shard 0 (one Updater thread,
+  // Updater.java:162): a request's load, its fold on the partition's shard and
+  // the hand-back run as one sequence under gbuf_mu (the sequence may wait on
+  // the host for a pinned zero-copy load; mu is never held across that)
+  std::mutex gbuf_mu;
+  std::vector<double*> gstage;       // per shard: Gradient_Buff copy when shard 0 is not peer-readable
+  std::atomic<int> last_shard{0};
+  std::atomic<int> last_staged{0};   // partials the last combine staged (ipls_launch_info.staged)
+  std::unique_ptr<ShardPool> pool;   // S > 1 only
   // asynchronous folds across shards: per shard, (handle ticket, engine ticket) in issue order
   uint64_t ticket_next = 1;
   std::vector<std::deque<std::pair<uint64_t, uint64_t>>> tickets;
@@ -137,7 +211,7 @@ int range_err(ipls_agg* H, int p) { return ferr(H, IPLS_E_RANGE, "partition %d o
 inline int route(ipls_agg* H, int p, int* local) {
   const int s = H->owner[p];
   *local = p - H->lo[s];
-  H->last_shard = s;
+  H->last_shard.store(s, std::memory_order_relaxed);
   return s;
 }
 
@@ -152,9 +226,9 @@ std::vector<int> shards_of(const ipls_agg* H, int p0, int p1) {
 
 std::vector<int> nonempty_shards(const ipls_agg* H) { return shards_of(H, 0, H->P); }
 
-// Run fn(s) for each shard: in this thread for one shard, else one host
-// thread per shard (calls that wait on host copies overlap across GPUs).
-// Returns the first negative code, with that shard's message.
+// Run fn(s) for each shard: the first in this thread, every other on its
+// shard's persistent worker (calls that wait on host copies overlap across
+// GPUs).  Returns the first negative code, with that shard's message.
 template <class F>
 int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
   if (ss.size() <= 1) {
@@ -164,21 +238,44 @@ int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
   }
   std::vector<int> rc(ss.size(), 0);
   std::vector<std::string> msg(ss.size());   // a worker's message lives in the worker's thread slot
-  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv;
+  size_t left = ss.size() - 1;
   for (size_t i = 1; i < ss.size(); ++i)
-    th.emplace_back([&, i] {
+    H->pool->post(ss[i], [&, i] {
       rc[i] = fn(ss[i]);
       if (rc[i] < 0) msg[i] = dev_last_error(nullptr);
+      std::lock_guard<std::mutex> lk(m);
+      if (--left == 0) cv.notify_one();
     });
   rc[0] = fn(ss[0]);
   if (rc[0] < 0) msg[0] = dev_last_error(nullptr);
-  for (auto& t : th) t.join();
+  {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return left == 0; });
+  }
   for (size_t i = 0; i < ss.size(); ++i)
     if (rc[i] < 0) {
       set_err(H, msg[i]);
       return rc[i];
     }
   return IPLS_OK;
+}
+
+// A device operand that shard s's GPU reads or writes (an output of a call
+// over several shards, a text buffer): it must be s's own memory or that of a
+// device s has peer access to -- anything else would fault the GPU instead of
+// failing the call.  Host memory and unknown pointers are left to the engine.
+int check_reach(ipls_agg* H, int s, const void* ptr, const char* what) {
+  if (!ptr) return IPLS_OK;
+  hipPointerAttribute_t at{};
+  const hipError_t e = hipPointerGetAttributes(&at, ptr);
+  (void)hipGetLastError();
+  if (e != hipSuccess || at.type != hipMemoryTypeDevice || at.device == H->devices[s]) return IPLS_OK;
+  for (int t = 0; t < H->S(); ++t)
+    if (H->devices[t] == at.device && H->peer[s][t]) return IPLS_OK;
+  return ferr(H, IPLS_E_DEVICE, "device %d cannot reach the %s on device %d (no peer access)", H->devices[s], what,
+              at.device);
 }
 
 // Order shard b's stream after the work queued so far on shard a's stream.
@@ -194,12 +291,16 @@ int order_after(ipls_agg* H, int a, int b) {
 }
 
 void destroy(ipls_agg* H) {
+  H->pool.reset();   // join the workers first: none may be inside an engine call below
   for (auto& row : H->part)
     for (Partial& q : row) {
       if (q.d) hipFree(q.d);
+      if (q.stage) hipFree(q.stage);
       if (q.ready) hipEventDestroy(q.ready);
       if (q.consumed) hipEventDestroy(q.consumed);
     }
+  for (double* g : H->gstage)
+    if (g) hipFree(g);
   for (size_t s = 0; s < H->sh.size(); ++s) {
     if (H->sh[s]) dev_close(H->sh[s]);
     if (s < H->xev.size() && H->xev[s]) hipEventDestroy(H->xev[s]);
@@ -303,6 +404,10 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
       (void)hipGetLastError();
       H->peer[a][b] = (char)can;
     }
+  const char* st = std::getenv("IPLS_PEER_STAGED");
+  H->force_staged = st && st[0] == '1';
+  H->gstage.assign(S, nullptr);
+  if (S > 1) H->pool = std::make_unique<ShardPool>(S);
   *out = H;
   return IPLS_OK;
 }
@@ -369,7 +474,9 @@ int ipls_agg_set_coalesce(ipls_agg* H, int max_group) {
 int ipls_agg_last_launch(ipls_agg* H, ipls_launch_info* out) {
   KeepDevice keep_device;
   if (!H || !out) return ferr(H, IPLS_E_INVAL, "null argument");
-  return dev_last_launch(H->sh[H->last_shard], out);
+  const int rc = dev_last_launch(H->sh[H->last_shard.load(std::memory_order_relaxed)], out);
+  out->staged = H->last_staged.load(std::memory_order_relaxed);
+  return rc;
 }
 
 int ipls_agg_load_model(ipls_agg* H, const void* src, int64_t n, int src_kind) {
@@ -480,15 +587,32 @@ int ipls_agg_update_indirect(ipls_agg* H, int p, int target, const void* bytes, 
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
   const int s = route(H, p, &q);
-  if (s == 0) return fwd(H, 0, dev_update_indirect(H->sh[0], q, target, bytes, n_bytes));
+  if (H->S() == 1) return fwd(H, 0, dev_update_indirect(H->sh[0], q, target, bytes, n_bytes));
   // The handle has ONE Gradient_Buff (one Updater thread, Updater.java:162),
-  // on shard 0: load it there, then fold it into p's owner over xGMI.
-  std::lock_guard<std::mutex> lk(H->mu);
+  // on shard 0: load it there, then fold it into p's owner (over xGMI, or
+  // from a staged copy when the owner cannot read shard 0's memory).  The
+  // whole sequence is one critical section for every shard, shard 0
+  // included: another request's load must not overwrite the buffer between
+  // this load and this fold's reads.
+  std::lock_guard<std::mutex> gk(H->gbuf_mu);
+  if (s == 0) return fwd(H, 0, dev_update_indirect(H->sh[0], q, target, bytes, n_bytes));
   const void* g = nullptr;
   int64_t glen = 0;
   if (int rc = fwd(H, 0, dev_gbuf_load(H->sh[0], bytes, n_bytes, &g, &glen))) return rc;
-  if (!H->peer[s][0]) return ferr(H, IPLS_E_DEVICE, "device %d cannot read device %d", H->devices[s], H->devices[0]);
   if (int rc = order_after(H, 0, s)) return rc;
+  if (!H->peer[s][0] || H->force_staged) {
+    hipStream_t st = (hipStream_t)dev_stream(H->sh[s]);
+    if (dev_use(H->devices[s]) != hipSuccess ||
+        (!H->gstage[s] && hipMalloc(&H->gstage[s], (size_t)std::max<int64_t>(glen, 1) * 8) != hipSuccess)) {
+      (void)hipGetLastError();
+      return ferr(H, IPLS_E_NOMEM, "Gradient_Buff copy on device %d", H->devices[s]);
+    }
+    if (hipMemcpyPeerAsync(H->gstage[s], H->devices[s], g, H->devices[0], (size_t)glen * 8, st) != hipSuccess) {
+      (void)hipGetLastError();
+      return ferr(H, IPLS_E_DEVICE, "Gradient_Buff copy from device %d to %d failed", H->devices[0], H->devices[s]);
+    }
+    g = H->gstage[s];
+  }
   const int rc = fwd(H, s, dev_accumulate(H->sh[s], q, target, g, glen, IPLS_DEV_F64));
   if (int r2 = order_after(H, s, 0)) return r2;   // the next load waits for this fold's reads
   return rc;
@@ -554,7 +678,12 @@ int ipls_agg_reduce_batch_out(ipls_agg* H, int p_first, int n_parts, const void*
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > H->P)
     return ferr(H, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, H->P);
   if (!dst || k < 0 || (k > 0 && !bufs)) return ferr(H, IPLS_E_INVAL, "bad bucket/destination list");
-  for (int s : shards_of(H, p_first, p_first + n_parts)) {
+  const std::vector<int> ss = shards_of(H, p_first, p_first + n_parts);
+  if (dst_kind == IPLS_DEV_F64 || dst_kind == IPLS_DEV_BE)
+    for (int s : ss)   // every destination is written by its partition's GPU: checked before any launch
+      for (int p = std::max(p_first, H->lo[s]); p < std::min(p_first + n_parts, H->lo[s + 1]); ++p)
+        if (int rc = check_reach(H, s, dst[p - p_first], "destination")) return rc;
+  for (int s : ss) {
     const int q0 = std::max(p_first, H->lo[s]), q1 = std::min(p_first + n_parts, H->lo[s + 1]);
     H->last_shard = s;
     if (int rc = fwd(H, s, dev_reduce_batch_out(H->sh[s], q0 - H->lo[s], q1 - q0, bufs + (size_t)(q0 - p_first) * k,
@@ -581,6 +710,9 @@ int ipls_agg_aggregate_round(ipls_agg* H, int p_first, int n_parts, const void* 
     return dev_aggregate_round(H->sh[s], q0 - H->lo[s], q1 - q0, bufs + (size_t)(q0 - p_first) * k, k, src_kind, a,
                                avg_kind);
   };
+  if (avg_out && avg_kind == IPLS_DEV_F64)
+    for (int s : ss)   // each shard writes its partitions' averages into avg_out
+      if (int rc = check_reach(H, s, avg_out, "averages buffer")) return rc;
   H->last_shard = ss.back();
   if (avg_out && avg_kind == IPLS_HOST_F64) return par_shards(H, ss, one);   // each shard copies its averages back
   for (int s : ss)
@@ -693,6 +825,9 @@ int ipls_agg_get_partitions(ipls_agg* H, void* out, int64_t n, int out_kind) {
     return ferr(H, IPLS_E_RANGE, "output of %lld < model size %lld", (long long)n, (long long)H->flat_total);
   if (out_kind != IPLS_HOST_F64 && out_kind != IPLS_HOST_BE_CANON && out_kind != IPLS_DEV_F64)
     return ferr(H, IPLS_E_INVAL, "bad out_kind %d", out_kind);
+  if (out_kind == IPLS_DEV_F64)
+    for (int s : nonempty_shards(H))
+      if (int rc = check_reach(H, s, out, "model buffer")) return rc;
   // every shard writes its flat segment [off[lo_s], ...) of the model
   return par_shards(H, nonempty_shards(H), [&](int s) {
     const int64_t base = H->off[H->lo[s]];
@@ -809,19 +944,8 @@ int64_t ipls_agg_publish_partials(ipls_agg* H, const int32_t* parts, int n_parts
   for (int i = 0; i < n_parts; ++i) idx[H->owner[parts[i]]].push_back(i);
   for (int s = 0; s < H->S(); ++s) {
     if (idx[s].empty()) continue;
-    if (out_kind == IPLS_DEV_TEXT) {
-      // the texts are written by shard s's device: out must be its memory or a peer's
-      hipPointerAttribute_t at{};
-      if (hipPointerGetAttributes(&at, out) == hipSuccess && at.type == hipMemoryTypeDevice &&
-          at.device != H->devices[s]) {
-        int ok = 0;
-        for (int t = 0; t < H->S(); ++t)
-          if (H->devices[t] == at.device && H->peer[s][t]) ok = 1;
-        if (!ok)
-          return ferr(H, IPLS_E_DEVICE, "device %d cannot write the texts on device %d", H->devices[s], at.device);
-      }
-      (void)hipGetLastError();
-    }
+    if (out_kind == IPLS_DEV_TEXT)   // the texts are written by shard s's device
+      if (int rc = check_reach(H, s, out, "text buffer")) return rc;
     std::vector<int> lp;
     std::vector<int32_t> bb;
     std::vector<int64_t> oo, ll;
@@ -917,7 +1041,7 @@ int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
     return ferr(H, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, H->P);
   std::lock_guard<std::mutex> lk(H->mu);
   const int S = H->S();
-  int total = 0;
+  int total = 0, n_staged = 0;
   int p = p_first;
   while (p < p_first + n_parts) {
     // a run of partitions of one owner with the same live slots -> one launch
@@ -941,12 +1065,26 @@ int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
       for (int q = p; q < e; ++q)
         for (int j = 0; j < k; ++j) {
           const int s = slots[j];
-          if (!H->peer[o][s])
-            return ferr(H, IPLS_E_DEVICE, "device %d has no peer access to device %d (xGMI)", H->devices[o],
-                        H->devices[s]);
           Partial& x = H->part[s][q];
           if (hipStreamWaitEvent(ost, x.ready, 0) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipStreamWaitEvent failed");
-          ptrs[(size_t)(q - p) * k + j] = x.d;
+          const void* src = x.d;
+          if (!H->peer[o][s] || (H->force_staged && s != o)) {
+            // no xGMI peer access: copy the partial into an owner-side buffer
+            // on the owner's stream (HIP routes the copy), then the same fold
+            // in the same slot order reads it locally
+            const size_t nb = (size_t)H->len[q] * 8;
+            if (!x.stage && hipMalloc(&x.stage, nb) != hipSuccess) {
+              (void)hipGetLastError();
+              return ferr(H, IPLS_E_NOMEM, "staging buffer of partition %d on device %d", q, H->devices[o]);
+            }
+            if (hipMemcpyPeerAsync(x.stage, H->devices[o], x.d, H->devices[s], nb, ost) != hipSuccess) {
+              (void)hipGetLastError();
+              return ferr(H, IPLS_E_DEVICE, "partial copy from device %d to %d failed", H->devices[s], H->devices[o]);
+            }
+            src = x.stage;
+            ++n_staged;
+          }
+          ptrs[(size_t)(q - p) * k + j] = src;
         }
       // REP[q] = ((REP[q] + R_s1) + R_s2) ...: the Updater replica branch /
       // Collect_Replicas fold (Updater.java:40-44, IPLS.java:1222-1234)
@@ -966,6 +1104,7 @@ int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
     }
     p = e;
   }
+  H->last_staged.store(n_staged, std::memory_order_relaxed);
   return total;
 }
 

@@ -72,7 +72,7 @@ class LaunchInfo(ctypes.Structure):
         ("vectors", ctypes.c_int32), ("seqf", ctypes.c_int32), ("map", ctypes.c_int32),
         ("grid", ctypes.c_int64),
         ("be_in", ctypes.c_int32), ("be_out", ctypes.c_int32), ("start", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("staged", ctypes.c_int32),
     ]
 
 
@@ -136,22 +136,54 @@ SIGNATURES = {
 _lib = None
 
 
+def load(path) -> ctypes.CDLL:
+    """Load and bind one build of the library (every symbol of the header)."""
+    if not Path(path).exists():
+        raise ImportError(
+            f"{path} not found: build it with `make -C ipls-java-api_amd` "
+            "(or __graft_entry__.build()); the aggregator has no CPU fallback")
+    L = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def lib() -> ctypes.CDLL:
     """Load the in-tree HIP library.  Raises if it has not been built --
     there is deliberately no CPU path behind this package."""
     global _lib
     if _lib is None:
-        if not LIB_PATH.exists():
-            raise ImportError(
-                f"{LIB_PATH} not found: build it with `make -C ipls-java-api_amd` "
-                "(or __graft_entry__.build()); the aggregator has no CPU fallback")
-        L = ctypes.CDLL(str(LIB_PATH))
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = load(LIB_PATH)
     return _lib
+
+
+def build_info() -> dict:
+    """Provenance of the library this process loads: its sha256 now, and the
+    build stamp written next to it at link time (tools/build_stamp.py: git
+    revision, whether the library's sources differed from it, kernel-source
+    sha256).  `stamp_matches_so` is False when the .so was replaced after the
+    stamp was written."""
+    import hashlib
+    import json
+    h = hashlib.sha256()
+    with open(LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    info = {"so": LIB_PATH.name, "so_sha256": h.hexdigest()}
+    stamp = LIB_PATH.with_name(LIB_PATH.name + ".buildinfo.json")
+    try:
+        rec = json.loads(stamp.read_text())
+    except (OSError, ValueError):
+        rec = None
+    if rec is None:
+        info.update(git_rev=None, sources_dirty=None, kernel_src_sha256=None, stamp_matches_so=None)
+    else:
+        info.update(git_rev=rec.get("git_rev"), sources_dirty=rec.get("sources_dirty"),
+                    kernel_src_sha256=rec.get("kernel_src_sha256"),
+                    stamp_matches_so=rec.get("so_sha256") == info["so_sha256"])
+    return info
 
 
 def last_error(h=None) -> str:

@@ -93,11 +93,13 @@ class Aggregator:
 
     def __init__(self, model_size: int = 0, n_partitions: int = 1, *, max_peers: int = 0,
                  partial_aggregation: int = 0, secure: bool = False, device: int = 0,
-                 bucket_len: int = 0, devices=None):
+                 bucket_len: int = 0, devices=None, library=None):
         """``devices``: a list of HIP device ordinals shards the partitions over
         several GPUs in contiguous blocks (cfg.devices, ipls_shard_plan); a
-        device may repeat (several shards on one GPU)."""
-        self._lib = N.lib()
+        device may repeat (several shards on one GPU).  ``library``: another
+        build of the C-ABI (``ipls._native.load(path)``) for same-process A/B
+        runs; default the in-tree library."""
+        self._lib = library if library is not None else N.lib()
         devs = None if devices is None else (ctypes.c_int32 * len(devices))(*devices)
         cfg = N.AggCfg(model_size=model_size, n_partitions=n_partitions, max_peers=max_peers,
                        partial_aggregation=partial_aggregation, secure=int(bool(secure)),
@@ -134,6 +136,9 @@ class Aggregator:
             pass
 
     def _chk(self, rc):
+        if rc < 0 and self._lib is not N.lib():   # a variant build keeps its own error slot
+            msg = self._lib.ipls_agg_last_error(None)
+            raise N.IplsError(rc, msg.decode(errors="replace") if msg else "")
         return N.check(rc, self._h)
 
     @property
@@ -482,7 +487,9 @@ class Aggregator:
             if not replace_agg:
                 self.Update(tensor.numpy(), partition, from_clients=False)
                 return
-            tensor = tensor.to(f"cuda:{self.device}")   # exact FIRST-start copy needs a device operand
+            # exact FIRST-start copy needs a device operand: on the GPU of the
+            # shard that owns the partition (the one whose kernel reads it)
+            tensor = tensor.to(f"cuda:{self.partition_device(partition)[0]}")
         d = DeviceBuffer.from_tensor(tensor)
         if replace_agg:
             self.reduce_batch(partition, [[d]], start_mode=N.START_FIRST, target=N.TGT_AGG)
@@ -518,13 +525,32 @@ class Aggregator:
         return self._chk(self._lib.ipls_agg_combine_partials(self._h, p_first, n))
 
     # ---- publish-side codec (a9) ----
+    @staticmethod
+    def _device_text_out(out, out_cap, need: int):
+        """(address, capacity in bytes) of a device text destination.  A
+        DeviceBuffer's capacity is its own size (8 * n); a raw address must come
+        with ``out_cap`` -- the library can only bound its writes by what it is
+        told, so an undersized buffer is refused here, never written past."""
+        if isinstance(out, DeviceBuffer):
+            ptr, cap = out.ptr, 8 * out.n
+            if out_cap is not None:
+                cap = min(cap, int(out_cap))
+        else:
+            if out_cap is None:
+                raise ValueError("a raw device address needs out_cap= (its capacity in bytes)")
+            ptr, cap = int(out), int(out_cap)
+        if cap < need:
+            raise ValueError(f"publish text needs {need} bytes, the device buffer holds {cap}")
+        return ptr, cap
+
     def publish_partial(self, partition: int, a: int, b: int, *, pid: int = 3, origin: bytes = b"",
-                        target: int = N.TGT_AGG, out=None) -> bytes | int:
+                        target: int = N.TGT_AGG, out=None, out_cap: int | None = None) -> bytes | int:
         """Marshall_Packet(target[p], origin, a, b, pid) as Base64.getUrlEncoder
         text (MyIPFSClass.java:990-1016; IPLS.java:1429-1430 publishes AGG with
         a = iteration, b = workers + 1, pid 3), encoded on the GPU.  Returns the
-        text bytes, or its length when ``out`` is a DeviceBuffer/int address
-        (device text, stream-ordered) or a PinnedBuffer (host text)."""
+        text bytes, or its length when ``out`` is a DeviceBuffer / int address
+        with ``out_cap`` bytes (device text, stream-ordered) or a PinnedBuffer
+        (host text)."""
         o = np.frombuffer(bytes(origin), dtype=np.uint8)
         op = o.ctypes.data if o.size else None
         n = self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op, o.size,
@@ -535,21 +561,22 @@ class Aggregator:
             return self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op,
                                                                 o.size, out.ptr, n, N.HOST_TEXT))
         if out is not None:
-            ptr = out.ptr if isinstance(out, DeviceBuffer) else int(out)
+            ptr, cap = self._device_text_out(out, out_cap, n)
             return self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op,
-                                                                o.size, ptr, n, N.DEV_TEXT))
+                                                                o.size, ptr, cap, N.DEV_TEXT))
         buf = np.empty(max(1, n), dtype=np.uint8)
         self._chk(self._lib.ipls_agg_publish_partial(self._h, partition, target, a, b, pid, op, o.size,
                                                      buf.ctypes.data, n, N.HOST_TEXT))
         return buf[:n].tobytes()
 
     def publish_partials(self, partitions, a: int, b, *, pid: int = 3, origin: bytes = b"",
-                         target: int = N.TGT_AGG, out=None):
+                         target: int = N.TGT_AGG, out=None, out_cap: int | None = None):
         """The publish loop over Auth_List (IPLS.java:1423-1431) in one launch
         per GPU: text i = Marshall_Packet(target[partitions[i]], origin, a,
         b[i], pid) base64url-encoded.  Returns the list of texts (bytes), or,
-        when ``out`` is a device address / DeviceBuffer / PinnedBuffer, the
-        (lens, offs) of the texts written there (device: stream-ordered)."""
+        when ``out`` is a DeviceBuffer / device address with ``out_cap`` bytes /
+        PinnedBuffer, the (lens, offs) of the texts written there (device:
+        stream-ordered)."""
         parts = np.ascontiguousarray(list(partitions), dtype=np.int32)
         bb = np.ascontiguousarray(list(b), dtype=np.int32)
         if bb.size != parts.size:
@@ -566,8 +593,7 @@ class Aggregator:
             if isinstance(out, PinnedBuffer):
                 ptr, cap, kind = out.ptr, out.nbytes, N.HOST_TEXT
             else:
-                ptr = out.ptr if isinstance(out, DeviceBuffer) else int(out)
-                cap, kind = total, N.DEV_TEXT
+                (ptr, cap), kind = self._device_text_out(out, out_cap, total), N.DEV_TEXT
             self._chk(self._lib.ipls_agg_publish_partials(
                 self._h, parts.ctypes.data, n, target, a, bb.ctypes.data, pid, op, o.size, ptr, cap, kind,
                 None, None))
@@ -582,7 +608,7 @@ class Aggregator:
         """What the last fold launch ran (kernel, shape, lanes, vectors, SEQ code, map, grid)."""
         li = N.LaunchInfo()
         self._chk(self._lib.ipls_agg_last_launch(self._h, ctypes.byref(li)))
-        return {f: getattr(li, f) for f, _ in N.LaunchInfo._fields_ if f != "reserved"}
+        return {f: getattr(li, f) for f, _ in N.LaunchInfo._fields_}
 
     # ---- state access ----
     def read(self, partition: int, target: int = N.TGT_AGG, *, big_endian: bool = False):

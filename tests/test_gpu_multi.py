@@ -226,6 +226,89 @@ def test_sharded_ingest_indirect_async_and_replicas(ipls, O):
     two.close()
 
 
+def test_staged_combine_and_indirect_without_peer_access(ipls, O, monkeypatch):
+    """a device pair without xGMI peer access is not an
+    error.  IPLS_PEER_STAGED=1 (read at open) forces the fallback on [0, 0, 0]:
+    every remote partial is copied into an owner-side buffer on the owner's
+    stream and the SAME fold reads it in the same slot order -- bit-identical
+    to the oracle's replica expression; the hash-only requests' Gradient_Buff
+    (on shard 0) is staged into the other shards the same way.  Two rounds, so
+    the staging buffers are reused behind the `consumed` ordering."""
+    monkeypatch.setenv("IPLS_PEER_STAGED", "1")
+    P, L, K, kh = 3, 600_007, 6, 2
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0, 0, 0])
+    monkeypatch.delenv("IPLS_PEER_STAGED")
+    t, rows = dev_buckets(ipls, P, L, K)
+    for rnd in range(2):
+        agg.reduce_batch(0, [r[:kh] for r in rows], start_mode=ipls.START_ZERO)
+        for q in range(P):
+            a, b = [s for s in range(3) if s != q]
+            agg.reduce_partial(a, q, [rows[q][kh:kh + 2]])
+            agg.reduce_partial(b, q, [rows[q][kh + 2:]])
+        assert agg.combine_partials() == 2 * P
+        assert agg.last_launch()["staged"] == 2 * P, rnd
+        agg.AggregatePartition(ipls.ALL_PARTITIONS)
+        for q in range(P):
+            b = [O.synth_bucket(L, q, k) for k in range(K)]
+            own = O.reduce(b[:kh], L)
+            rep = (0.0 + O.reduce(b[kh:kh + 2], L)) + O.reduce(b[kh + 2:], L)
+            assert_bits_equal(agg.read(q, ipls.TGT_WEIGHTS), own + rep, f"round {rnd} W[{q}]")
+    # without the switch the same handle shape uses peer loads (nothing staged)
+    plain = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0, 0, 0])
+    plain.reduce_partial(1, 0, [rows[0][kh:kh + 2]])
+    assert plain.combine_partials() == 1 and plain.last_launch()["staged"] == 0
+    plain.close()
+    # hash-only requests through the staged Gradient_Buff vs a one-shard handle
+    M = 300_001
+    one = ipls.Aggregator(M, P)
+    monkeypatch.setenv("IPLS_PEER_STAGED", "1")
+    three = ipls.Aggregator(M, P, devices=[0, 0, 0])
+    monkeypatch.delenv("IPLS_PEER_STAGED")
+    Ls = one.lengths
+    for p, n in ((2, Ls[2]), (0, Ls[0] - 70), (1, 33), (2, 5), (1, Ls[1])):
+        data = O.be_encode(O.synth_bucket(n, p, 17))
+        one.UpdateIndirect(data, p)
+        three.UpdateIndirect(data, p)
+    for p in range(P):
+        assert_bits_equal(three.read(p), one.read(p), f"indirect AGG[{p}]")
+    one.close()
+    three.close()
+    agg.close()
+
+
+def test_indirect_requests_from_two_threads_on_two_shards(ipls, O):
+    """the handle's ONE Gradient_Buff lives on shard 0, so a
+    hash-only request for a partition of shard 1 loads it there and folds it
+    over on shard 1.  Two threads feed different files to a partition of each
+    shard at once; each partition must receive exactly its own files (the
+    load -> fold -> hand-back sequence is one critical section for every
+    shard, shard 0 included).  Files are full length, so every partition's
+    result is its own thread's fixed-order fold, whatever the interleaving."""
+    import threading
+    M, P, n_req = 400_004, 4, 24
+    agg = ipls.Aggregator(M, P, devices=[0, 0])
+    Ls = agg.lengths
+    files = {p: [O.be_encode(O.synth_bucket(Ls[p], p, 100 + i)) for i in range(n_req)] for p in (0, 3)}
+    errs = []
+
+    def feed(p):
+        try:
+            for f in files[p]:
+                agg.UpdateIndirect(f, p)
+        except Exception as e:   # noqa: BLE001
+            errs.append(e)
+    th = [threading.Thread(target=feed, args=(p,)) for p in (0, 3)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for p in (0, 3):
+        want = O.reduce([np.frombuffer(f, dtype=">f8").astype(np.float64) for f in files[p]], Ls[p])
+        assert_bits_equal(agg.read(p), want, f"AGG[{p}]")
+    agg.close()
+
+
 # ---------------------------------------------------------------------------
 # a9: Marshall_Packet + Base64.getUrlEncoder on the device
 # ---------------------------------------------------------------------------
@@ -252,9 +335,23 @@ def test_publish_partial_matches_marshall_packet(ipls, O, L, origin):
     assert len(text) == len(want) and text == want
     # device text
     buf = torch.empty(len(want) + 16, dtype=torch.uint8, device="cuda")
-    n = agg.publish_partial(1, 12, 4, origin=origin, out=int(buf.data_ptr()))
+    n = agg.publish_partial(1, 12, 4, origin=origin, out=int(buf.data_ptr()), out_cap=buf.numel())
     agg.sync()
     assert n == len(want) and bytes(buf[:n].cpu().numpy()) == want
+    # an undersized device buffer is refused before anything is written:
+    # a DeviceBuffer's size is its own, a raw address needs its capacity
+    small = torch.full((len(want) + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError):
+        agg.publish_partial(1, 12, 4, origin=origin, out=ipls.DeviceBuffer(int(small.data_ptr()), (len(want) - 1) // 8))
+    with pytest.raises(ValueError):
+        agg.publish_partial(1, 12, 4, origin=origin, out=int(small.data_ptr()))
+    with pytest.raises(ValueError):
+        agg.publish_partial(1, 12, 4, origin=origin, out=int(small.data_ptr()), out_cap=len(want) - 1)
+    with pytest.raises(ValueError):
+        agg.publish_partials([1], 12, [4], origin=origin, out=int(small.data_ptr()), out_cap=len(want) - 1)
+    agg.sync()
+    assert bool((small == 0xAB).all())
     # round trip: the IPFS daemon wraps the text once more (IPLS.java:855-859)
     rx = ipls.Aggregator(n_partitions=13, bucket_len=L)
     k, st = rx.ingest_pubsub([O.java_b64url_encode(text)], layers=2)   # routed by field a = 12
@@ -368,7 +465,8 @@ def test_publish_partials_batch_matches_single(ipls, O):
     # device memory
     dev = torch.zeros(pos + 64, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()   # torch's stream; the handle's stream does not order after it
-    assert agg.publish_partials(parts, 12, bs, origin=origin, out=int(dev.data_ptr())) == (lens, offs)
+    assert agg.publish_partials(parts, 12, bs, origin=origin, out=int(dev.data_ptr()),
+                                out_cap=dev.numel()) == (lens, offs)
     agg.sync()
     host = dev.cpu().numpy().tobytes()
     for i, t in enumerate(texts):

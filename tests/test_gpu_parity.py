@@ -1467,7 +1467,7 @@ def test_full_ipls_round_four_peers(ipls, O):
 
 @pytest.mark.parametrize("seed,group,devices", [(1, 1, None), (2, 4, None), (3, 32, None), (4, 2, None), (5, 8, None),
                                                 (6, 4, [0, 0]), (7, 32, [0, 0, 0])])
-def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, steps=300, shapes=None):
+def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, steps=300, shapes=None, prefix=()):
     """A random sequence over the whole accumulator surface, checked step by
     step against a numpy model of the Java state (Aggregated_Gradients,
     Replicas_Gradients, Aggregated_Gradients_from_future, Weights): host and
@@ -1479,8 +1479,11 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     sequence through a multi-device handle (shards [0,2) | [2,4), and a
     three-entry list whose last shard owns no partition), so the front's
     routing of every call is checked against the same model.  ``shapes``: a
-    set that collects the (kernel, shape, map) of every batched launch, for
-    callers that must show which production shapes a sequence reached."""
+    set that collects the (kernel, shape, map, big-endian, start) of every
+    batched launch, for callers that must show which production shapes a
+    sequence reached.  ``prefix``: scripted steps run before the random ones,
+    each a dict fixing some of a step's draws (op, p, n, kk, mode, be, tg);
+    the draws it does not fix come from the rng as usual."""
     rng = np.random.default_rng(seed)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
     agg.set_coalesce(group)
@@ -1506,9 +1509,14 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     gbuf = np.zeros(L)          # the Updater's one Gradient_Buff (synthetic geometry: L doubles)
     store = {}                  # Other_Replica_Gradients
     msgs = [O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmS")) for g in pool]
-    for step in range(steps):
-        op = int(rng.integers(0, 17))
-        p = int(rng.integers(0, P))
+    script = list(prefix)
+    for step in range(len(script) + steps):
+        fixed = script[step] if step < len(script) else {}
+
+        def draw(key, fn):
+            return fixed[key] if key in fixed else fn()
+        op = draw("op", lambda: int(rng.integers(0, 17)))
+        p = draw("p", lambda: int(rng.integers(0, P)))
         k = int(rng.integers(0, len(pool)))
         g = pool[k]
         if op == 0:                                         # Updater._Update from host bytes/doubles
@@ -1526,17 +1534,17 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
             agg.UpdateAsync(DB[k] if rng.integers(0, 3) == 0 else D[k], p, from_clients=tg == ipls.TGT_AGG)
             M[T[tg]][p] = M[T[tg]][p] + g
         elif op == 4:                                       # batched folds, any start mode
-            n = int(rng.integers(1, P - p + 1))
-            kk = int(rng.integers(1, 4))
+            n = draw("n", lambda: int(rng.integers(1, P - p + 1)))
+            kk = draw("kk", lambda: int(rng.integers(1, 4)))
             ks = [[int(x) for x in rng.integers(0, len(pool), kk)] for _ in range(n)]
-            mode = [ipls.START_ZERO, ipls.START_ACCUM, ipls.START_FIRST][int(rng.integers(0, 3))]
-            be = bool(rng.integers(0, 2))
-            tg = [ipls.TGT_AGG, ipls.TGT_REP][int(rng.integers(0, 2))]
+            mode = draw("mode", lambda: [ipls.START_ZERO, ipls.START_ACCUM, ipls.START_FIRST][int(rng.integers(0, 3))])
+            be = draw("be", lambda: bool(rng.integers(0, 2)))
+            tg = draw("tg", lambda: [ipls.TGT_AGG, ipls.TGT_REP][int(rng.integers(0, 2))])
             agg.reduce_batch(p, [[(DB if be else D)[j] for j in row] for row in ks], start_mode=mode, target=tg,
                              big_endian=be)
             if shapes is not None:
                 li = agg.last_launch()
-                shapes.add((li["kernel"], li["shape"], li["map"], be))
+                shapes.add((li["kernel"], li["shape"], li["map"], be, mode))
             for q, row in enumerate(ks):
                 bufs = [pool[j] for j in row]
                 M[T[tg]][p + q] = O.reduce(bufs, L, mode, acc=M[T[tg]][p + q])
@@ -1569,13 +1577,13 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
             agg.cache_partition(p, O.be_encode(g[:n]))
             M["w"][p][:n] = g[:n]
         elif op == 10:                                      # fused round over a range
-            n = int(rng.integers(1, P - p + 1))
-            kk = int(rng.integers(0, 3))
+            n = draw("n", lambda: int(rng.integers(1, P - p + 1)))
+            kk = draw("kk", lambda: int(rng.integers(0, 3)))
             ks = [[int(x) for x in rng.integers(0, len(pool), kk)] for _ in range(n)]
             avg = agg.aggregate_round(p, [[D[j] for j in row] for row in ks])
             if shapes is not None and kk:
                 li = agg.last_launch()
-                shapes.add((li["kernel"], li["shape"], li["map"], False))
+                shapes.add((li["kernel"], li["shape"], li["map"], False, -1))
             exp = []
             for q, row in enumerate(ks):
                 a = O.reduce([pool[j] for j in row], L, ipls.START_ACCUM, acc=M["agg"][p + q]) if row \
@@ -1621,18 +1629,44 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     agg.close()
 
 
-@pytest.mark.parametrize("seed,P,L", [(23, 4, 4 * 1048576 + 5), (22, 1, 4 * 1048576 + 3)])
+def production_prefix(ipls, P):
+    """Scripted steps that reach every production launch shape whatever the
+    seed: a batched fold over all P partitions (the big 1024-lane tiles when
+    P = 4) and over one partition (the 256-lane mid shape), for each byte order
+    and each start mode, then the fused round over all P and over one.  Each
+    fused round and AggregatePartition in between keeps the state moving."""
+    steps = []
+    for be in (False, True):
+        for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
+            for p, n in ((0, P), (P - 1, 1)):
+                steps.append({"op": 4, "p": p, "n": n, "kk": 2, "mode": mode, "be": be, "tg": ipls.TGT_AGG})
+            steps.append({"op": 5, "p": 0})
+    steps.append({"op": 10, "p": 0, "n": P, "kk": 2})
+    steps.append({"op": 10, "p": P - 1, "n": 1, "kk": 2})
+    return steps
+
+
+@pytest.mark.parametrize("seed,P,L", [(21, 4, 4 * 1048576 + 5), (22, 4, 4 * 1048576 + 5), (23, 4, 4 * 1048576 + 5),
+                                      (22, 1, 4 * 1048576 + 3)])
 def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
     """The random sequence at config-C bucket lengths (ragged, so every batch
     ends in a partial tile), so that its batched folds and fused rounds run
     the production launch shapes -- the big 1024-lane R = 16 / R = 8 tiles
     and the 256-lane mid shape, native and big-endian, every start mode --
-    interleaved with every other call on the same state.  Four partitions
-    reach the big shape (batches of 2-4 partitions) and the mid one (single
-    partitions); one partition reaches the mid shape only."""
+    interleaved with every other call on the same state.  A scripted prefix
+    (production_prefix) reaches every (shape, byte order, start mode) and the
+    fused round's shapes first, so the coverage does not depend on the seed
+    (seed 21 alone never reached the big shape); the random steps
+    follow.  With one partition only the mid shape exists."""
     shapes = set()
-    test_stateful_random_sequence(ipls, O, seed, 32, None, P=P, L=L, steps=300, shapes=shapes)
-    reduce_shapes = {(s, be) for k, s, _, be in shapes if k == ipls.KERNEL_REDUCE}
-    assert (ipls.SHAPE_MID, False) in reduce_shapes and (ipls.SHAPE_MID, True) in reduce_shapes, shapes
-    if P == 4:
-        assert (ipls.SHAPE_BIG, False) in reduce_shapes and (ipls.SHAPE_BIG, True) in reduce_shapes, shapes
+    test_stateful_random_sequence(ipls, O, seed, 32, None, P=P, L=L, steps=300, shapes=shapes,
+                                  prefix=production_prefix(ipls, P))
+    reduce_shapes = {(s, be, mode) for k, s, _, be, mode in shapes if k == ipls.KERNEL_REDUCE}
+    sizes = (ipls.SHAPE_BIG, ipls.SHAPE_MID) if P == 4 else (ipls.SHAPE_MID,)
+    for shape in sizes:
+        for be in (False, True):
+            for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
+                assert (shape, be, mode) in reduce_shapes, (shape, be, mode, sorted(reduce_shapes))
+    round_shapes = {s for k, s, _, _, _ in shapes if k == ipls.KERNEL_ROUND}
+    for shape in sizes:
+        assert shape in round_shapes, (shape, sorted(round_shapes))

@@ -1,0 +1,43 @@
+#!/bin/bash
+# GPU-box script for the round-3 A/Bs (from the repo root):
+#   shard pool: tools/shard_pool_probe.py on the round-2 library vs the current one
+#   D schedule: bench.py --be-schedule-ab in three processes
+#   D-be PMC:   FETCH_SIZE / WRITE_SIZE passes of config D (BE in + out) on the current library
+# Usage: tools/gpu_ab.sh TAG [steps...]   (steps: pool, dsched, dpmc; default all)
+set -o pipefail
+TAG=${1:-ab}; shift
+STEPS=${*:-pool dsched dpmc}
+R=$(pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    pool)
+      for lib in ab/libipls_agg_r2.so libipls_agg.so; do
+        IPLS_AGG_LIB=$R/ipls-java-api_amd/lib/$lib timeout -k 10 120 python tools/shard_pool_probe.py 2000 8 \
+          >> $O/shard_pool_probe.jsonl 2>> $O/shard_pool_probe.err || exit 21
+      done
+      IPLS_AGG_LIB=$R/ipls-java-api_amd/lib/ab/libipls_agg_r2.so timeout -k 10 120 python tools/shard_pool_probe.py 2000 8 \
+        >> $O/shard_pool_probe.jsonl 2>> $O/shard_pool_probe.err || exit 21
+      timeout -k 10 120 python tools/shard_pool_probe.py 2000 8 >> $O/shard_pool_probe.jsonl 2>> $O/shard_pool_probe.err || exit 21
+      ;;
+    dsched)
+      for i in 1 2 3; do
+        timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-other-configs \
+          --no-per-arrival --be-schedule-ab >> $O/be_schedule_ab.jsonl 2>> $O/be_schedule_ab.err || exit 22
+      done
+      ;;
+    dpmc)
+      cd /tmp
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_D -o run -- \
+        python3 $R/bench.py --config D --be --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
+        --steps 3 --warmup 1 > $O/pmc_fetch_D.log 2>&1 || exit 23
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/pmc_write_D -o run -- \
+        python3 $R/bench.py --config D --be --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
+        --steps 3 --warmup 1 > $O/pmc_write_D.log 2>&1 || exit 24
+      cd $R
+      ;;
+  esac
+done
+echo done > $O/done
