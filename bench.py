@@ -37,6 +37,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "aggregated-gradient GB/s (device-resident), 32 peers×4M doubles/partition"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0       # one xGMI link, per direction (7 links per GPU)
 
 CONFIGS = {
     # name: (partitions per GPU, bucket length incl. count slot, peers)
@@ -445,22 +446,35 @@ def c_abi_multi_gpu(ipls, torch, devices, P: int, L: int, K: int, reps: int = 5,
             torch.cuda.synchronize(d)
         own = [r[:kh] for r in rows]
 
+        # per owner shard: its stream (HIP events around the combine's launch there)
+        owner_streams = []
+        for o in range(G):
+            d, st = agg.partition_device(o * P)
+            owner_streams.append(torch.cuda.ExternalStream(st, device=torch.device("cuda", d)))
+
         def one_round():
             agg.reduce_batch(0, own, start_mode=ipls.START_ZERO)
             for p in range(PT):
                 agg.reduce_partial(slot[p], p, [far[p]], start_mode=ipls.START_ZERO)
             agg.sync()
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+            for o in range(G):
+                evs[o][0].record(owner_streams[o])
             t0 = time.perf_counter()
             n = agg.combine_partials()
+            for o in range(G):
+                evs[o][1].record(owner_streams[o])
             agg.sync()
             t1 = time.perf_counter()
             agg.AggregatePartition(ipls.ALL_PARTITIONS)
             agg.sync()
-            return t1 - t0, n
+            return t1 - t0, n, [a.elapsed_time(b) for a, b in evs]
         one_round()
-        ex = []
+        ex, per_owner = [], []
         for _ in range(reps):
-            ex.append(one_round()[0])
+            t, _, ev_ms = one_round()
+            ex.append(t)
+            per_owner.append(ev_ms)
         tex = float(np.median(ex))
         moved = PT * L * 8
         out["combine_ms"] = round(tex * 1e3, 4)
@@ -468,6 +482,24 @@ def c_abi_multi_gpu(ipls, torch, devices, P: int, L: int, K: int, reps: int = 5,
         out["combine_note"] = (f"{PT} partials of {L * 8 / 2**20:.0f} MiB pulled by their owners "
                                "(peer loads over xGMI; shards on one GPU read local memory), folded into REP in "
                                "slot order; median of the combine step alone")
+        # the combine's roofline: per owner, its P partials arrive
+        # over the xGMI links of the distinct GPUs holding them; algorithmic
+        # bytes = partials * L * 8 over xGMI + L * 8 REP write per partition
+        # (+ L * 8 REP read when REP already held a value -- not in this leg)
+        own_ms = np.median(np.asarray(per_owner), axis=0)
+        links = [len({devices[slot[o * P + q]] for q in range(P)} - {devices[o]}) for o in range(G)]
+        xg = P * L * 8
+        fr = [xg / (own_ms[o] / 1e3) / (links[o] * XGMI_LINK_GBS * 1e9) if links[o] else None for o in range(G)]
+        out["combine"] = {
+            "bytes_formula": "per partition: S*L*8 (S remote partials over xGMI) + L*8 (REP write) [+ L*8 REP read]",
+            "xgmi_bytes_per_owner": xg, "algorithmic_bytes_per_owner": xg + P * L * 8,
+            "owner_kernel_ms": [round(float(x), 4) for x in own_ms], "links_per_owner": links,
+            "xgmi_link_GBps": XGMI_LINK_GBS,
+            "frac_of_xgmi": [None if f is None else round(f, 4) for f in fr],
+            "frac_of_xgmi_min": None if None in fr else round(min(fr), 4),
+            "status": ("rehearsal: every shard on one GPU, local reads (no xGMI link); unmeasured on hardware"
+                       if len(set(devices)) == 1 else "measured: distinct GPUs, peer loads over xGMI"),
+            "timing": "HIP events on each owner's stream around the combine launch, median of the rounds"}
         if verify:
             from oracle import oracle as O   # checker only
             out["verified_replica_checksum_p0"] = (agg.checksum(0, ipls.TGT_WEIGHTS) ==
@@ -478,14 +510,17 @@ def c_abi_multi_gpu(ipls, torch, devices, P: int, L: int, K: int, reps: int = 5,
     return out
 
 
-def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, verify: bool = True) -> dict:
+def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, verify: bool = True,
+               rounds: int = 4) -> dict:
     """One more BASELINE config on the same box, N=1: B
     (16 x 1M x 8, native doubles) or D (64 x 4M x 32) with big-endian IPFS
     bytes in and the sum packed to big-endian bytes out, i.e. config D's
     'double<->byte pack/unpack in the timed region', or F (one GPU's slice of
     config F: 16 x 8M x 64, 69.8 GB of buckets resident).  Same algorithmic-bytes
     accounting as the headline; kernel time by HIP events on the handle's
-    stream; partition 0 checked against the oracle's checksum."""
+    stream, `rounds` rounds of `steps` launches, the median round reported
+    (the first launches after a fresh allocation can run a few % slow);
+    partition 0 checked against the oracle's checksum."""
     P, L, K = CONFIGS[name]
     elem = L + 32
     arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
@@ -506,13 +541,17 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
     step()
     step()
     agg.sync()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-    ev[0].record(stream)
-    for i in range(steps):
-        step()
-        ev[i + 1].record(stream)
-    agg.sync()
-    ms = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)]))
+    per_round = []
+    for _ in range(rounds):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        ev[0].record(stream)
+        for i in range(steps):
+            step()
+            ev[i + 1].record(stream)
+        agg.sync()
+        per_round.append(float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])))
+    ms = float(np.median(per_round))
+    launch = agg.last_launch()
     nbytes = P * (K + 1) * L * 8
     verified = None
     if verify:
@@ -525,6 +564,8 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
                         + (" (BE IPFS bytes in, BE sum bytes out: fused unpack/pack)" if be else ""),
             "kernel_ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
             "frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes,
+            "round_ms": [round(x, 4) for x in per_round],
+            "launch": {k: launch[k] for k in ("shape", "block", "vectors", "seqf", "map", "grid")},
             "verified_checksum_p0": verified}
 
 
@@ -1217,7 +1258,7 @@ def main():
             # the other single-GPU BASELINE configs, measured in the same run (never the value)
             del arena, rows
             torch.cuda.empty_cache()
-            # B's launch is 0.19 ms: 50 launches (10 ms) average out the ramp of the first ones
+            # B's launch is 0.19 ms: 50 launches (10 ms) per round average out the ramp of the first ones
             out["other_configs"] = {nm: side(config_leg, ipls, torch, nm, be, local, steps=st,
                                              verify=not args.no_verify)
                                     for nm, be, st in (("B", False, 50), ("D", True, 5), ("F", False, 5))}

@@ -49,14 +49,19 @@ static void throw_iae(JNIEnv *env, const char *what) {
 #define H(x) ((ipls_agg *)(intptr_t)(x))
 #define CHECK(rc, h) do { int rc_ = (rc); if (rc_ < 0) { throw_for(env, rc_, (h)); } } while (0)
 
-/* The bytes [pos, pos + nbytes) of a direct buffer, or NULL with an
+/* The bytes [pos, pos + count * elem) of a direct buffer, or NULL with an
  * IllegalArgumentException pending. */
-static void *direct_span(JNIEnv *env, jobject buf, jint pos, jlong nbytes) {
+static void *direct_span(JNIEnv *env, jobject buf, jint pos, jlong count, jlong elem) {
     if (!buf) { throw_iae(env, "null buffer"); return NULL; }
     char *a = (char *)(*env)->GetDirectBufferAddress(env, buf);
     const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
     if (!a || cap < 0) { throw_iae(env, "not a direct ByteBuffer (allocate it with hostAlloc)"); return NULL; }
-    if (pos < 0 || nbytes < 0 || (jlong)pos + nbytes > cap) { throw_iae(env, "position/length outside the buffer"); return NULL; }
+    /* count elements of elem bytes from byte pos: checked before any
+     * multiplication, so a huge count from Java cannot overflow */
+    if (pos < 0 || (jlong)pos > cap || count < 0 || count > (cap - (jlong)pos) / elem) {
+        throw_iae(env, "position/length outside the buffer");
+        return NULL;
+    }
     return a + pos;
 }
 
@@ -208,7 +213,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                                 jobject buf, jint pos, jlong n, jint kind) {
     (void)c;
-    void *src = direct_span(env, buf, pos, 8 * n);
+    void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
     CHECK(ipls_agg_accumulate(H(h), p, tgt, src, n, kind), H(h));
 }
@@ -217,7 +222,7 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_accumulateAsyncDirect(JNIEnv *env,
                                                                       jint tgt, jobject buf, jint pos, jlong n,
                                                                       jint kind) {
     (void)c;
-    void *src = direct_span(env, buf, pos, 8 * n);
+    void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return 0;
     uint64_t t = 0;
     CHECK(ipls_agg_accumulate_async(H(h), p, tgt, src, n, kind, &t), H(h));
@@ -237,7 +242,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_flushQueued(JNIEnv *env, jclass c, 
 JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                               jobject buf, jint pos, jlong nBytes) {
     (void)c;
-    void *src = direct_span(env, buf, pos, nBytes);
+    void *src = direct_span(env, buf, pos, nBytes, 1);
     if (!src) return;
     CHECK(ipls_agg_update_indirect(H(h), p, tgt, src, nBytes), H(h));
 }
@@ -314,7 +319,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartitionDirect(JNIEnv *env
     (void)c;
     const int64_t L = part_len(env, h, p);
     if (L < 0) return;
-    void *dst = direct_span(env, sum, pos, 8 * L);
+    void *dst = direct_span(env, sum, pos, L, 8);
     if (!dst) return;
     CHECK(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL), H(h));
 }
@@ -322,7 +327,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartitionDirect(JNIEnv *env
 JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclass c, jlong h, jint p, jobject buf,
                                                                 jint pos, jlong n) {
     (void)c;
-    void *src = direct_span(env, buf, pos, 8 * n);
+    void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
     CHECK(ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_BE), H(h));
 }
@@ -377,7 +382,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c
 JNIEXPORT void JNICALL Java_NativeAggregator_otherReplicaDirect(JNIEnv *env, jclass c, jlong h, jint p, jint a,
                                                                   jobject buf, jint pos, jlong n) {
     (void)c;
-    void *src = direct_span(env, buf, pos, 8 * n);
+    void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
     CHECK(ipls_agg_other_replica(H(h), p, a, src, n, IPLS_HOST_BE), H(h));
 }
@@ -478,7 +483,7 @@ done:
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jclass c, jlong h, jobject buf,
                                                                  jint pos, jlong nBytes) {
     (void)c;
-    void *dst = direct_span(env, buf, pos, nBytes);
+    void *dst = direct_span(env, buf, pos, nBytes, 1);
     if (!dst) return;
     CHECK(ipls_agg_get_partitions(H(h), dst, nBytes / 8, IPLS_HOST_BE_CANON), H(h));
 }
@@ -591,7 +596,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_publishPartialsDirect(JNIEnv *env, 
     if (!parts) { throw_iae(env, "null partition list"); return; }
     const jsize n = (*env)->GetArrayLength(env, parts);
     if (!need_len(env, b, n, "b (one value per partition)")) return;
-    void *dst = direct_span(env, buf, pos, cap);
+    void *dst = direct_span(env, buf, pos, cap, 1);
     if (!dst) return;
     const jsize ol = origin ? (*env)->GetArrayLength(env, origin) : 0;
     jint *pp = (*env)->GetIntArrayElements(env, parts, NULL);

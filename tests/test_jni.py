@@ -157,7 +157,15 @@ def test_direct_buffer_checks_before_the_library(jvm):
                        ("updateIndirect", (L64(0), 0, 0, buf, 8, L64(57))),
                        ("setWeightsDirect", (L64(0), 0, heap, 0, L64(1))),
                        ("otherReplicaDirect", (L64(0), 0, 1, buf, 0, L64(9))),
-                       ("getPartitionsWire", (L64(0), heap, 0, L64(8)))]:
+                       ("getPartitionsWire", (L64(0), heap, 0, L64(8))),
+                       # counts whose byte size overflows a jlong (8 * n wraps to a small or
+                       # negative value) are rejected before any multiplication
+                       ("accumulateDirect", (L64(0), 0, 0, buf, 0, L64(1 << 61), 1)),
+                       ("accumulateDirect", (L64(0), 0, 0, buf, 8, L64((1 << 63) - 1), 1)),
+                       ("accumulateAsyncDirect", (L64(0), 0, 0, buf, 0, L64((1 << 61) + 1), 1)),
+                       ("setWeightsDirect", (L64(0), 0, buf, 0, L64(1 << 62))),
+                       ("otherReplicaDirect", (L64(0), 0, 1, buf, 0, L64(1 << 61))),
+                       ("updateIndirect", (L64(0), 0, 0, buf, 65, L64(0)))]:          # pos past the end
         _, exc = jvm.call(name, *args)
         assert exc == "java/lang/IllegalArgumentException", (name, exc)
 

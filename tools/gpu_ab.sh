@@ -3,7 +3,12 @@
 #   shard pool: tools/shard_pool_probe.py on the round-2 library vs the current one
 #   D schedule: bench.py --be-schedule-ab in three processes
 #   D-be PMC:   FETCH_SIZE / WRITE_SIZE passes of config D (BE in + out) on the current library
-# Usage: tools/gpu_ab.sh TAG [steps...]   (steps: pool, dsched, dpmc; default all)
+#   B sweep:    tools/reduce_sweep.hip over config B's dispatch (lanes x vectors, big vs mid) beside the
+#               streaming-read and dwordx4-copy ceilings, three processes
+#   B PMC:      FETCH_SIZE / WRITE_SIZE passes of config B
+#   rehearsal:  bench.py --multi-rehearsal (the single-handle multi-GPU leg over two shards of GPU 0)
+#   bench:      the default bench line
+# Usage: tools/gpu_ab.sh TAG [steps...]   (steps: pool dsched dpmc bsweep bpmc rehearsal bench; default the first 3)
 set -o pipefail
 TAG=${1:-ab}; shift
 STEPS=${*:-pool dsched dpmc}
@@ -37,6 +42,29 @@ for s in $STEPS; do
         python3 $R/bench.py --config D --be --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
         --steps 3 --warmup 1 > $O/pmc_write_D.log 2>&1 || exit 24
       cd $R
+      ;;
+    bsweep)
+      for i in 1 2 3; do
+        SWEEP_QUICK=1 SWEEP_B=1 SWEEP_COPY=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 1048576 8 32 50 \
+          >> $O/sweep_B.txt 2>&1 || exit 25
+      done
+      ;;
+    bpmc)
+      cd /tmp
+      timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \
+        python3 $R/bench.py --config B --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
+        --steps 20 --warmup 2 > $O/pmc_fetch_B.log 2>&1 || exit 26
+      timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/pmc_write_B -o run -- \
+        python3 $R/bench.py --config B --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
+        --steps 20 --warmup 2 > $O/pmc_write_B.log 2>&1 || exit 27
+      cd $R
+      ;;
+    rehearsal)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-other-configs \
+        --no-per-arrival --multi-rehearsal > $O/bench_multi_rehearsal.json 2> $O/bench_multi_rehearsal.err || exit 28
+      ;;
+    bench)
+      timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 29
       ;;
   esac
 done

@@ -282,6 +282,16 @@ int main(int argc, char** argv) {
     ADDSB(8, 256, 0);
     ADDSB(16, 256, 0);
   }
+  if (getenv("SWEEP_B")) {   // config B (16 x 1M x 8): lanes x vectors per lane, big vs mid
+    ADDSB(16, 1024, 0);       // shipped big shape (512 tiles)
+    ADDSB(8, 1024, 0);
+    ADDSB(4, 1024, 0);
+    ADDSB(16, 512, 0);
+    ADDSB(8, 512, 0);
+    ADDSB(16, 256, 0);        // shipped mid shape
+    ADDSB(8, 256, 0);
+    ADDSB(4, 256, 0);
+  }
   if (getenv("SWEEP_BS")) {   // block size / fence interval of the big-endian fold
     ADDSB(16, 1024, 2);
     ADDSB(16, 512, 2);
