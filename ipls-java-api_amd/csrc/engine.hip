@@ -429,13 +429,16 @@ constexpr int big_r() { return START != kAccum ? (BE_IN ? IPLS_BE_BIG_R : 16) : 
 template <bool BE_IN, int START>
 constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? IPLS_BE_SEQF : 0; }
 // Block order of the big shape over whole tiles: partition-major (map 0),
-// except big-endian input on grids of at most 4096 tiles, which runs
-// XCD-chunked (map 2: each XCD walks one contiguous eighth of the work).  With
-// SEQF = 3, map 2 measured +2 to +3.6 points at 2-4 partitions of 4M x 32,
-// +0.2 to +0.6 at 16, and -3.6 at 64 (config D, 8192 tiles); native doubles
-// gain nothing from it (profiles/r02/s3/sweep_be_map.txt, sweep_map_fewp.txt).
+// except big-endian input on grids of at most 4096 tiles and native doubles
+// on grids of at most 512 (two waves of 256 CUs), which run XCD-chunked
+// (map 2: each XCD walks one contiguous eighth of the work).  With SEQF = 3,
+// map 2 measured +2 to +3.6 points at 2-4 partitions of 4M x 32, +0.2 to +0.6
+// at 16, and -3.6 at 64 (config D, 8192 tiles) (profiles/r02/s3/
+// sweep_be_map.txt); native doubles gain nothing from it at config C's 2048
+// tiles (sweep_map_fewp.txt) but +0.8 to +1.1 points at config B's 512 (16 x
+// 1M x 8, three processes, profiles/r03/c/sweep_B.txt) and +0.3 at 2 x 4M's 256.
 template <bool BE_IN>
-inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMap; }
+inline int big_map(int64_t tiles) { return tiles <= (BE_IN ? 4096 : 512) ? 2 : kBigMap; }
 // The mid shape (256 lanes, one or two partitions: per-partition flushes, the
 // storage merge of one partition's files) with big-endian input runs 8
 // vectors per lane on hipcc's own schedule (100 VGPRs, no spills): one

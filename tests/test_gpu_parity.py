@@ -407,6 +407,10 @@ def test_full_size_checksums(ipls, golden_meta, cfg):
     torch.cuda.synchronize()
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+    li = agg.last_launch()
+    # the launch the bench measures: big tiles; B's 512 tiles run XCD-chunked (map 2)
+    assert (li["shape"], li["block"], li["vectors"], li["map"]) == \
+        (ipls.SHAPE_BIG, 1024, 16, 2 if cfg == "B" else 0), li
     got = [agg.checksum(p) for p in range(P)]
     assert got == m["sum_checksum"]
     agg.close()

@@ -8,7 +8,9 @@
 #   B PMC:      FETCH_SIZE / WRITE_SIZE passes of config B
 #   rehearsal:  bench.py --multi-rehearsal (the single-handle multi-GPU leg over two shards of GPU 0)
 #   bench:      the default bench line
-# Usage: tools/gpu_ab.sh TAG [steps...]   (steps: pool dsched dpmc bsweep bpmc rehearsal bench; default the first 3)
+#   dprobe:     config D in the default line beside the A/B leg, in one process
+#   tests:      the GPU suite
+# Usage: tools/gpu_ab.sh TAG [steps...]   (steps: pool dsched dpmc bsweep bpmc rehearsal bench dprobe tests; default the first 3)
 set -o pipefail
 TAG=${1:-ab}; shift
 STEPS=${*:-pool dsched dpmc}
@@ -65,6 +67,16 @@ for s in $STEPS; do
       ;;
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 29
+      ;;
+    dprobe)   # config D in the default line vs the A/B leg, same process: with and without the other legs
+      timeout -k 10 400 python bench.py --no-cpu-baseline --no-e2e --no-per-arrival --be-schedule-ab \
+        >> $O/dprobe.jsonl 2>> $O/dprobe.err || exit 30
+      timeout -k 10 500 python bench.py --be-schedule-ab >> $O/dprobe.jsonl 2>> $O/dprobe.err || exit 31
+      ;;
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > $O/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
+      case $rc in 0|1) ;; *) exit 32;; esac
       ;;
   esac
 done
