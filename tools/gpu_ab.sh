@@ -9,6 +9,7 @@
 #   rehearsal:  bench.py --multi-rehearsal (the single-handle multi-GPU leg over two shards of GPU 0)
 #   bench:      the default bench line
 #   dprobe:     config D in the default line beside the A/B leg, in one process
+#   gloo:       bench.py at N = 2 and 4 over gloo, every rank on GPU 0 (rehearsal of the N>1 legs)
 #   tests:      the GPU suite
 # Usage: tools/gpu_ab.sh TAG [steps...]   (steps: pool dsched dpmc bsweep bpmc rehearsal bench dprobe tests; default the first 3)
 set -o pipefail
@@ -72,6 +73,13 @@ for s in $STEPS; do
       timeout -k 10 400 python bench.py --no-cpu-baseline --no-e2e --no-per-arrival --be-schedule-ab \
         >> $O/dprobe.jsonl 2>> $O/dprobe.err || exit 30
       timeout -k 10 500 python bench.py --be-schedule-ab >> $O/dprobe.jsonl 2>> $O/dprobe.err || exit 31
+      ;;
+    gloo)     # the N>1 bench legs over gloo with every rank on the one GPU (a code-path rehearsal)
+      for n in 2 4; do
+        timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+          --master-port $((29500 + n)) bench.py --gpus $n --dist-backend gloo --steps 20 --warmup 5 \
+          > $O/bench_gloo$n.json 2> $O/bench_gloo$n.err || exit 33
+      done
       ;;
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
