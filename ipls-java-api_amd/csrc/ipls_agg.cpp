@@ -450,9 +450,14 @@ void* ipls_agg_stream(ipls_agg* H) { return H ? dev_stream(H->sh[0]) : nullptr; 
 int ipls_agg_sync(ipls_agg* H) {
   KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
-  std::vector<int> all(H->S());
-  for (int s = 0; s < H->S(); ++s) all[s] = s;
-  return par_shards(H, all, [&](int s) { return dev_sync(H->sh[s]); });
+  // start every shard's queued folds first, then wait on the streams one by
+  // one: the waits overlap the GPUs' work anyway (the total is the slowest
+  // shard), and no host thread needs to wake per shard
+  for (int s = 0; s < H->S(); ++s)
+    if (int rc = fwd(H, s, dev_flush(H->sh[s]))) return rc;
+  for (int s = 0; s < H->S(); ++s)
+    if (int rc = fwd(H, s, dev_sync(H->sh[s]))) return rc;
+  return IPLS_OK;
 }
 
 int ipls_agg_flush(ipls_agg* H) {
