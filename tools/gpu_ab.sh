@@ -6,6 +6,7 @@
 #   B sweep:    tools/reduce_sweep.hip over config B's dispatch (lanes x vectors, big vs mid) beside the
 #               streaming-read and dwordx4-copy ceilings, three processes
 #   B PMC:      FETCH_SIZE / WRITE_SIZE passes of config B
+#   fewp:       the same sweep over 1-7 partitions of 4M x 32 (which shape a short batch should get)
 #   rehearsal:  bench.py --multi-rehearsal (the single-handle multi-GPU leg over two shards of GPU 0)
 #   bench:      the default bench line
 #   dprobe:     config D in the default line beside the A/B leg, in one process
@@ -50,6 +51,21 @@ for s in $STEPS; do
       for i in 1 2 3; do
         SWEEP_QUICK=1 SWEEP_B=1 SWEEP_COPY=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 1048576 8 32 50 \
           >> $O/sweep_B.txt 2>&1 || exit 25
+      done
+      ;;
+    fewp)     # few-partition batches (per-partition flushes, short ranges): lanes x vectors per lane, P = 1..7
+      for P in 1 3 5 7 2; do
+        SWEEP_QUICK=1 SWEEP_B=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep $P 4194304 32 32 10 \
+          >> $O/sweep_fewp.txt 2>&1 || exit 34
+      done
+      ;;
+    s512)     # 1024 vs 512 lanes at R = 16 on B, C, F and D (BE in + out), three processes each
+      for i in 1 2 3; do
+        SWEEP_QUICK=1 SWEEP_512=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 4194304 32 32 20 >> $O/sweep_512_C.txt 2>&1 || exit 35
+        SWEEP_QUICK=1 SWEEP_512=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 1048576 8 32 50 >> $O/sweep_512_B.txt 2>&1 || exit 35
+        SWEEP_QUICK=1 SWEEP_512=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep 16 8388608 64 32 10 >> $O/sweep_512_F.txt 2>&1 || exit 35
+        SWEEP_QUICK=1 SWEEP_512=1 SWEEP_BE=1 SWEEP_BE_OUT=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep 64 4194304 32 32 10 \
+          >> $O/sweep_512_D.txt 2>&1 || exit 35
       done
       ;;
     bpmc)

@@ -292,6 +292,19 @@ int main(int argc, char** argv) {
     ADDSB(8, 256, 0);
     ADDSB(4, 256, 0);
   }
+  if (getenv("SWEEP_512")) {   // the big shape at 1024 vs 512 lanes (R = 16; 512 lanes keeps 164 VGPRs, one block per CU)
+    if (be) {
+      ADDSB(16, 1024, 3);
+      ADDSB(16, 512, 3);
+      ADDSB(16, 512, 2);
+      ADDSB(16, 512, 0);
+    } else {
+      ADDSB(16, 1024, 0);
+      ADDSB(16, 512, 0);
+      ADDSB(16, 1024, 0);
+      ADDSB(16, 512, 0);
+    }
+  }
   if (getenv("SWEEP_BS")) {   // block size / fence interval of the big-endian fold
     ADDSB(16, 1024, 2);
     ADDSB(16, 512, 2);
