@@ -417,6 +417,7 @@ int64_t ipls_agg_publish_partials(ipls_agg *h, const int32_t *parts, int n_parts
 #define IPLS_SHAPE_BIG    1
 #define IPLS_SHAPE_MID    2
 #define IPLS_SHAPE_SMALL  3
+#define IPLS_SHAPE_HALF   4  /* 512 lanes x 16 vectors: native doubles, few partitions */
 typedef struct ipls_launch_info {
     int32_t kernel, shape, block, vectors, seqf, map;
     int64_t grid;

@@ -429,16 +429,29 @@ constexpr int big_r() { return START != kAccum ? (BE_IN ? IPLS_BE_BIG_R : 16) : 
 template <bool BE_IN, int START>
 constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? IPLS_BE_SEQF : 0; }
 // Block order of the big shape over whole tiles: partition-major (map 0),
-// except big-endian input on grids of at most 4096 tiles and native doubles
-// on grids of at most 512 (two waves of 256 CUs), which run XCD-chunked
-// (map 2: each XCD walks one contiguous eighth of the work).  With SEQF = 3,
-// map 2 measured +2 to +3.6 points at 2-4 partitions of 4M x 32, +0.2 to +0.6
-// at 16, and -3.6 at 64 (config D, 8192 tiles) (profiles/r02/s3/
-// sweep_be_map.txt); native doubles gain nothing from it at config C's 2048
-// tiles (sweep_map_fewp.txt) but +0.8 to +1.1 points at config B's 512 (16 x
-// 1M x 8, three processes, profiles/r03/c/sweep_B.txt) and +0.3 at 2 x 4M's 256.
+// except big-endian input on grids of at most 4096 tiles, which runs
+// XCD-chunked (map 2: each XCD walks one contiguous eighth of the work).  With
+// SEQF = 3, map 2 measured +2 to +3.6 points at 2-4 partitions of 4M x 32,
+// +0.2 to +0.6 at 16, and -3.6 at 64 (config D, 8192 tiles); native doubles
+// gain nothing from it at 16 (profiles/r02/s3/sweep_be_map.txt,
+// sweep_map_fewp.txt) and run the half shape below on short grids.
 template <bool BE_IN>
-inline int big_map(int64_t tiles) { return tiles <= (BE_IN ? 4096 : 512) ? 2 : kBigMap; }
+inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMap; }
+// The half shape (round 3): native doubles, ZERO/FIRST start, batches of
+// fewer than 4 rounds of big tiles on 256 CUs (fewer than 1024 whole big
+// tiles: one to seven partitions of 4M, config B).  512-lane workgroups at
+// R = 16 -- 128 KiB of a bucket per block, 164 VGPRs, one workgroup per CU,
+// no spills, every load of a peer's chunk in flight.  Same process, same
+// buckets (profiles/r03/e/sweep_fewp.txt, r03/f/sweep_512_*.txt): 1/2/3/5/7
+// partitions of 4M x 32 at 87.1/83.2/89.8/89.5/89.1 % against 56.2/80.5/
+// 74.9/80.7/82.7 % for the big shape (whose 128 tiles per partition leave
+// half a round idle at odd counts) and 87.4/70.1/85.2/78.5/81.0 % for mid;
+// config B 80.2-82.3 % against 78.7-81.8 %.  At config C (2048 big tiles) the
+// big shape stays ahead (87.1-87.8 vs 85.0-87.1 %), at F they tie.
+constexpr int kHalfBS = 512, kHalfR = 16;
+inline bool use_half(int64_t maxL, int n_parts, int64_t big_tile, int64_t half_tpp) {
+  return (maxL / big_tile) * n_parts < 1024 && fill(half_tpp * n_parts);
+}
 // The mid shape (256 lanes, one or two partitions: per-partition flushes, the
 // storage merge of one partition's files) with big-endian input runs 8
 // vectors per lane on hipcc's own schedule (100 VGPRs, no spills): one
@@ -483,6 +496,22 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   const int64_t mid_tile = (int64_t)kMidBS * 2 * RM;
   const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
+  if constexpr (!BE_IN && !FIN && START != kAccum) {
+    const int64_t half_tile = (int64_t)kHalfBS * 2 * kHalfR;
+    const int64_t half_tpp = (maxL + half_tile - 1) / half_tile;
+    if (use_half(maxL, n_parts, big_tile, half_tpp)) {
+      const bool partial = half_tpp > 1 && maxL % half_tile != 0;
+      const dim3 grid((unsigned)(half_tpp * n_parts));
+      if (partial)
+        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kHalfR, true, 3, kHalfBS>), grid, dim3(kHalfBS),
+                           0, st, bufs, parts, k, (int)half_tpp, n_parts);
+      else
+        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kHalfR, true, kBigMap, kHalfBS>), grid,
+                           dim3(kHalfBS), 0, st, bufs, parts, k, (int)half_tpp, n_parts);
+      return launch_info(KER, IPLS_SHAPE_HALF, kHalfBS, kHalfR, 0, partial ? 3 : kBigMap, grid.x, BE_IN, BE_OUT,
+                         START);
+    }
+  }
   if (fill(big_tpp * n_parts)) {
     // partial last tiles are scheduled first (map 3, ipls_kernels.hpp map_block)
     const bool partial = big_tpp > 1 && maxL % big_tile != 0;

@@ -7,7 +7,7 @@ binding plus the Middleware wire codec.
 """
 from ._native import (  # noqa: F401
     ALL_PARTITIONS, DEV_BE, DEV_F64, DEV_TEXT, HOST_BE, HOST_BE_CANON, HOST_F64, HOST_FRAME, HOST_PAIR,
-    HOST_TEXT, KERNEL_FOLD1, KERNEL_REDUCE, KERNEL_REDUCE_SCALAR, KERNEL_ROUND, SHAPE_BIG, SHAPE_MID,
+    HOST_TEXT, KERNEL_FOLD1, KERNEL_REDUCE, KERNEL_REDUCE_SCALAR, KERNEL_ROUND, SHAPE_BIG, SHAPE_HALF, SHAPE_MID,
     SHAPE_SMALL, START_ACCUM, START_FIRST, START_ZERO, TGT_AGG, TGT_FUTURE, TGT_REP, TGT_WADDR, TGT_WEIGHTS,
     IplsError, build_info, lib,
 )

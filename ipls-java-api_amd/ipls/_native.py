@@ -24,7 +24,7 @@ TGT_AGG, TGT_REP, TGT_WEIGHTS, TGT_WADDR, TGT_FUTURE = 0, 1, 2, 3, 4
 HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON, HOST_PAIR = 0, 1, 2, 3, 4, 5, 6
 HOST_TEXT, DEV_TEXT = 7, 8
 KERNEL_REDUCE, KERNEL_ROUND, KERNEL_FOLD1, KERNEL_REDUCE_SCALAR = 1, 2, 3, 4
-SHAPE_BIG, SHAPE_MID, SHAPE_SMALL = 1, 2, 3
+SHAPE_BIG, SHAPE_MID, SHAPE_SMALL, SHAPE_HALF = 1, 2, 3, 4
 ABI_VERSION = 2
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1

@@ -408,9 +408,9 @@ def test_full_size_checksums(ipls, golden_meta, cfg):
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
     li = agg.last_launch()
-    # the launch the bench measures: big tiles; B's 512 tiles run XCD-chunked (map 2)
+    # the launch the bench measures: C's 2048 big tiles; B's 512 run the half shape (512 lanes)
     assert (li["shape"], li["block"], li["vectors"], li["map"]) == \
-        (ipls.SHAPE_BIG, 1024, 16, 2 if cfg == "B" else 0), li
+        ((ipls.SHAPE_HALF, 512, 16, 0) if cfg == "B" else (ipls.SHAPE_BIG, 1024, 16, 0)), li
     got = [agg.checksum(p) for p in range(P)]
     assert got == m["sum_checksum"]
     agg.close()
@@ -1650,27 +1650,35 @@ def production_prefix(ipls, P):
     return steps
 
 
-@pytest.mark.parametrize("seed,P,L", [(21, 4, 4 * 1048576 + 5), (22, 4, 4 * 1048576 + 5), (23, 4, 4 * 1048576 + 5),
+@pytest.mark.parametrize("seed,P,L", [(21, 4, 8 * 1048576 + 5), (22, 4, 8 * 1048576 + 5), (23, 4, 8 * 1048576 + 5),
                                       (22, 1, 4 * 1048576 + 3)])
 def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
-    """The random sequence at config-C bucket lengths (ragged, so every batch
-    ends in a partial tile), so that its batched folds and fused rounds run
-    the production launch shapes -- the big 1024-lane R = 16 / R = 8 tiles
-    and the 256-lane mid shape, native and big-endian, every start mode --
-    interleaved with every other call on the same state.  A scripted prefix
-    (production_prefix) reaches every (shape, byte order, start mode) and the
-    fused round's shapes first, so the coverage does not depend on the seed
-    (seed 21 alone never reached the big shape); the random steps
-    follow.  With one partition only the mid shape exists."""
+    """The random sequence at production bucket lengths (ragged, so every
+    batch ends in a partial tile), so that its batched folds and fused rounds
+    run the production launch shapes interleaved with every other call on the
+    same state: native doubles on the big 1024-lane tiles (4 partitions of 8M:
+    1024 big tiles) and the 512-lane half shape (one partition), big-endian
+    input on the big R = 16 SEQ tiles and the 256-lane mid shape, every start
+    mode.  A scripted prefix (production_prefix) reaches every (shape, byte
+    order, start mode) and the fused round's shapes first, so the coverage
+    does not depend on the seed (seed 21 alone never reached the
+    big shape); the random steps follow.  With one partition of 4M only the
+    half (native) and mid (big-endian) shapes exist.  ACCUM runs R = 8 big
+    tiles for native doubles at every size."""
     shapes = set()
     test_stateful_random_sequence(ipls, O, seed, 32, None, P=P, L=L, steps=300, shapes=shapes,
                                   prefix=production_prefix(ipls, P))
     reduce_shapes = {(s, be, mode) for k, s, _, be, mode in shapes if k == ipls.KERNEL_REDUCE}
-    sizes = (ipls.SHAPE_BIG, ipls.SHAPE_MID) if P == 4 else (ipls.SHAPE_MID,)
-    for shape in sizes:
-        for be in (False, True):
-            for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
-                assert (shape, be, mode) in reduce_shapes, (shape, be, mode, sorted(reduce_shapes))
+    want = []
+    for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
+        want.append((ipls.SHAPE_MID, True, mode))
+        if P == 4:
+            want.append((ipls.SHAPE_BIG, True, mode))
+            want.append((ipls.SHAPE_BIG, False, mode))
+    for mode in (ipls.START_ZERO, ipls.START_FIRST):
+        want.append((ipls.SHAPE_HALF, False, mode))
+    for w in want:
+        assert w in reduce_shapes, (w, sorted(reduce_shapes))
     round_shapes = {s for k, s, _, _, _ in shapes if k == ipls.KERNEL_ROUND}
-    for shape in sizes:
+    for shape in ((ipls.SHAPE_BIG, ipls.SHAPE_MID) if P == 4 else (ipls.SHAPE_MID,)):
         assert shape in round_shapes, (shape, sorted(round_shapes))

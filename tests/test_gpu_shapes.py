@@ -1,8 +1,10 @@
 """GPU parity of the launch shapes the production sizes take.
 
 The fold kernel's dispatch picks a tile shape by how many tiles a batch fills
-(engine.hip launch_reduce_v: big = 1024 lanes x 16 vectors, mid = 256 lanes x
-16 vectors (8 for big-endian input), small = 256 lanes x 8 peers in flight).
+(engine.hip launch_reduce_v: big = 1024 lanes x 16 vectors, half = 512 lanes
+x 16 vectors (native doubles, fewer than 1024 whole big tiles), mid = 256
+lanes x 16 vectors (8 for big-endian input), small = 256 lanes x 8 peers in
+flight).
 Big-endian input at R = 16 runs the hand-fenced SEQ schedule (SEQF = 3),
 START_ACCUM runs R = 8,
 partial last tiles run map 3.  Every case below asserts through
@@ -245,5 +247,40 @@ def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
         w = s + (0.0 + rep[q])                             # AggregatePartition, IPLS.java:1256
         assert_bits_equal(agg.read(q, ipls.TGT_WEIGHTS), w, f"W[{q}]")
         assert_bits_equal(out[q * (L - 1):(q + 1) * (L - 1)], O.c_divide(w), f"avg[{q}]")
+    agg.close()
+    pool.free()
+
+
+@pytest.mark.parametrize("P,L,K", [(1, 4_194_304, 32), (3, 4_194_304, 8), (5, 4_194_304 + 4099, 6),
+                                   (7, 2_097_152 + 5, 4), (16, 1_048_576, 8)])
+def test_native_half_shape(ipls, O, P, L, K):
+    """Round 3's half shape (512 lanes x 16 vectors, native doubles, ZERO and
+    FIRST start, fewer than 1024 whole big tiles): one to seven partitions,
+    whole and partial last tiles (map 3), config B's geometry; into the
+    accumulators, into caller buffers as doubles and as BE bytes (the
+    update_file image); checked bit for bit on the first and last partition
+    and by checksum on every one."""
+    pool = Pool(ipls, P, L, K, False, O.SEED)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    partial = L % (512 * 2 * 16) != 0
+    for start in (ipls.START_ZERO, ipls.START_FIRST):
+        agg.reduce_batch(0, pool.rows, start_mode=start)
+        li = agg.last_launch()
+        assert (li["kernel"], li["shape"], li["block"], li["vectors"], li["seqf"], li["map"]) == \
+            (ipls.KERNEL_REDUCE, ipls.SHAPE_HALF, 512, 16, 0, 3 if partial else 0), li
+        for q in (0, P - 1):
+            ref = ref_sum(O, L, q, K, O.START_ZERO if start == ipls.START_ZERO else O.START_FIRST)
+            assert_bits_equal(agg.read(q), ref, f"start {start} partition {q}")
+        if start == ipls.START_ZERO:
+            assert [agg.checksum(q) for q in range(P)] == [O.c_synth_sum_checksum(L, q, K) for q in range(P)]
+    for be_out in (False, True):
+        agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ZERO, big_endian_out=be_out)
+        li = agg.last_launch()
+        assert (li["shape"], li["be_out"]) == (ipls.SHAPE_HALF, int(be_out)), li
+        agg.sync()
+        assert_bits_equal(pool.out_host(P - 1, L, be_out), ref_sum(O, L, P - 1, K), f"out be={be_out}")
+    # ACCUM keeps the big R = 8 shape
+    agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ACCUM)
+    assert agg.last_launch()["shape"] != ipls.SHAPE_HALF
     agg.close()
     pool.free()
