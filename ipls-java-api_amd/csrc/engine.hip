@@ -448,9 +448,12 @@ inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMa
 // half a round idle at odd counts) and 87.4/70.1/85.2/78.5/81.0 % for mid;
 // config B 80.2-82.3 % against 78.7-81.8 %.  At config C (2048 big tiles) the
 // big shape stays ahead (87.1-87.8 vs 85.0-87.1 %), at F they tie.
+// Both counts are of WHOLE tiles: a partial last tile (map 3) is scheduled
+// first and runs beside the first round, so 4M + 3 doubles is one round of
+// 256 half tiles, not 257.
 constexpr int kHalfBS = 512, kHalfR = 16;
-inline bool use_half(int64_t maxL, int n_parts, int64_t big_tile, int64_t half_tpp) {
-  return (maxL / big_tile) * n_parts < 1024 && fill(half_tpp * n_parts);
+inline bool use_half(int64_t maxL, int n_parts, int64_t big_tile, int64_t half_tile) {
+  return (maxL / big_tile) * n_parts < 1024 && fill((maxL / half_tile) * n_parts);
 }
 // The mid shape (256 lanes, one or two partitions: per-partition flushes, the
 // storage merge of one partition's files) with big-endian input runs 8
@@ -499,7 +502,7 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
   if constexpr (!BE_IN && !FIN && START != kAccum) {
     const int64_t half_tile = (int64_t)kHalfBS * 2 * kHalfR;
     const int64_t half_tpp = (maxL + half_tile - 1) / half_tile;
-    if (use_half(maxL, n_parts, big_tile, half_tpp)) {
+    if (use_half(maxL, n_parts, big_tile, half_tile)) {
       const bool partial = half_tpp > 1 && maxL % half_tile != 0;
       const dim3 grid((unsigned)(half_tpp * n_parts));
       if (partial)

@@ -1657,9 +1657,9 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
     batch ends in a partial tile), so that its batched folds and fused rounds
     run the production launch shapes interleaved with every other call on the
     same state: native doubles on the big 1024-lane tiles (4 partitions of 8M:
-    1024 big tiles) and the 512-lane half shape (one partition), big-endian
-    input on the big R = 16 SEQ tiles and the 256-lane mid shape, every start
-    mode.  A scripted prefix (production_prefix) reaches every (shape, byte
+    1024 big tiles) and the 512-lane half shape (one partition, ZERO/FIRST),
+    big-endian input on the big R = 16 SEQ / R = 8 ACCUM tiles and the 256-lane
+    mid shape, every start mode.  A scripted prefix (production_prefix) reaches every (shape, byte
     order, start mode) and the fused round's shapes first, so the coverage
     does not depend on the seed (seed 21 alone never reached the
     big shape); the random steps follow.  With one partition of 4M only the
@@ -1670,13 +1670,15 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
                                   prefix=production_prefix(ipls, P))
     reduce_shapes = {(s, be, mode) for k, s, _, be, mode in shapes if k == ipls.KERNEL_REDUCE}
     want = []
-    for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
-        want.append((ipls.SHAPE_MID, True, mode))
-        if P == 4:
-            want.append((ipls.SHAPE_BIG, True, mode))
-            want.append((ipls.SHAPE_BIG, False, mode))
     for mode in (ipls.START_ZERO, ipls.START_FIRST):
-        want.append((ipls.SHAPE_HALF, False, mode))
+        want.append((ipls.SHAPE_HALF, False, mode))            # native, one partition
+        want.append((ipls.SHAPE_MID, True, mode))              # big-endian, one partition
+    if P == 4:
+        for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
+            want.append((ipls.SHAPE_BIG, True, mode))          # 4 partitions of 8M
+            want.append((ipls.SHAPE_BIG, False, mode))
+    else:
+        want.append((ipls.SHAPE_MID, True, ipls.START_ACCUM))  # BE ACCUM R = 8: 257 big tiles do not fill
     for w in want:
         assert w in reduce_shapes, (w, sorted(reduce_shapes))
     round_shapes = {s for k, s, _, _, _ in shapes if k == ipls.KERNEL_ROUND}

@@ -68,6 +68,13 @@ for s in $STEPS; do
           >> $O/sweep_512_D.txt 2>&1 || exit 35
       done
       ;;
+    btrace)   # config B under rocprofv3 --kernel-trace --stats: the kernel's own duration
+      cd /tmp
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/trace_B -o run -- \
+        python3 $R/bench.py --config B --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival \
+        > $O/bench_B_trace.json 2> $O/bench_B_trace.err || exit 36
+      cd $R
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \
