@@ -437,17 +437,21 @@ constexpr int big_seqf() { return (BE_IN && big_r<BE_IN, START>() > 8) ? IPLS_BE
 // sweep_map_fewp.txt) and run the half shape below on short grids.
 template <bool BE_IN>
 inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMap; }
-// The half shape (round 3): native doubles, ZERO/FIRST start, batches of
-// fewer than 4 rounds of big tiles on 256 CUs (fewer than 1024 whole big
-// tiles: one to seven partitions of 4M, config B).  512-lane workgroups at
-// R = 16 -- 128 KiB of a bucket per block, 164 VGPRs, one workgroup per CU,
-// no spills, every load of a peer's chunk in flight.  Same process, same
-// buckets (profiles/r03/e/sweep_fewp.txt, r03/f/sweep_512_*.txt): 1/2/3/5/7
+// The half shape (round 3): ZERO/FIRST start, batches of fewer than 4
+// rounds of big tiles on 256 CUs (fewer than 1024 whole big tiles: one to
+// seven partitions of 4M, config B).  512-lane workgroups at R = 16 -- 128
+// KiB of a bucket per block, one workgroup per CU, no spills, every load of a
+// peer's chunk in flight: native doubles at 164 VGPRs, big-endian input on
+// hipcc's own schedule at 172 (the 256-VGPR budget of 512 lanes needs no SEQ
+// fences).  Same process, same buckets (profiles/r03/e/sweep_fewp.txt,
+// r03/f/sweep_512_*.txt, r03/h/sweep_fewp_be.txt): native 1/2/3/5/7
 // partitions of 4M x 32 at 87.1/83.2/89.8/89.5/89.1 % against 56.2/80.5/
 // 74.9/80.7/82.7 % for the big shape (whose 128 tiles per partition leave
 // half a round idle at odd counts) and 87.4/70.1/85.2/78.5/81.0 % for mid;
-// config B 80.2-82.3 % against 78.7-81.8 %.  At config C (2048 big tiles) the
-// big shape stays ahead (87.1-87.8 vs 85.0-87.1 %), at F they tie.
+// big-endian in + out 88.2/87.8/87.0/86.0/85.0 % against 84.3 (mid)/82.7/
+// 84.5 (mid)/79.6/82.9 % for what shipped; config B 80.2-82.3 % against
+// 78.7-81.8 %.  At config C (2048 big tiles) the big shape stays ahead
+// (87.1-87.8 vs 85.0-87.1 %), at F they tie, at D (BE) big SEQF = 3 wins.
 // Both counts are of WHOLE tiles: a partial last tile (map 3) is scheduled
 // first and runs beside the first round, so 4M + 3 doubles is one round of
 // 256 half tiles, not 257.
@@ -499,7 +503,7 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   const int64_t mid_tile = (int64_t)kMidBS * 2 * RM;
   const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
-  if constexpr (!BE_IN && !FIN && START != kAccum) {
+  if constexpr (!FIN && START != kAccum) {
     const int64_t half_tile = (int64_t)kHalfBS * 2 * kHalfR;
     const int64_t half_tpp = (maxL + half_tile - 1) / half_tile;
     if (use_half(maxL, n_parts, big_tile, half_tile)) {

@@ -2,7 +2,7 @@
 
 The fold kernel's dispatch picks a tile shape by how many tiles a batch fills
 (engine.hip launch_reduce_v: big = 1024 lanes x 16 vectors, half = 512 lanes
-x 16 vectors (native doubles, fewer than 1024 whole big tiles), mid = 256
+x 16 vectors (fewer than 1024 whole big tiles, ZERO/FIRST start), mid = 256
 lanes x 16 vectors (8 for big-endian input), small = 256 lanes x 8 peers in
 flight).
 Big-endian input at R = 16 runs the hand-fenced SEQ schedule (SEQF = 3),
@@ -127,9 +127,10 @@ def test_config_d_full_size_be_in_out(ipls, O, golden_meta):
 
 def test_be_big_shape_xcd_order(ipls, O):
     """Big-endian input on a grid of at most 4096 whole tiles runs the big
-    shape XCD-chunked (map 2): 2 x 4M x 32 = 256 tiles, the fold with BE
-    bytes out and the fused round, against the oracle."""
-    P, L, K = 2, 4_194_304, 32
+    shape XCD-chunked (map 2): 8 x 4M x 8 = 1024 tiles (fewer would take the
+    half shape), the fold with BE bytes out and the fused round, against the
+    oracle."""
+    P, L, K = 8, 4_194_304, 8
     pool = Pool(ipls, P, L, K, True, O.SEED)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     refs = [ref_sum(O, L, q, K) for q in range(P)]
@@ -152,8 +153,8 @@ def test_be_big_shape_xcd_order(ipls, O):
 
 @pytest.mark.parametrize("be_out", [True, False])
 def test_be_big_shape_partial_tile(ipls, O, be_out):
-    """>= 512 big tiles with a partial last tile (map 3): 4 x 4,200,001 x 32."""
-    P, L, K = 4, 4_200_001, 32
+    """>= 1024 whole big tiles with a partial last tile (map 3): 8 x 4,200,001 x 8."""
+    P, L, K = 8, 4_200_001, 8
     pool = Pool(ipls, P, L, K, True, O.SEED)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     want = [O.c_synth_sum_checksum(L, q, K) for q in range(P)]
@@ -173,10 +174,11 @@ def test_be_big_shape_partial_tile(ipls, O, be_out):
     pool.free()
 
 
-@pytest.mark.parametrize("P,L", [(1, 4_194_304 + 4099), (2, 2_100_003)])
+@pytest.mark.parametrize("P,L", [(1, 2_100_003), (2, 1_050_003)])
 def test_be_mid_shape(ipls, O, P, L):
-    """One or two partitions: too few big tiles, so the 256-lane mid shape
-    (8 vectors per lane on hipcc's schedule for BE input) with a partial last tile."""
+    """One or two partitions too short for 256 whole half tiles: the 256-lane
+    mid shape (8 vectors per lane on hipcc's schedule for BE input) with a
+    partial last tile."""
     K = 32
     pool = Pool(ipls, P, L, K, True, O.SEED)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
@@ -251,20 +253,21 @@ def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
     pool.free()
 
 
+@pytest.mark.parametrize("be", [False, True])
 @pytest.mark.parametrize("P,L,K", [(1, 4_194_304, 32), (3, 4_194_304, 8), (5, 4_194_304 + 4099, 6),
                                    (7, 2_097_152 + 5, 4), (16, 1_048_576, 8)])
-def test_native_half_shape(ipls, O, P, L, K):
-    """Round 3's half shape (512 lanes x 16 vectors, native doubles, ZERO and
-    FIRST start, fewer than 1024 whole big tiles): one to seven partitions,
-    whole and partial last tiles (map 3), config B's geometry; into the
-    accumulators, into caller buffers as doubles and as BE bytes (the
-    update_file image); checked bit for bit on the first and last partition
-    and by checksum on every one."""
-    pool = Pool(ipls, P, L, K, False, O.SEED)
+def test_half_shape(ipls, O, P, L, K, be):
+    """Round 3's half shape (512 lanes x 16 vectors, ZERO and FIRST start,
+    fewer than 1024 whole big tiles; big-endian input on hipcc's schedule):
+    one to seven partitions, whole and partial last tiles (map 3), config B's
+    geometry; into the accumulators, into caller buffers as doubles and as BE
+    bytes (the update_file image); checked bit for bit on the first and last
+    partition and by checksum on every one."""
+    pool = Pool(ipls, P, L, K, be, O.SEED)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     partial = L % (512 * 2 * 16) != 0
     for start in (ipls.START_ZERO, ipls.START_FIRST):
-        agg.reduce_batch(0, pool.rows, start_mode=start)
+        agg.reduce_batch(0, pool.rows, start_mode=start, big_endian=be)
         li = agg.last_launch()
         assert (li["kernel"], li["shape"], li["block"], li["vectors"], li["seqf"], li["map"]) == \
             (ipls.KERNEL_REDUCE, ipls.SHAPE_HALF, 512, 16, 0, 3 if partial else 0), li
@@ -274,13 +277,14 @@ def test_native_half_shape(ipls, O, P, L, K):
         if start == ipls.START_ZERO:
             assert [agg.checksum(q) for q in range(P)] == [O.c_synth_sum_checksum(L, q, K) for q in range(P)]
     for be_out in (False, True):
-        agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ZERO, big_endian_out=be_out)
+        agg.reduce_batch_out(0, pool.rows, pool.outs, start_mode=ipls.START_ZERO, big_endian_in=be,
+                             big_endian_out=be_out)
         li = agg.last_launch()
-        assert (li["shape"], li["be_out"]) == (ipls.SHAPE_HALF, int(be_out)), li
+        assert (li["shape"], li["be_in"], li["be_out"]) == (ipls.SHAPE_HALF, int(be), int(be_out)), li
         agg.sync()
         assert_bits_equal(pool.out_host(P - 1, L, be_out), ref_sum(O, L, P - 1, K), f"out be={be_out}")
-    # ACCUM keeps the big R = 8 shape
-    agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ACCUM)
+    # ACCUM keeps its R = 8 shapes
+    agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ACCUM, big_endian=be)
     assert agg.last_launch()["shape"] != ipls.SHAPE_HALF
     agg.close()
     pool.free()

@@ -75,6 +75,12 @@ for s in $STEPS; do
         > $O/bench_B_trace.json 2> $O/bench_B_trace.err || exit 36
       cd $R
       ;;
+    fewp_be)  # few-partition big-endian batches (in + out): 1024/512/256 lanes, R = 16 SEQ vs R = 8
+      for P in 1 2 3 5 7; do
+        SWEEP_QUICK=1 SWEEP_512=1 SWEEP_BE=1 SWEEP_BE_OUT=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep $P 4194304 32 32 10 \
+          >> $O/sweep_fewp_be.txt 2>&1 || exit 37
+      done
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \

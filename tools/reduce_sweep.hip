@@ -298,6 +298,9 @@ int main(int argc, char** argv) {
       ADDSB(16, 512, 3);
       ADDSB(16, 512, 2);
       ADDSB(16, 512, 0);
+      ADDSB(8, 256, 0);         // the shipped big-endian mid shape
+      ADDSB(8, 512, 0);
+      ADDSB(8, 1024, 0);
     } else {
       ADDSB(16, 1024, 0);
       ADDSB(16, 512, 0);
