@@ -456,6 +456,11 @@ inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMa
 // first and runs beside the first round, so 4M + 3 doubles is one round of
 // 256 half tiles, not 257.
 constexpr int kHalfBS = 512, kHalfR = 16;
+// IPLS_HALF_ROUND=1 builds the fused round's half shape too (A/B variant,
+// make -C ipls-java-api_amd variants); the shipped fused round keeps big/mid.
+#ifndef IPLS_HALF_ROUND
+#define IPLS_HALF_ROUND 0
+#endif
 inline bool use_half(int64_t maxL, int n_parts, int64_t big_tile, int64_t half_tile) {
   return (maxL / big_tile) * n_parts < 1024 && fill((maxL / half_tile) * n_parts);
 }
@@ -503,18 +508,24 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   const int64_t mid_tile = (int64_t)kMidBS * 2 * RM;
   const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
-  if constexpr (!FIN && START != kAccum) {
+  if constexpr ((!FIN || IPLS_HALF_ROUND) && START != kAccum) {
     const int64_t half_tile = (int64_t)kHalfBS * 2 * kHalfR;
     const int64_t half_tpp = (maxL + half_tile - 1) / half_tile;
     if (use_half(maxL, n_parts, big_tile, half_tile)) {
       const bool partial = half_tpp > 1 && maxL % half_tile != 0;
       const dim3 grid((unsigned)(half_tpp * n_parts));
-      if (partial)
-        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kHalfR, true, 3, kHalfBS>), grid, dim3(kHalfBS),
-                           0, st, bufs, parts, k, (int)half_tpp, n_parts);
-      else
-        hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kHalfR, true, kBigMap, kHalfBS>), grid,
-                           dim3(kHalfBS), 0, st, bufs, parts, k, (int)half_tpp, n_parts);
+#define HALF(MAP)                                                                                         \
+      do {                                                                                                \
+        if constexpr (FIN)                                                                                \
+          hipLaunchKernelGGL((k_round<BE_IN, START, kBigG, kHalfR, MAP, kHalfBS, 0>), grid, dim3(kHalfBS), \
+                             0, st, bufs, parts, k, (int)half_tpp, n_parts, secure, cnts);                \
+        else                                                                                              \
+          hipLaunchKernelGGL((k_reduce<BE_IN, BE_OUT, START, kBigG, kHalfR, true, MAP, kHalfBS>), grid,   \
+                             dim3(kHalfBS), 0, st, bufs, parts, k, (int)half_tpp, n_parts);               \
+      } while (0)
+      if (partial) HALF(3);
+      else HALF(kBigMap);
+#undef HALF
       return launch_info(KER, IPLS_SHAPE_HALF, kHalfBS, kHalfR, 0, partial ? 3 : kBigMap, grid.x, BE_IN, BE_OUT,
                          START);
     }

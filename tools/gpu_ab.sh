@@ -81,6 +81,9 @@ for s in $STEPS; do
           >> $O/sweep_fewp_be.txt 2>&1 || exit 37
       done
       ;;
+    halfround)  # the fused round on few partitions: shipped big/mid vs the half shape (IPLS_HALF_ROUND=1 build)
+      timeout -k 10 300 python tools/half_round_probe.py 5 > $O/half_round_probe.jsonl 2> $O/half_round_probe.err || exit 38
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \
