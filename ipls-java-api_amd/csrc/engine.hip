@@ -456,10 +456,15 @@ inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMa
 // first and runs beside the first round, so 4M + 3 doubles is one round of
 // 256 half tiles, not 257.
 constexpr int kHalfBS = 512, kHalfR = 16;
-// IPLS_HALF_ROUND=1 builds the fused round's half shape too (A/B variant,
-// make -C ipls-java-api_amd variants); the shipped fused round keeps big/mid.
+// The fused round (k_round, 166 VGPRs native / 174 big-endian at 512 lanes,
+// no spills) takes the half shape on the same rule: same process, same
+// buckets against its big/mid shapes (tools/half_round_probe.py,
+// profiles/r03/i/half_round_probe.jsonl): 1/2/3/5 partitions of 4M x 32 at
+// 85.4/81.2/80.8/81.0 % vs 84.5/79.0/78.1/74.2 %, 3 x 4M big-endian 80.2 vs
+// 74.3 %, config B's shape 71.9 vs 72.8 %.  IPLS_HALF_ROUND=0 builds the
+// fused round without it (the A/B variant, make variants).
 #ifndef IPLS_HALF_ROUND
-#define IPLS_HALF_ROUND 0
+#define IPLS_HALF_ROUND 1
 #endif
 inline bool use_half(int64_t maxL, int n_parts, int64_t big_tile, int64_t half_tile) {
   return (maxL / big_tile) * n_parts < 1024 && fill((maxL / half_tile) * n_parts);

@@ -882,8 +882,9 @@ def test_aggregate_round_model_geometry(ipls, O, be, secure):
 
 @pytest.mark.parametrize("shift", [0, 1])
 def test_aggregate_round_big_shape_device_out(ipls, O, shift):
-    """1024-lane shape with a partial tile; averages into a device buffer
-    that is 16-B aligned (shift 0) or 8 mod 16 (shift 1: lane-pair stores)."""
+    """The fused round's half shape (4 x 64 big tiles: 512 lanes) with a
+    partial tile; averages into a device buffer that is 16-B aligned (shift
+    0) or 8 mod 16 (shift 1: lane-pair stores)."""
     P, L, K = 4, 2100001, 3
     arena = torch.empty(P * K * (L + 1), dtype=torch.float64, device="cuda")
     base = int(arena.data_ptr())
@@ -912,15 +913,19 @@ def test_aggregate_round_big_shape_device_out(ipls, O, shift):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("shift,accum,secure", [(0, False, False), (1, True, False), (0, True, True)])
-def test_aggregate_round_whole_tiles(ipls, O, shift, accum, secure):
+@pytest.mark.parametrize("P", [16, 4])
+@pytest.mark.parametrize("shift,accum,secure", [(0, False, False), (1, True, False), (0, True, True),
+                                                (1, False, False)])
+def test_aggregate_round_whole_tiles(ipls, O, shift, accum, secure, P):
     """Partitions of whole 1024-lane tiles (config C's shape class, no
     partial tile anywhere) through the fused round's big shape: every
     partition's W and averages compared in full (odd and even partitions,
     averages buffer 16-B aligned or 8 mod 16, i.e. both store paths of the
     averages-before-W epilogue), with AGG started from a previous arrival
-    (ACCUM) or zero, and the secure divide."""
-    P, L, K = 4, 2097152, 3
+    (ACCUM) or zero, and the secure divide.  16 partitions of 2M run the big
+    shape (1024 big tiles); 4 run the half shape from zero and the big R = 8
+    shape on top of AGG (ACCUM)."""
+    L, K = 2097152, 3
     arena = torch.empty(P * K * (L + 32), dtype=torch.float64, device="cuda")
     base = (int(arena.data_ptr()) + 255) // 256 * 256
     rows = [[ipls.DeviceBuffer(base + 8 * (p * K + k) * (L + 32), L) for k in range(K)] for p in range(P)]
@@ -936,7 +941,8 @@ def test_aggregate_round_whole_tiles(ipls, O, shift, accum, secure):
             agg.Update(first[p], p, from_clients=True)
     agg.aggregate_round(0, rows, out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1)))
     li = agg.last_launch()
-    assert li["kernel"] == ipls.KERNEL_ROUND and li["shape"] == ipls.SHAPE_BIG and li["map"] != 3, li
+    want = ipls.SHAPE_BIG if (P == 16 or accum) else ipls.SHAPE_HALF
+    assert li["kernel"] == ipls.KERNEL_ROUND and li["shape"] == want and li["map"] != 3, li
     torch.cuda.synchronize()
     full = out.cpu().numpy()
     got = full[shift:shift + P * (L - 1)]
@@ -1680,5 +1686,5 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
     for w in want:
         assert w in reduce_shapes, (w, sorted(reduce_shapes))
     round_shapes = {s for k, s, _, _, _ in shapes if k == ipls.KERNEL_ROUND}
-    for shape in ((ipls.SHAPE_BIG, ipls.SHAPE_MID) if P == 4 else (ipls.SHAPE_MID,)):
+    for shape in ((ipls.SHAPE_BIG, ipls.SHAPE_HALF) if P == 4 else (ipls.SHAPE_HALF,)):
         assert shape in round_shapes, (shape, sorted(round_shapes))

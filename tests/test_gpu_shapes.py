@@ -229,10 +229,12 @@ def test_be_fused_round_config_c(ipls, O, golden_meta):
     pool.free()
 
 
-@pytest.mark.parametrize("P,L,K", [(4, 4_200_001, 8), (1, 4_194_304 + 4099, 16)])
-def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
-    """The fused round's big shape with a partial tile, and its mid shape,
-    on BE buckets, on top of a REP accumulator that is not zero."""
+@pytest.mark.parametrize("P,L,K,shape", [(8, 4_200_001, 8, "big"), (1, 4_194_304 + 4099, 16, "half"),
+                                         (1, 2_100_003, 8, "mid")])
+def test_be_fused_round_partial_and_mid(ipls, O, P, L, K, shape):
+    """The fused round's big (SEQF = 3), half (512 lanes, hipcc's schedule)
+    and mid (R = 8) shapes, each with a partial tile, on BE buckets, on top
+    of a REP accumulator that is not zero."""
     pool = Pool(ipls, P, L, K, True, O.SEED, out=False)
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     rep = [O.c_synth_bucket(L, 100 + q, 0) for q in range(P)]
@@ -240,10 +242,10 @@ def test_be_fused_round_partial_and_mid(ipls, O, P, L, K):
         agg.Update(rep[q], q, from_clients=False)          # Replicas_Gradients = +0.0 + R
     out = agg.aggregate_round(0, pool.rows, big_endian=True)
     li = agg.last_launch()
-    big = P > 1
-    assert (li["kernel"], li["vectors"], li["seqf"], li["be_in"]) == \
-        (ipls.KERNEL_ROUND, 16 if big else 8, 3 if big else 0, 1), li
-    assert li["shape"] == (ipls.SHAPE_BIG if big else ipls.SHAPE_MID) and li["map"] == 3, li
+    want = {"big": (ipls.SHAPE_BIG, 1024, 16, 3), "half": (ipls.SHAPE_HALF, 512, 16, 0),
+            "mid": (ipls.SHAPE_MID, 256, 8, 0)}[shape]
+    assert (li["kernel"], li["be_in"], li["map"]) == (ipls.KERNEL_ROUND, 1, 3), li
+    assert (li["shape"], li["block"], li["vectors"], li["seqf"]) == want, li
     for q in range(P):
         s = ref_sum(O, L, q, K)
         w = s + (0.0 + rep[q])                             # AggregatePartition, IPLS.java:1256

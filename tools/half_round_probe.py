@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fused round (ipls_agg_aggregate_round, k_round) on few partitions: the
-shipped library (big/mid shapes) against the IPLS_HALF_ROUND=1 build (the
-512-lane half shape for the fused round too), same process, same buckets,
+fused round on its big/mid shapes (the IPLS_HALF_ROUND=0 build) against the
+512-lane half shape (the shipped library), same process, same buckets,
 interleaved; averages into device memory; bit-identity of W and the
 averages checked between the two.  Algorithmic bytes (K+2)*L*8 per partition
 (K buckets read, W and the averages written).
@@ -19,7 +19,7 @@ from ipls import _native as N  # noqa: E402
 
 
 def run(P, L, K, be, reps):
-    elem = L + 32
+    elem = (L + 1) // 2 * 2 + 32      # every bucket 16-B aligned (the vector path)
     arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
     base = (int(arena.data_ptr()) + 255) // 256 * 256
     rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L, big_endian=be) for k in range(K)] for q in range(P)]
@@ -27,7 +27,7 @@ def run(P, L, K, be, reps):
         for k in range(K):
             ipls.synth_fill(rows[q][k], q, k, ipls.SEED)
     torch.cuda.synchronize()
-    libs = {"shipped": None, "half_round": N.load(N.PKG_ROOT / "lib" / "ab" / "libipls_agg_halfround.so")}
+    libs = {"big_mid_round": N.load(N.PKG_ROOT / "lib" / "ab" / "libipls_agg_nohalfround.so"), "half_round": None}
     aggs = {nm: ipls.Aggregator(n_partitions=P, bucket_len=L, library=lb) for nm, lb in libs.items()}
     outs = {nm: torch.empty(P * (L - 1) + 2, dtype=torch.float64, device="cuda") for nm in libs}
     ms = {nm: [] for nm in libs}
@@ -46,8 +46,8 @@ def run(P, L, K, be, reps):
             agg.sync()
             ms[nm].append(e0.elapsed_time(e1) / 5)
             shape[nm] = agg.last_launch()["shape"]
-    same = bool(torch.equal(outs["shipped"].view(torch.int64), outs["half_round"].view(torch.int64))) and all(
-        np.array_equal(aggs["shipped"].read(q, ipls.TGT_WEIGHTS).view(np.uint64),
+    same = bool(torch.equal(outs["big_mid_round"].view(torch.int64), outs["half_round"].view(torch.int64))) and all(
+        np.array_equal(aggs["big_mid_round"].read(q, ipls.TGT_WEIGHTS).view(np.uint64),
                        aggs["half_round"].read(q, ipls.TGT_WEIGHTS).view(np.uint64)) for q in (0, P - 1))
     nbytes = P * (K + 2) * L * 8
     res = {"P": P, "L": L, "K": K, "be": be, "bit_identical": same}
