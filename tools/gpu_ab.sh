@@ -84,6 +84,18 @@ for s in $STEPS; do
     halfround)  # the fused round on few partitions: shipped big/mid vs the half shape (IPLS_HALF_ROUND=1 build)
       timeout -k 10 300 python tools/half_round_probe.py 5 > $O/half_round_probe.jsonl 2> $O/half_round_probe.err || exit 38
       ;;
+    midp)     # 8-15 partitions of 4M (4-7.5 rounds of big tiles): 1024 vs 512 lanes
+      for P in 9 10 12 13 8; do
+        SWEEP_QUICK=1 SWEEP_512=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep $P 4194304 32 32 10 \
+          >> $O/sweep_midp.txt 2>&1 || exit 39
+      done
+      ;;
+    accum)    # ACCUM start (reads the target): R = 8 x 1024 (shipped) vs R = 16 x 512 / 256 on few and many partitions
+      for P in 1 2 3 5 16; do
+        SWEEP_QUICK=1 SWEEP_ACCUM=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep $P 4194304 32 32 10 \
+          >> $O/sweep_accum.txt 2>&1 || exit 40
+      done
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \
