@@ -96,6 +96,16 @@ for s in $STEPS; do
           >> $O/sweep_accum.txt 2>&1 || exit 40
       done
       ;;
+    accum2)   # ACCUM on many partitions, and big-endian ACCUM
+      for P in 32 64; do
+        SWEEP_QUICK=1 SWEEP_ACCUM=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep $P 4194304 32 32 6 \
+          >> $O/sweep_accum2.txt 2>&1 || exit 41
+      done
+      for P in 1 3 16; do
+        SWEEP_QUICK=1 SWEEP_ACCUM=1 SWEEP_BE=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep $P 4194304 32 32 8 \
+          >> $O/sweep_accum2_be.txt 2>&1 || exit 42
+      done
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \
