@@ -446,64 +446,84 @@ def c_abi_multi_gpu(ipls, torch, devices, P: int, L: int, K: int, reps: int = 5,
             torch.cuda.synchronize(d)
         own = [r[:kh] for r in rows]
 
-        # per owner shard: its stream (HIP events around the combine's launch there)
-        owner_streams = []
-        for o in range(G):
-            d, st = agg.partition_device(o * P)
-            owner_streams.append(torch.cuda.ExternalStream(st, device=torch.device("cuda", d)))
+        links = [len({devices[slot[o * P + q]] for q in range(P)} - {devices[o]}) for o in range(G)]
 
-        def one_round():
-            agg.reduce_batch(0, own, start_mode=ipls.START_ZERO)
-            for p in range(PT):
-                agg.reduce_partial(slot[p], p, [far[p]], start_mode=ipls.START_ZERO)
-            agg.sync()
-            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+        def measure(h, staged: bool) -> dict:
+            # per owner shard: its stream (HIP events around the combine's launch there)
+            owner_streams = []
             for o in range(G):
-                evs[o][0].record(owner_streams[o])
-            t0 = time.perf_counter()
-            n = agg.combine_partials()
-            for o in range(G):
-                evs[o][1].record(owner_streams[o])
-            agg.sync()
-            t1 = time.perf_counter()
-            agg.AggregatePartition(ipls.ALL_PARTITIONS)
-            agg.sync()
-            return t1 - t0, n, [a.elapsed_time(b) for a, b in evs]
-        one_round()
-        ex, per_owner = [], []
-        for _ in range(reps):
-            t, _, ev_ms = one_round()
-            ex.append(t)
-            per_owner.append(ev_ms)
-        tex = float(np.median(ex))
-        moved = PT * L * 8
-        out["combine_ms"] = round(tex * 1e3, 4)
-        out["combine_xgmi_GBps"] = round(moved / tex / 1e9, 1)
+                d, st = h.partition_device(o * P)
+                owner_streams.append(torch.cuda.ExternalStream(st, device=torch.device("cuda", d)))
+
+            def one_round():
+                h.reduce_batch(0, own, start_mode=ipls.START_ZERO)
+                for p in range(PT):
+                    h.reduce_partial(slot[p], p, [far[p]], start_mode=ipls.START_ZERO)
+                h.sync()
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+                for o in range(G):
+                    evs[o][0].record(owner_streams[o])
+                t0 = time.perf_counter()
+                n = h.combine_partials()
+                for o in range(G):
+                    evs[o][1].record(owner_streams[o])
+                h.sync()
+                t1 = time.perf_counter()
+                h.AggregatePartition(ipls.ALL_PARTITIONS)
+                h.sync()
+                return t1 - t0, n, [a.elapsed_time(b) for a, b in evs]
+            one_round()
+            ex, per_owner = [], []
+            for _ in range(reps):
+                t, _, ev_ms = one_round()
+                ex.append(t)
+                per_owner.append(ev_ms)
+            tex = float(np.median(ex))
+            # the combine's roofline: per owner, its P partials arrive
+            # over the xGMI links of the distinct GPUs holding them; algorithmic
+            # bytes = partials * L * 8 over xGMI + L * 8 REP write per partition
+            # (+ L * 8 REP read when REP already held a value -- not in this leg)
+            own_ms = np.median(np.asarray(per_owner), axis=0)
+            xg = P * L * 8
+            fr = [xg / (own_ms[o] / 1e3) / (links[o] * XGMI_LINK_GBS * 1e9) if links[o] else None for o in range(G)]
+            res = {
+                "transfer": ("hipMemcpyPeerAsync of each partial into an owner-side buffer, then the fold "
+                             "(IPLS_PEER_STAGED=1)" if staged else "peer loads in the owner's fold kernel"),
+                "combine_ms": round(tex * 1e3, 4), "combine_xgmi_GBps": round(PT * L * 8 / tex / 1e9, 1),
+                "bytes_formula": "per partition: S*L*8 (S remote partials over xGMI) + L*8 (REP write) [+ L*8 REP read]",
+                "xgmi_bytes_per_owner": xg, "algorithmic_bytes_per_owner": xg + P * L * 8,
+                "owner_kernel_ms": [round(float(x), 4) for x in own_ms], "links_per_owner": links,
+                "xgmi_link_GBps": XGMI_LINK_GBS,
+                "frac_of_xgmi": [None if f is None else round(f, 4) for f in fr],
+                "frac_of_xgmi_min": None if None in fr else round(min(fr), 4),
+                "staged_partials": h.last_launch()["staged"],
+                "status": ("rehearsal: every shard on one GPU, local reads (no xGMI link); unmeasured on hardware"
+                           if len(set(devices)) == 1 else "measured: distinct GPUs over xGMI"),
+                "timing": "HIP events on each owner's stream around the combine (median of the rounds); "
+                          "combine_ms = host wall time of the combine call + sync"}
+            if verify:
+                from oracle import oracle as O   # checker only
+                res["verified_replica_checksum_p0"] = (h.checksum(0, ipls.TGT_WEIGHTS) ==
+                                                       O.c_synth_replica_checksum(L, 0, K, kh))
+            return res
+
+        out["combine"] = measure(agg, False)
+        out["combine_ms"] = out["combine"]["combine_ms"]
+        out["combine_xgmi_GBps"] = out["combine"]["combine_xgmi_GBps"]
+        out["verified_replica_checksum_p0"] = out["combine"].get("verified_replica_checksum_p0")
         out["combine_note"] = (f"{PT} partials of {L * 8 / 2**20:.0f} MiB pulled by their owners "
                                "(peer loads over xGMI; shards on one GPU read local memory), folded into REP in "
                                "slot order; median of the combine step alone")
-        # the combine's roofline: per owner, its P partials arrive
-        # over the xGMI links of the distinct GPUs holding them; algorithmic
-        # bytes = partials * L * 8 over xGMI + L * 8 REP write per partition
-        # (+ L * 8 REP read when REP already held a value -- not in this leg)
-        own_ms = np.median(np.asarray(per_owner), axis=0)
-        links = [len({devices[slot[o * P + q]] for q in range(P)} - {devices[o]}) for o in range(G)]
-        xg = P * L * 8
-        fr = [xg / (own_ms[o] / 1e3) / (links[o] * XGMI_LINK_GBS * 1e9) if links[o] else None for o in range(G)]
-        out["combine"] = {
-            "bytes_formula": "per partition: S*L*8 (S remote partials over xGMI) + L*8 (REP write) [+ L*8 REP read]",
-            "xgmi_bytes_per_owner": xg, "algorithmic_bytes_per_owner": xg + P * L * 8,
-            "owner_kernel_ms": [round(float(x), 4) for x in own_ms], "links_per_owner": links,
-            "xgmi_link_GBps": XGMI_LINK_GBS,
-            "frac_of_xgmi": [None if f is None else round(f, 4) for f in fr],
-            "frac_of_xgmi_min": None if None in fr else round(min(fr), 4),
-            "status": ("rehearsal: every shard on one GPU, local reads (no xGMI link); unmeasured on hardware"
-                       if len(set(devices)) == 1 else "measured: distinct GPUs, peer loads over xGMI"),
-            "timing": "HIP events on each owner's stream around the combine launch, median of the rounds"}
-        if verify:
-            from oracle import oracle as O   # checker only
-            out["verified_replica_checksum_p0"] = (agg.checksum(0, ipls.TGT_WEIGHTS) ==
-                                                   O.c_synth_replica_checksum(L, 0, K, kh))
+        # the other transfer: each partial copied to its owner first (the
+        # no-peer-access fallback, forced), then the same fold -- copy engines
+        # instead of the owner's CUs pulling over xGMI
+        agg.close()
+        os.environ["IPLS_PEER_STAGED"] = "1"
+        try:
+            agg = ipls.Aggregator(n_partitions=PT, bucket_len=L, devices=list(devices))
+        finally:
+            del os.environ["IPLS_PEER_STAGED"]
+        out["combine_staged"] = measure(agg, True)
     agg.close()
     del pools, rows
     torch.cuda.empty_cache()

@@ -439,7 +439,8 @@ template <bool BE_IN>
 inline int big_map(int64_t tiles) { return (BE_IN && tiles <= 4096) ? 2 : kBigMap; }
 // The half shape (round 3): ZERO/FIRST start, batches of fewer than 4
 // rounds of big tiles on 256 CUs (fewer than 1024 whole big tiles: one to
-// seven partitions of 4M, config B).  512-lane workgroups at R = 16 -- 128
+// seven partitions of 4M, config B), and larger grids that the big tiles
+// would leave partly idle in their last round (below).  512-lane workgroups at R = 16 -- 128
 // KiB of a bucket per block, one workgroup per CU, no spills, every load of a
 // peer's chunk in flight: native doubles at 164 VGPRs, big-endian input on
 // hipcc's own schedule at 172 (the 256-VGPR budget of 512 lanes needs no SEQ
@@ -466,8 +467,31 @@ constexpr int kHalfBS = 512, kHalfR = 16;
 #ifndef IPLS_HALF_ROUND
 #define IPLS_HALF_ROUND 1
 #endif
-inline bool use_half(int64_t maxL, int n_parts, int64_t big_tile, int64_t half_tile) {
-  return (maxL / big_tile) * n_parts < 1024 && fill((maxL / half_tile) * n_parts);
+// ACCUM (the fold reads its target too) on fewer than 1024 big R = 16
+// tiles: the half shape at R = 16 (202 VGPRs native, 204 big-endian, no
+// spills) instead of the big R = 8 tiles of the same size.  Same process
+// (profiles/r03/k/sweep_accum.txt, r03/l/sweep_accum2*.txt): 1/2/3/5
+// partitions of 4M x 32 at 83.9/82.7/85.3/84.9 % vs 81.0/80.9/82.3/82.5 %,
+// big-endian 1/3 at 81.8/82.9 vs 79.2/81.4 %; at 16/32/64 partitions the two
+// tie (82.3/79.9/81.6 vs 81.8/80.2/81.2 %), which the big R = 8 tiles keep.
+// The fused round's ACCUM start (AGG already holds arrivals) keeps big/mid.
+#ifndef IPLS_HALF_ACCUM
+#define IPLS_HALF_ACCUM 1
+#endif
+// Past 4 rounds the half shape also takes grids whose big tiles leave part
+// of the last round idle while its own tiles do not (with L = 4M: 9, 11, 13,
+// 15 partitions; profiles/r03/k/sweep_midp.txt: 9 x 4M 87.3-87.5 vs 82.8-83.0 %,
+// 13 x 4M 84.3-84.4 vs 83.4-83.5 %), and leaves whole rounds to the big shape
+// (8, 10, 12 x 4M: big ahead by 0-0.8 points).
+inline double round_eff(int64_t tiles) {   // busy fraction of the rounds of 256 one-workgroup CUs
+  const int64_t r = (tiles + 255) / 256;
+  return r > 0 ? (double)tiles / (double)(r * 256) : 0.0;
+}
+// The big tiles counted are the R = 16 ones (32768 doubles) for every start
+// mode: ACCUM's big shape runs R = 8 tiles the size of a half tile.
+inline bool use_half(int64_t maxL, int n_parts, int64_t half_tile) {
+  const int64_t tb = (maxL / ((int64_t)kBigBS * 2 * 16)) * n_parts, th = (maxL / half_tile) * n_parts;
+  return fill(th) && (tb < 1024 || round_eff(th) > round_eff(tb) + 0.06);
 }
 // The mid shape (256 lanes, one or two partitions: per-partition flushes, the
 // storage merge of one partition's files) with big-endian input runs 8
@@ -513,10 +537,10 @@ ipls_launch_info launch_reduce_v(int64_t maxL, int n_parts, hipStream_t st, cons
   const int64_t big_tpp = (maxL + big_tile - 1) / big_tile;
   const int64_t mid_tile = (int64_t)kMidBS * 2 * RM;
   const int64_t mid_tpp = (maxL + mid_tile - 1) / mid_tile;
-  if constexpr ((!FIN || IPLS_HALF_ROUND) && START != kAccum) {
+  if constexpr ((!FIN || IPLS_HALF_ROUND) && (START != kAccum || (IPLS_HALF_ACCUM && !FIN))) {
     const int64_t half_tile = (int64_t)kHalfBS * 2 * kHalfR;
     const int64_t half_tpp = (maxL + half_tile - 1) / half_tile;
-    if (use_half(maxL, n_parts, big_tile, half_tile)) {
+    if (use_half(maxL, n_parts, half_tile)) {
       const bool partial = half_tpp > 1 && maxL % half_tile != 0;
       const dim3 grid((unsigned)(half_tpp * n_parts));
 #define HALF(MAP)                                                                                         \

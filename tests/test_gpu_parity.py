@@ -1664,11 +1664,11 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
     run the production launch shapes interleaved with every other call on the
     same state: the big 1024-lane tiles (4 partitions of 8M: 1024 big tiles;
     big-endian input on the R = 16 SEQ schedule, ACCUM at R = 8) and the
-    512-lane half shape (one partition, ZERO/FIRST), every start mode.  A scripted prefix (production_prefix) reaches every (shape, byte
+    512-lane half shape (one partition), every start mode.  A scripted prefix (production_prefix) reaches every (shape, byte
     order, start mode) and the fused round's shapes first, so the coverage
     does not depend on the seed (seed 21 alone never reached the
     big shape); the random steps follow.  With one partition of 4M only the
-    half shape and, for big-endian ACCUM, the mid shape exist."""
+    half shape exists."""
     shapes = set()
     test_stateful_random_sequence(ipls, O, seed, 32, None, P=P, L=L, steps=300, shapes=shapes,
                                   prefix=production_prefix(ipls, P))
@@ -1681,8 +1681,8 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
         for mode in (ipls.START_ZERO, ipls.START_FIRST, ipls.START_ACCUM):
             want.append((ipls.SHAPE_BIG, True, mode))          # 4 partitions of 8M
             want.append((ipls.SHAPE_BIG, False, mode))
-    else:
-        want.append((ipls.SHAPE_MID, True, ipls.START_ACCUM))  # BE ACCUM R = 8: 257 big tiles do not fill
+    for be in (False, True):
+        want.append((ipls.SHAPE_HALF, be, ipls.START_ACCUM))   # one partition, ACCUM at R = 16
     for w in want:
         assert w in reduce_shapes, (w, sorted(reduce_shapes))
     round_shapes = {s for k, s, _, _, _ in shapes if k == ipls.KERNEL_ROUND}

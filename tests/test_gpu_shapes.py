@@ -259,8 +259,8 @@ def test_be_fused_round_partial_and_mid(ipls, O, P, L, K, shape):
 @pytest.mark.parametrize("P,L,K", [(1, 4_194_304, 32), (3, 4_194_304, 8), (5, 4_194_304 + 4099, 6),
                                    (7, 2_097_152 + 5, 4), (16, 1_048_576, 8)])
 def test_half_shape(ipls, O, P, L, K, be):
-    """Round 3's half shape (512 lanes x 16 vectors, ZERO and FIRST start,
-    fewer than 1024 whole big tiles; big-endian input on hipcc's schedule):
+    """Round 3's half shape (512 lanes x 16 vectors, ZERO / FIRST / ACCUM
+    start, fewer than 1024 whole big tiles; big-endian input on hipcc's schedule):
     one to seven partitions, whole and partial last tiles (map 3), config B's
     geometry; into the accumulators, into caller buffers as doubles and as BE
     bytes (the update_file image); checked bit for bit on the first and last
@@ -285,8 +285,14 @@ def test_half_shape(ipls, O, P, L, K, be):
         assert (li["shape"], li["be_in"], li["be_out"]) == (ipls.SHAPE_HALF, int(be), int(be_out)), li
         agg.sync()
         assert_bits_equal(pool.out_host(P - 1, L, be_out), ref_sum(O, L, P - 1, K), f"out be={be_out}")
-    # ACCUM keeps its R = 8 shapes
+    # ACCUM on top of the last fold: the half shape at R = 16 as well
+    agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ZERO, big_endian=be)
     agg.reduce_batch(0, pool.rows, start_mode=ipls.START_ACCUM, big_endian=be)
-    assert agg.last_launch()["shape"] != ipls.SHAPE_HALF
+    li = agg.last_launch()
+    assert (li["shape"], li["block"], li["vectors"], li["start"]) == \
+        (ipls.SHAPE_HALF, 512, 16, ipls.START_ACCUM), li
+    for q in (0, P - 1):
+        s = ref_sum(O, L, q, K)
+        assert_bits_equal(agg.read(q), ref_sum(O, L, q, K, O.START_ACCUM, s), f"accum partition {q}")
     agg.close()
     pool.free()
