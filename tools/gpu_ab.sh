@@ -135,6 +135,15 @@ for s in $STEPS; do
           > $O/bench_gloo$n.json 2> $O/bench_gloo$n.err || exit 33
       done
       ;;
+    gloo8)    # the N = 8 bench over gloo with every rank on GPU 0 (rehearsal of the 8-GPU code path and memory)
+      timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29508 bench.py --gpus 8 --dist-backend gloo --steps 10 --warmup 2 \
+        > $O/bench_gloo8.json 2> $O/bench_gloo8.err || exit 43
+      ;;
+    soak)     # random call sequences: 40 seeds at production bucket lengths, 400 short ones
+      timeout -k 10 900 python -u tools/fuzz_stateful.py 3000 40 big > $O/fuzz_stateful_big_40.txt 2>&1 || exit 44
+      timeout -k 10 600 python -u tools/fuzz_stateful.py 4000 400 > $O/fuzz_stateful_400.txt 2>&1 || exit 45
+      ;;
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
         > $O/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
