@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <functional>
 #include <map>
 #include <memory>
@@ -241,13 +242,19 @@ int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
   std::mutex m;
   std::condition_variable cv;
   size_t left = ss.size() - 1;
-  for (size_t i = 1; i < ss.size(); ++i)
-    H->pool->post(ss[i], [&, i] {
+  for (size_t i = 1; i < ss.size(); ++i) {
+    auto task = [&, i] {
       rc[i] = fn(ss[i]);
       if (rc[i] < 0) msg[i] = dev_last_error(nullptr);
       std::lock_guard<std::mutex> lk(m);
       if (--left == 0) cv.notify_one();
-    });
+    };
+    try {
+      H->pool->post(ss[i], task);
+    } catch (...) {   // could not queue it (allocation): run that shard's part here
+      task();
+    }
+  }
   rc[0] = fn(ss[0]);
   if (rc[0] < 0) msg[0] = dev_last_error(nullptr);
   {
@@ -407,7 +414,14 @@ int ipls_agg_open(const ipls_agg_cfg* cfg, ipls_agg** out) {
   const char* st = std::getenv("IPLS_PEER_STAGED");
   H->force_staged = st && st[0] == '1';
   H->gstage.assign(S, nullptr);
-  if (S > 1) H->pool = std::make_unique<ShardPool>(S);
+  if (S > 1) {
+    try {
+      H->pool = std::make_unique<ShardPool>(S);
+    } catch (const std::exception& e) {   // thread creation failed: no exception crosses the C-ABI
+      destroy(H);
+      return ferr(nullptr, IPLS_E_NOMEM, "shard worker threads: %s", e.what());
+    }
+  }
   *out = H;
   return IPLS_OK;
 }
