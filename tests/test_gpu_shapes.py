@@ -296,3 +296,40 @@ def test_half_shape(ipls, O, P, L, K, be):
         assert_bits_equal(agg.read(q), ref_sum(O, L, q, K, O.START_ACCUM, s), f"accum partition {q}")
     agg.close()
     pool.free()
+
+
+@pytest.mark.parametrize("start", ["ZERO", "ACCUM"])
+def test_half_shape_ragged_model_geometry(ipls, O, start):
+    """The half shape over a model geometry whose partitions differ in length
+    (IPLS.java:1019-1028: chunk = ceil(M / P), the last partition short):
+    partitions 0-1 are 256 whole half tiles (map 0, no partial tile in the
+    grid's plan) and the last stops 2 doubles short, so its last tile is
+    partial inside a whole-tile grid; every partition compared in full with
+    the oracle, ZERO start and ACCUM on top of an arrival."""
+    M, P, K = 3 * 4_194_303 - 2, 3, 5
+    agg = ipls.Aggregator(M, P, max_peers=K)
+    Ls = agg.lengths
+    assert Ls[-1] < Ls[0]
+    t = torch.empty(P * K * (max(Ls) + 32), dtype=torch.float64, device="cuda")
+    base = (int(t.data_ptr()) + 255) // 256 * 256
+    stride = (max(Ls) + 31) // 32 * 32
+    rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * stride, Ls[q]) for k in range(K)] for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[q][k], q, k, O.SEED)
+    torch.cuda.synchronize()
+    first = [O.synth_bucket(Ls[q], q, 40) for q in range(P)]
+    if start == "ACCUM":
+        for q in range(P):
+            agg.Update(first[q], q)
+    agg.reduce_batch(0, rows, start_mode=ipls.START_ACCUM if start == "ACCUM" else ipls.START_ZERO)
+    li = agg.last_launch()
+    assert (li["shape"], li["block"], li["vectors"], li["map"]) == (ipls.SHAPE_HALF, 512, 16, 0), li
+    assert Ls == [4_194_304, 4_194_304, 4_194_302], Ls
+    for q in range(P):
+        bk = [O.c_synth_bucket(Ls[q], q, k) for k in range(K)]
+        ref = O.c_reduce(bk, Ls[q], O.START_ACCUM, 0.0 + first[q]) if start == "ACCUM" else O.c_reduce(bk, Ls[q])
+        assert_bits_equal(agg.read(q), ref, f"partition {q} (L={Ls[q]})")
+    agg.close()
+    del t
+    torch.cuda.empty_cache()
