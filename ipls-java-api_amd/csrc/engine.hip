@@ -489,9 +489,13 @@ inline double round_eff(int64_t tiles) {   // busy fraction of the rounds of 256
 }
 // The big tiles counted are the R = 16 ones (32768 doubles) for every start
 // mode: ACCUM's big shape runs R = 8 tiles the size of a half tile.
+// IPLS_HALF_ALWAYS=1 (A/B builds only) sends every grid that fills to it.
+#ifndef IPLS_HALF_ALWAYS
+#define IPLS_HALF_ALWAYS 0
+#endif
 inline bool use_half(int64_t maxL, int n_parts, int64_t half_tile) {
   const int64_t tb = (maxL / ((int64_t)kBigBS * 2 * 16)) * n_parts, th = (maxL / half_tile) * n_parts;
-  return fill(th) && (tb < 1024 || round_eff(th) > round_eff(tb) + 0.06);
+  return fill(th) && (IPLS_HALF_ALWAYS || tb < 1024 || round_eff(th) > round_eff(tb) + 0.06);
 }
 // The mid shape (256 lanes, one or two partitions: per-partition flushes, the
 // storage merge of one partition's files) with big-endian input runs 8

@@ -135,6 +135,11 @@ for s in $STEPS; do
           > $O/bench_gloo$n.json 2> $O/bench_gloo$n.err || exit 33
       done
       ;;
+    halfalways)  # the big shape's remaining grids (C fold / round / ACCUM, F fold) vs the half shape, 3 processes
+      for i in 1 2 3; do
+        timeout -k 10 300 python tools/half_always_probe.py 4 >> $O/half_always_probe.jsonl 2>> $O/half_always_probe.err || exit 46
+      done
+      ;;
     gloo8)    # the N = 8 bench over gloo with every rank on GPU 0 (rehearsal of the 8-GPU code path and memory)
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29508 bench.py --gpus 8 --dist-backend gloo --steps 10 --warmup 2 \
