@@ -531,7 +531,7 @@ def c_abi_multi_gpu(ipls, torch, devices, P: int, L: int, K: int, reps: int = 5,
 
 
 def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, verify: bool = True,
-               rounds: int = 4) -> dict:
+               rounds: int = 4, build: dict | None = None) -> dict:
     """One more BASELINE config on the same box, N=1: B
     (16 x 1M x 8, native doubles) or D (64 x 4M x 32) with big-endian IPFS
     bytes in and the sum packed to big-endian bytes out, i.e. config D's
@@ -580,12 +580,15 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
     agg.close()
     del arena, out_arena, rows
     torch.cuda.empty_cache()
+    # HBM bytes per launch from the committed PMC passes of this config, for this build only
+    traffic, traffic_prov = pmc_traffic(f"{name}{'-be' if be else ''}", build or {})
     return {"workload": f"{name}: {P} partitions x {L} doubles x {K} peers"
                         + (" (BE IPFS bytes in, BE sum bytes out: fused unpack/pack)" if be else ""),
             "kernel_ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
             "frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": nbytes,
             "round_ms": [round(x, 4) for x in per_round],
             "launch": {k: launch[k] for k in ("shape", "block", "vectors", "seqf", "map", "grid")},
+            "traffic": traffic, "traffic_provenance": traffic_prov,
             "verified_checksum_p0": verified}
 
 
@@ -1280,7 +1283,7 @@ def main():
             torch.cuda.empty_cache()
             # B's launch is 0.19 ms: 50 launches (10 ms) per round average out the ramp of the first ones
             out["other_configs"] = {nm: side(config_leg, ipls, torch, nm, be, local, steps=st,
-                                             verify=not args.no_verify)
+                                             verify=not args.no_verify, build=build)
                                     for nm, be, st in (("B", False, 50), ("D", True, 5), ("F", False, 5))}
             out["other_configs"]["A"] = side(config_a_leg, ipls)
             if isinstance(out["other_configs"]["F"], dict) and not args.no_e2e:
