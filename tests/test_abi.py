@@ -48,6 +48,11 @@ def test_header_constants_match_binding():
     assert ctypes.sizeof(N.LaunchInfo) == 48
     assert defs["IPLS_HOST_TEXT"] == N.HOST_TEXT and defs["IPLS_DEV_TEXT"] == N.DEV_TEXT
     assert defs["IPLS_SHAPE_BIG"] == N.SHAPE_BIG and defs["IPLS_KERNEL_ROUND"] == N.KERNEL_ROUND
+    for nm in ("SHAPE_MID", "SHAPE_SMALL", "SHAPE_HALF", "KERNEL_REDUCE", "KERNEL_FOLD1", "KERNEL_REDUCE_SCALAR"):
+        assert defs["IPLS_" + nm] == getattr(N, nm), nm
+    # ipls_launch_info: the last int32 is `staged` (was `reserved`), layout unchanged
+    assert [f for f, _ in N.LaunchInfo._fields_][-1] == "staged"
+    assert re.search(r"int32_t\s+staged;", text)
 
 
 def test_library_is_gfx950_code_object():
