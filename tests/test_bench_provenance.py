@@ -1,0 +1,92 @@
+"""Provenance of the bench numbers, on the CPU: the build
+record of the library (ipls.build_info, tools/build_stamp.py), the rule by
+which bench.py reports roofline.traffic only for the build the PMC passes
+were taken on, and tools/pmc_traffic.py reading the profiled process's build
+from its bench line.  Also the publish wrappers' capacity checks,
+which run before any library call."""
+import hashlib
+import json
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def test_build_info_hashes_the_loaded_library():
+    import ipls
+    from ipls import _native as N
+    info = ipls.build_info()
+    assert info["so_sha256"] == hashlib.sha256(N.LIB_PATH.read_bytes()).hexdigest()
+    stamp = N.LIB_PATH.with_name(N.LIB_PATH.name + ".buildinfo.json")
+    if stamp.exists():                      # written by every `make` of the library
+        rec = json.loads(stamp.read_text())
+        assert info["stamp_matches_so"] == (rec["so_sha256"] == info["so_sha256"])
+        assert info["kernel_src_sha256"] == rec["kernel_src_sha256"]
+
+
+def test_build_stamp_records_kernel_source_hash(tmp_path):
+    sys.path.insert(0, str(ROOT / "tools"))
+    import build_stamp
+    lib = tmp_path / "libx.so"
+    lib.write_bytes(b"not really a library")
+    subprocess.run([sys.executable, str(ROOT / "tools" / "build_stamp.py"), str(lib)], check=True,
+                   capture_output=True)
+    rec = json.loads((tmp_path / "libx.so.buildinfo.json").read_text())
+    assert rec["so_sha256"] == hashlib.sha256(b"not really a library").hexdigest()
+    assert rec["kernel_src_sha256"] == build_stamp.kernel_src_sha256()
+    assert rec["so"] == "libx.so"
+
+
+@pytest.fixture
+def bench(tmp_path, monkeypatch):
+    sys.path.insert(0, str(ROOT))
+    import bench as b
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"hbm_bytes_per_launch": 123, "build": {"so_sha256": "aa", "kernel_src_sha256": "kk", "git_rev": "r"},
+             "source": "profiles/rXX"}
+    (prof / "pmc_traffic.json").write_text(json.dumps({"C": entry, "old": {"hbm_bytes_per_launch": 7}}))
+    monkeypatch.setattr(b, "ROOT", tmp_path)
+    return b
+
+
+def test_traffic_reported_only_for_the_profiled_build(bench):
+    t, p = bench.pmc_traffic("C", {"so_sha256": "aa", "kernel_src_sha256": "zz"})
+    assert t == 123 and p["match"] == "so_sha256" and p["traffic_stale"] is False
+    t, p = bench.pmc_traffic("C", {"so_sha256": "bb", "kernel_src_sha256": "kk"})
+    assert t == 123 and p["match"] == "kernel_src_sha256"          # relinked, same kernels
+    t, p = bench.pmc_traffic("C", {"so_sha256": "bb", "kernel_src_sha256": "zz"})
+    assert t is None and p["traffic_stale"] is True and p["entry_so_sha256"] == "aa"
+    t, p = bench.pmc_traffic("old", {"so_sha256": "aa"})            # an entry without a build record
+    assert t is None and p["traffic_stale"] is True
+    t, p = bench.pmc_traffic("D-be", {"so_sha256": "aa"})
+    assert t is None and "no PMC entry" in p["why"]
+
+
+def test_pmc_tool_reads_the_build_from_the_bench_line(tmp_path):
+    sys.path.insert(0, str(ROOT / "tools"))
+    import pmc_traffic
+    log = tmp_path / "pmc_fetch.log"
+    line = {"metric": "x", "build": {"so_sha256": "aa", "kernel_src_sha256": "kk"}}
+    log.write_text("rocprofv3 chatter\n" + json.dumps(line) + "\nmore chatter\n")
+    assert pmc_traffic.build_of(log) == line["build"]
+    bad = tmp_path / "bad.log"
+    bad.write_text("no json here\n")
+    with pytest.raises(SystemExit):
+        pmc_traffic.build_of(bad)
+
+
+def test_device_text_capacity_checks():
+    import ipls
+    out = ipls.Aggregator._device_text_out
+    assert out(ipls.DeviceBuffer(4096, 100), None, 800) == (4096, 800)       # capacity = 8 * n
+    assert out(ipls.DeviceBuffer(4096, 100), 600, 600) == (4096, 600)       # a smaller explicit cap wins
+    with pytest.raises(ValueError):
+        out(ipls.DeviceBuffer(4096, 99), None, 800)                         # 792 B < 800 needed
+    with pytest.raises(ValueError):
+        out(4096, None, 10)                                                 # raw address without a capacity
+    with pytest.raises(ValueError):
+        out(4096, 9, 10)
+    assert out(4096, 10, 10) == (4096, 10)
