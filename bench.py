@@ -650,6 +650,50 @@ def be_schedule_ab(ipls, torch, device: int, rounds: int = 4, steps: int = 5, ve
             "algorithmic_bytes_per_launch": nbytes, "variants": res}
 
 
+def few_partitions_leg(ipls, torch, device: int, P: int = 3, L: int = 4194304, K: int = 32, steps: int = 10,
+                       verify: bool = True) -> dict:
+    """A shard's share when -pa is small (-pa 24 over 8 GPUs: 3 partitions of
+    4M per GPU), N=1, never the value: the fold and the fused round on 3 x 4M
+    x 32, which run the 512-lane half shape; HIP events over
+    back-to-back launches, partition 0 checked against the oracle."""
+    elem = L + 32
+    arena = torch.empty(P * K * elem + 32, dtype=torch.float64, device="cuda")
+    base = (int(arena.data_ptr()) + 255) // 256 * 256
+    rows = [[ipls.DeviceBuffer(base + 8 * (q * K + k) * elem, L) for k in range(K)] for q in range(P)]
+    for q in range(P):
+        for k in range(K):
+            ipls.synth_fill(rows[q][k], q, k, ipls.SEED)
+    avg = torch.empty(P * (L - 1) + 2, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=device)
+    stream = torch.cuda.ExternalStream(agg.stream, device=torch.device("cuda", device))
+    out = {"workload": f"{P} partitions x {L} doubles x {K} peers (a GPU's share of -pa {8 * P} over 8 GPUs)"}
+    for name, fn, nbytes in (
+            ("fold", lambda: agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO), P * (K + 1) * L * 8),
+            ("fused_round", lambda: agg.aggregate_round(0, rows, out=ipls.DeviceBuffer.from_tensor(avg)),
+             P * (K + 2) * L * 8)):
+        fn()
+        agg.sync()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            fn()
+        e1.record(stream)
+        agg.sync()
+        ms = e0.elapsed_time(e1) / steps
+        li = agg.last_launch()
+        out[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
+                     "frac": round(nbytes / ms / 1e6 / HBM_PEAK_GBS, 4),
+                     "launch": {k: li[k] for k in ("shape", "block", "vectors", "map", "grid")}}
+    if verify:
+        from oracle import oracle as O   # checker only
+        out["verified_checksum_p0"] = agg.checksum(0, ipls.TGT_WEIGHTS) == O.c_synth_sum_checksum(L, 0, K)
+    agg.close()
+    del arena, avg, rows
+    torch.cuda.empty_cache()
+    return out
+
+
 def config_a_leg(ipls, reps: int = 20) -> dict:
     """BASELINE configs[0], the reference's own CPU-runnable case: ETHModel
     (M = 443,610, tests/golden/ethmodel.f64be.gz), -pa 3 -n 3, three peers.
@@ -1286,6 +1330,7 @@ def main():
                                              verify=not args.no_verify, build=build)
                                     for nm, be, st in (("B", False, 50), ("D", True, 5), ("F", False, 5))}
             out["other_configs"]["A"] = side(config_a_leg, ipls)
+            out["few_partitions"] = side(few_partitions_leg, ipls, torch, local, verify=not args.no_verify)
             if isinstance(out["other_configs"]["F"], dict) and not args.no_e2e:
                 # config F is the end-to-end case: its buckets start as host IPFS bytes
                 _, LF, KF = CONFIGS["F"]
