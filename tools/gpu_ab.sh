@@ -106,6 +106,16 @@ for s in $STEPS; do
           >> $O/sweep_accum2_be.txt 2>&1 || exit 42
       done
       ;;
+    fpmc)     # config F (16 x 8M x 64, one GPU's slice) PMC passes
+      cd /tmp
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_F -o run -- \
+        python3 $R/bench.py --config F --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
+        --steps 3 --warmup 1 > $O/pmc_fetch_F.log 2>&1 || exit 47
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $O/pmc_write_F -o run -- \
+        python3 $R/bench.py --config F --no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival --no-verify \
+        --steps 3 --warmup 1 > $O/pmc_write_F.log 2>&1 || exit 48
+      cd $R
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \
