@@ -19,6 +19,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef IPLS_ROT
+#define IPLS_ROT 0
+#endif
+
 namespace ipls {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -199,8 +203,17 @@ __device__ __forceinline__ void reduce_tiles(
     // the DRAM pattern that measured best -- forcing all R loads in flight
     // with scheduling barriers was slower.)
     int64_t off[R];
+    // IPLS_ROT=1 (A/B builds only): tile t visits its R sub-windows starting
+    // at sub-window t mod R, so neighbouring tiles in flight at the same loop
+    // step touch different offsets of their chunks (accumulator r always
+    // pairs with the same sub-window, so every element's fold is unchanged)
+#if IPLS_ROT
+    const int rot = t & (R - 1);
+#else
+    constexpr int rot = 0;
+#endif
 #pragma unroll
-    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * kBlock + tid);
+    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)((r + rot) & (R - 1)) * kBlock + tid);
 
     // SEQ: one peer per step, each of its R vectors loaded, decoded and added
     // before the next is issued (a scheduling fence between them).  This is

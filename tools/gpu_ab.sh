@@ -150,6 +150,12 @@ for s in $STEPS; do
         timeout -k 10 300 python tools/half_always_probe.py 4 >> $O/half_always_probe.jsonl 2>> $O/half_always_probe.err || exit 46
       done
       ;;
+    rot)      # sub-window rotation per tile (IPLS_ROT=1 build) vs shipped, 3 processes
+      for i in 1 2 3; do
+        timeout -k 10 400 python tools/half_always_probe.py 4 libipls_agg_rot.so C,Cround,F,B,D \
+          >> $O/rot_probe.jsonl 2>> $O/rot_probe.err || exit 49
+      done
+      ;;
     gloo8)    # the N = 8 bench over gloo with every rank on GPU 0 (rehearsal of the 8-GPU code path and memory)
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29508 bench.py --gpus 8 --dist-backend gloo --steps 10 --warmup 2 \
