@@ -367,8 +367,10 @@ int ipls_agg_reduce_partial(ipls_agg *h, int slot, int p_first, int n_parts, con
 
 /* For every partition of [p_first, p_first+n_parts): REP[p] += the partial of
  * every slot that folded into p since the last combine, slots ascending, in
- * one launch per owner shard that reads the partials over xGMI; the partials
- * are then logically +0.0 again.  Returns the number of partials folded.
+ * one launch per owner shard that reads the partials over xGMI (partitions
+ * with the same number of live slots share a launch whichever GPUs hold their
+ * partials, so an owner reads over all its links at once); the partials are
+ * then logically +0.0 again.  Returns the number of partials folded.
  * A pair of devices without peer access is not an error: such a partial is
  * first copied into an owner-side buffer (hipMemcpyPeerAsync on the owner's
  * stream) and the same fold reads that copy, in the same slot order, so the

@@ -1059,67 +1059,83 @@ int ipls_agg_combine_partials(ipls_agg* H, int p_first, int n_parts) {
   if (n_parts <= 0 || p_first < 0 || p_first + n_parts > H->P)
     return ferr(H, IPLS_E_RANGE, "partitions [%d,%d) out of range [0,%d)", p_first, p_first + n_parts, H->P);
   std::lock_guard<std::mutex> lk(H->mu);
-  const int S = H->S();
+  const int S = H->S(), end = p_first + n_parts;
+  auto live_slots = [&](int q) {
+    std::vector<int> v;
+    for (int s = 0; s < S; ++s)
+      if (!H->part[s].empty() && H->part[s][q].live) v.push_back(s);
+    return v;
+  };
   int total = 0, n_staged = 0;
   int p = p_first;
-  while (p < p_first + n_parts) {
-    // a run of partitions of one owner with the same live slots -> one launch
+  while (p < end) {
+    // A run of partitions of one owner with the same NUMBER of live slots is
+    // one launch, whichever GPUs hold them: the pointer table is per
+    // partition, so an owner whose partitions' replicas sit on different GPUs
+    // (ReplicaPlan.spread: every owner pulls from all G-1 others) reads them
+    // all at once, over every link, instead of one link per launch.
     const int o = H->owner[p];
-    std::vector<int> slots;
-    for (int s = 0; s < S; ++s)
-      if (!H->part[s].empty() && H->part[s][p].live) slots.push_back(s);
+    std::vector<std::vector<int>> sl{live_slots(p)};
+    const size_t k = sl[0].size();
     int e = p + 1;
-    while (e < p_first + n_parts && H->owner[e] == o) {
-      std::vector<int> s2;
-      for (int s = 0; s < S; ++s)
-        if (!H->part[s].empty() && H->part[s][e].live) s2.push_back(s);
-      if (s2 != slots) break;
+    while (e < end && H->owner[e] == o) {
+      std::vector<int> v = live_slots(e);
+      if (v.size() != k) break;
+      sl.push_back(std::move(v));
       ++e;
     }
-    if (!slots.empty()) {
+    if (k > 0) {
+      const int od = H->devices[o];
       hipStream_t ost = (hipStream_t)dev_stream(H->sh[o]);
-      if (dev_use(H->devices[o]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
-      const int k = (int)slots.size();
+      // no xGMI peer access (or IPLS_PEER_STAGED=1): copy each such partial
+      // into an owner-side buffer on its SLOT's stream -- the copies of
+      // different slots run on their own engines at once -- and re-record its
+      // `ready` there; the same fold then reads the copies in the same order
+      std::vector<std::vector<char>> staged(e - p, std::vector<char>(k, 0));
+      for (int q = p; q < e; ++q)
+        for (size_t j = 0; j < k; ++j) {
+          const int s = sl[q - p][j];
+          if (H->peer[o][s] && !(H->force_staged && s != o)) continue;
+          Partial& x = H->part[s][q];
+          const size_t nb = (size_t)H->len[q] * 8;
+          if (!x.stage && (dev_use(od) != hipSuccess || hipMalloc(&x.stage, nb) != hipSuccess)) {
+            (void)hipGetLastError();
+            return ferr(H, IPLS_E_NOMEM, "staging buffer of partition %d on device %d", q, od);
+          }
+          hipStream_t sst = (hipStream_t)dev_stream(H->sh[s]);
+          if (dev_use(H->devices[s]) != hipSuccess ||
+              hipMemcpyPeerAsync(x.stage, od, x.d, H->devices[s], nb, sst) != hipSuccess ||
+              hipEventRecord(x.ready, sst) != hipSuccess) {
+            (void)hipGetLastError();
+            return ferr(H, IPLS_E_DEVICE, "partial copy from device %d to %d failed", H->devices[s], od);
+          }
+          staged[q - p][j] = 1;
+          ++n_staged;
+        }
+      if (dev_use(od) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
       std::vector<const void*> ptrs((size_t)(e - p) * k);
       for (int q = p; q < e; ++q)
-        for (int j = 0; j < k; ++j) {
-          const int s = slots[j];
-          Partial& x = H->part[s][q];
+        for (size_t j = 0; j < k; ++j) {
+          Partial& x = H->part[sl[q - p][j]][q];
           if (hipStreamWaitEvent(ost, x.ready, 0) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipStreamWaitEvent failed");
-          const void* src = x.d;
-          if (!H->peer[o][s] || (H->force_staged && s != o)) {
-            // no xGMI peer access: copy the partial into an owner-side buffer
-            // on the owner's stream (HIP routes the copy), then the same fold
-            // in the same slot order reads it locally
-            const size_t nb = (size_t)H->len[q] * 8;
-            if (!x.stage && hipMalloc(&x.stage, nb) != hipSuccess) {
-              (void)hipGetLastError();
-              return ferr(H, IPLS_E_NOMEM, "staging buffer of partition %d on device %d", q, H->devices[o]);
-            }
-            if (hipMemcpyPeerAsync(x.stage, H->devices[o], x.d, H->devices[s], nb, ost) != hipSuccess) {
-              (void)hipGetLastError();
-              return ferr(H, IPLS_E_DEVICE, "partial copy from device %d to %d failed", H->devices[s], H->devices[o]);
-            }
-            src = x.stage;
-            ++n_staged;
-          }
-          ptrs[(size_t)(q - p) * k + j] = src;
+          ptrs[(size_t)(q - p) * k + j] = staged[q - p][j] ? (const void*)x.stage : (const void*)x.d;
         }
-      // REP[q] = ((REP[q] + R_s1) + R_s2) ...: the Updater replica branch /
-      // Collect_Replicas fold (Updater.java:40-44, IPLS.java:1222-1234)
+      // REP[q] = ((REP[q] + R_s1) + R_s2) ..., slots ascending per partition:
+      // the Updater replica branch / Collect_Replicas fold (Updater.java:40-44,
+      // IPLS.java:1222-1234)
       H->last_shard = o;
-      if (int rc = fwd(H, o, dev_reduce_batch(H->sh[o], p - H->lo[o], e - p, ptrs.data(), k, IPLS_DEV_F64,
+      if (int rc = fwd(H, o, dev_reduce_batch(H->sh[o], p - H->lo[o], e - p, ptrs.data(), (int)k, IPLS_DEV_F64,
                                               IPLS_START_ACCUM, IPLS_TGT_REP)))
         return rc;
-      if (dev_use(H->devices[o]) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
+      if (dev_use(od) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipSetDevice failed");
       for (int q = p; q < e; ++q)
-        for (int s : slots) {
+        for (int s : sl[q - p]) {
           Partial& x = H->part[s][q];
           if (hipEventRecord(x.consumed, ost) != hipSuccess) return ferr(H, IPLS_E_DEVICE, "hipEventRecord failed");
           x.consumed_pending = true;
           x.live = false;
         }
-      total += (e - p) * k;
+      total += (e - p) * (int)k;
     }
     p = e;
   }

@@ -276,6 +276,42 @@ def test_staged_combine_and_indirect_without_peer_access(ipls, O, monkeypatch):
     agg.close()
 
 
+@pytest.mark.parametrize("staged", [False, True])
+def test_combine_one_launch_per_owner_across_slots(ipls, O, monkeypatch, staged):
+    """The spread replica plan (every owner pulls from all G-1 other GPUs):
+    the partitions of one owner have their partials on DIFFERENT slots, one
+    each.  The combine folds them in one launch per owner (per-partition
+    pointer table), so on 8 GPUs an owner reads over all its links at once;
+    here [0]*4, 3 partitions per owner of 4M (the half shape: a 3-partition
+    launch has 3x the grid of a 1-partition one).  Bit-exact against the
+    oracle's replica expression, with peer loads and with staged copies."""
+    if staged:
+        monkeypatch.setenv("IPLS_PEER_STAGED", "1")
+    G, Pg, L, K, kh = 4, 3, 4_194_304, 4, 2
+    P = G * Pg
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=[0] * G)
+    monkeypatch.delenv("IPLS_PEER_STAGED", raising=False)
+    t, rows = dev_buckets(ipls, P, L, K)
+    slot = {o * Pg + q: (o + 1 + q % (G - 1)) % G for o in range(G) for q in range(Pg)}
+    assert len({slot[q] for q in range(Pg)}) == Pg            # owner 0's partitions: three different slots
+    # one partition alone first, for the grid of a 1-partition combine launch
+    agg.reduce_partial(slot[P - 1], P - 1, [rows[P - 1][kh:]])
+    assert agg.combine_partials(P - 1, 1) == 1
+    g1 = agg.last_launch()["grid"]
+    agg.reset()
+    agg.reduce_batch(0, [r[:kh] for r in rows], start_mode=ipls.START_ZERO)
+    for p in range(P):
+        agg.reduce_partial(slot[p], p, [rows[p][kh:]])
+    assert agg.combine_partials() == P
+    li = agg.last_launch()
+    assert li["grid"] == Pg * g1, (li, g1)                    # the last owner's 3 partitions in one launch
+    assert li["staged"] == (P if staged else 0)
+    agg.AggregatePartition(ipls.ALL_PARTITIONS)
+    for p in range(P):
+        assert agg.checksum(p, ipls.TGT_WEIGHTS) == O.c_synth_replica_checksum(L, p, K, kh), p
+    agg.close()
+
+
 def test_indirect_requests_from_two_threads_on_two_shards(ipls, O):
     """the handle's ONE Gradient_Buff lives on shard 0, so a
     hash-only request for a partition of shard 1 loads it there and folds it
