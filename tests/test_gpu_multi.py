@@ -282,8 +282,8 @@ def test_combine_one_launch_per_owner_across_slots(ipls, O, monkeypatch, staged)
     the partitions of one owner have their partials on DIFFERENT slots, one
     each.  The combine folds them in one launch per owner (per-partition
     pointer table), so on 8 GPUs an owner reads over all its links at once;
-    here [0]*4, 3 partitions per owner of 4M (the half shape: a 3-partition
-    launch has 3x the grid of a 1-partition one).  Bit-exact against the
+    here [0]*4, 3 partitions per owner of 4M (the half shape: 256 tiles per
+    partition, so one launch over all three has a grid of 768).  Bit-exact against the
     oracle's replica expression, with peer loads and with staged copies."""
     if staged:
         monkeypatch.setenv("IPLS_PEER_STAGED", "1")
@@ -294,17 +294,13 @@ def test_combine_one_launch_per_owner_across_slots(ipls, O, monkeypatch, staged)
     t, rows = dev_buckets(ipls, P, L, K)
     slot = {o * Pg + q: (o + 1 + q % (G - 1)) % G for o in range(G) for q in range(Pg)}
     assert len({slot[q] for q in range(Pg)}) == Pg            # owner 0's partitions: three different slots
-    # one partition alone first, for the grid of a 1-partition combine launch
-    agg.reduce_partial(slot[P - 1], P - 1, [rows[P - 1][kh:]])
-    assert agg.combine_partials(P - 1, 1) == 1
-    g1 = agg.last_launch()["grid"]
-    agg.reset()
     agg.reduce_batch(0, [r[:kh] for r in rows], start_mode=ipls.START_ZERO)
     for p in range(P):
         agg.reduce_partial(slot[p], p, [rows[p][kh:]])
     assert agg.combine_partials() == P
     li = agg.last_launch()
-    assert li["grid"] == Pg * g1, (li, g1)                    # the last owner's 3 partitions in one launch
+    # the last owner's 3 partitions in one launch: 3 x 256 half tiles (one partition alone: 256)
+    assert (li["kernel"], li["shape"], li["grid"]) == (ipls.KERNEL_REDUCE, ipls.SHAPE_HALF, Pg * 256), li
     assert li["staged"] == (P if staged else 0)
     agg.AggregatePartition(ipls.ALL_PARTITIONS)
     for p in range(P):
