@@ -133,6 +133,11 @@ for s in $STEPS; do
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 29
       ;;
+    repeat)   # three default bench runs (no CPU baseline) on one box: the process-to-process spread
+      for i in 1 2 3; do
+        timeout -k 10 400 python bench.py --no-cpu-baseline >> $O/bench_repeat.jsonl 2>> $O/bench_repeat.err || exit 50
+      done
+      ;;
     dprobe)   # config D in the default line vs the A/B leg, same process: with and without the other legs
       timeout -k 10 400 python bench.py --no-cpu-baseline --no-e2e --no-per-arrival --be-schedule-ab \
         >> $O/dprobe.jsonl 2>> $O/dprobe.err || exit 30
