@@ -161,6 +161,11 @@ for s in $STEPS; do
           >> $O/rot_probe.jsonl 2>> $O/rot_probe.err || exit 49
       done
       ;;
+    soak2)    # longer soaks: 120 production-length seeds, 1000 short ones, ingest mutations
+      timeout -k 10 1000 python -u tools/fuzz_stateful.py 5000 120 big > $O/fuzz_stateful_big_120.txt 2>&1 || exit 51
+      timeout -k 10 600 python -u tools/fuzz_stateful.py 6000 1000 > $O/fuzz_stateful_1000.txt 2>&1 || exit 52
+      timeout -k 10 600 python -u tools/fuzz_ingest.py 7000 200 > $O/fuzz_ingest_200.txt 2>&1 || exit 53
+      ;;
     gloo8)    # the N = 8 bench over gloo with every rank on GPU 0 (rehearsal of the 8-GPU code path and memory)
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29508 bench.py --gpus 8 --dist-backend gloo --steps 10 --warmup 2 \
