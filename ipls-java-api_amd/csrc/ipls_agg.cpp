@@ -81,7 +81,6 @@ class ShardPool {
         w->th.join();
       }
   }
-  bool has(int s) const { return s > 0 && s < (int)w_.size() && w_[s]; }
   void post(int s, std::function<void()> fn) {
     W* w = w_[s].get();
     {
@@ -242,10 +241,19 @@ int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
   std::mutex m;
   std::condition_variable cv;
   size_t left = ss.size() - 1;
-  for (size_t i = 1; i < ss.size(); ++i) {
-    auto task = [&, i] {
+  // one shard's part; never throws (the caller waits for every part, and the
+  // parts reference this frame)
+  auto part = [&](size_t i) noexcept {
+    try {
       rc[i] = fn(ss[i]);
       if (rc[i] < 0) msg[i] = dev_last_error(nullptr);
+    } catch (...) {
+      rc[i] = IPLS_E_NOMEM;
+    }
+  };
+  for (size_t i = 1; i < ss.size(); ++i) {
+    auto task = [&, i]() noexcept {
+      part(i);
       std::lock_guard<std::mutex> lk(m);
       if (--left == 0) cv.notify_one();
     };
@@ -255,8 +263,7 @@ int par_shards(ipls_agg* H, const std::vector<int>& ss, F fn) {
       task();
     }
   }
-  rc[0] = fn(ss[0]);
-  if (rc[0] < 0) msg[0] = dev_last_error(nullptr);
+  part(0);
   {
     std::unique_lock<std::mutex> lk(m);
     cv.wait(lk, [&] { return left == 0; });
