@@ -152,12 +152,12 @@ for s in $STEPS; do
       ;;
     halfalways)  # the big shape's remaining grids (C fold / round / ACCUM, F fold) vs the half shape, 3 processes
       for i in 1 2 3; do
-        timeout -k 10 300 python tools/half_always_probe.py 4 >> $O/half_always_probe.jsonl 2>> $O/half_always_probe.err || exit 46
+        timeout -k 10 300 python tools/variant_probe.py 4 >> $O/half_always_probe.jsonl 2>> $O/half_always_probe.err || exit 46
       done
       ;;
     rot)      # sub-window rotation per tile (IPLS_ROT=1 build) vs shipped, 3 processes
       for i in 1 2 3; do
-        timeout -k 10 400 python tools/half_always_probe.py 4 libipls_agg_rot.so C,Cround,F,B,D \
+        timeout -k 10 400 python tools/variant_probe.py 4 libipls_agg_rot.so C,Cround,F,B,D \
           >> $O/rot_probe.jsonl 2>> $O/rot_probe.err || exit 49
       done
       ;;

@@ -5,7 +5,7 @@ shape) on the grids the big shape ships for: config C's fold, its fused
 round, ACCUM on C, config F's fold, config B's fold, config D's BE in + out
 fold.  Same process, same buckets, interleaved rounds, HIP events on each
 handle's stream; results compared bit for bit.
-Usage: half_always_probe.py [ROUNDS] [VARIANT_SO] [CASES]   (needs make -C ipls-java-api_amd variants;
+Usage: variant_probe.py [ROUNDS] [VARIANT_SO] [CASES]   (needs make -C ipls-java-api_amd variants;
 CASES: comma list of C,Cround,Caccum,F,B,D)"""
 import json
 import sys
