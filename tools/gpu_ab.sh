@@ -116,6 +116,13 @@ for s in $STEPS; do
         --steps 3 --warmup 1 > $O/pmc_write_F.log 2>&1 || exit 48
       cd $R
       ;;
+    cpol)     # cache-policy bits of the bucket loads (buffer loads, sc0/sc1/nt) on C, F and B, three processes
+      for i in 1 2 3; do
+        SWEEP_QUICK=1 SWEEP_CPOL=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 4194304 32 32 10 >> $O/sweep_cpol_C.txt 2>&1 || exit 54
+      done
+      SWEEP_QUICK=1 SWEEP_CPOL=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep 16 8388608 64 32 6 >> $O/sweep_cpol_F.txt 2>&1 || exit 54
+      SWEEP_QUICK=1 SWEEP_CPOL=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 1048576 8 32 40 >> $O/sweep_cpol_B.txt 2>&1 || exit 54
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \

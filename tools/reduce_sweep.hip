@@ -88,6 +88,41 @@ __global__ __launch_bounds__(BS) void k_exp(const unsigned long long* const* __r
     __builtin_nontemporal_store(encode2<false>(acc[r]), (gu2)(d + (size_t)r * BS * 16 + lane16));
 }
 
+// Cache-policy probe (SWEEP_CPOL): the same ZERO-start fold, each bucket
+// read through a buffer resource with the load's cache-policy bits set
+// explicitly (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1); full tiles only,
+// partition-major.  The shipped kernel's loads are global_load ... nt (2).
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+template <int CPOL, int R, int BS>
+__global__ __launch_bounds__(BS) void k_cpol(const unsigned long long* const* __restrict__ bufs,
+                                             unsigned long long* __restrict__ dst, int64_t dstride, int k,
+                                             int tpp) {
+  const int q = blockIdx.x / tpp, t = blockIdx.x - q * tpp;
+  const int64_t base = (int64_t)t * BS * 2 * R;
+  const unsigned lane16 = threadIdx.x * 16u;
+  const unsigned long long* const* pb = bufs + (size_t)q * k;
+  d2 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = d2{0.0, 0.0};
+  for (int j = 0; j < k; ++j) {
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(pb[j] + base), (short)0, BS * 16 * R, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(r * BS * 16) + lane16, 0, CPOL);
+      const u2 w = u2{(unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                      (unsigned long long)v.z | ((unsigned long long)v.w << 32)};
+      const d2 x = decode2<false>(w);
+      acc[r].x = acc[r].x + x.x;
+      acc[r].y = acc[r].y + x.y;
+    }
+  }
+  char* d = (char*)(dst + q * dstride + base);
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    __builtin_nontemporal_store(encode2<false>(acc[r]), (gu2)(d + (size_t)r * BS * 16 + lane16));
+}
+
 __global__ __launch_bounds__(kBlock) void k_copy(const u2* __restrict__ in, u2* __restrict__ out, int64_t n2) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (int64_t)gridDim.x * kBlock)
     __builtin_nontemporal_store(__builtin_nontemporal_load((gcu2)(in + i)), (gu2)(out + i));
@@ -307,6 +342,27 @@ int main(int argc, char** argv) {
       ADDSB(16, 1024, 0);
       ADDSB(16, 512, 0);
     }
+  }
+  if (getenv("SWEEP_CPOL") && !be && L % (1024 * 2 * 16) == 0) {   // cache policy of the bucket loads
+    ADDSB(16, 1024, 0);   // shipped (global_load ... nt)
+#define CPOLV(C, BS)                                                                              \
+    vars.push_back(Var{"cpol " #C " R=16 BS=" #BS,                                                   \
+                       [=](hipStream_t s) {                                                        \
+                         const int tpp = (int)(L / ((int64_t)BS * 2 * 16));                        \
+                         hipLaunchKernelGGL((k_cpol<C, 16, BS>), dim3(tpp * P), dim3(BS), 0, s,    \
+                                            (const unsigned long long* const*)d_ptrs, dst,         \
+                                            (L + 31) / 32 * 32, K, tpp);                           \
+                       },                                                                          \
+                       alg, {}})
+    CPOLV(2, 1024);
+    CPOLV(0, 1024);
+    CPOLV(1, 1024);
+    CPOLV(3, 1024);
+    CPOLV(16, 1024);
+    CPOLV(18, 1024);
+    CPOLV(17, 1024);
+    CPOLV(19, 1024);
+#undef CPOLV
   }
   if (getenv("SWEEP_BS")) {   // block size / fence interval of the big-endian fold
     ADDSB(16, 1024, 2);
