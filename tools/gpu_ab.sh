@@ -123,6 +123,14 @@ for s in $STEPS; do
       SWEEP_QUICK=1 SWEEP_CPOL=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep 16 8388608 64 32 6 >> $O/sweep_cpol_F.txt 2>&1 || exit 54
       SWEEP_QUICK=1 SWEEP_CPOL=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 1048576 8 32 40 >> $O/sweep_cpol_B.txt 2>&1 || exit 54
       ;;
+    cpolbe)   # big-endian in + out through buffer loads (no SEQ fences) vs the shipped SEQF = 3 kernel, D and C shapes
+      for i in 1 2; do
+        SWEEP_QUICK=1 SWEEP_CPOL_BE=1 SWEEP_BE=1 SWEEP_BE_OUT=1 timeout -k 10 200 ipls-java-api_amd/lib/reduce_sweep 64 4194304 32 32 8 \
+          >> $O/sweep_cpol_be_D.txt 2>&1 || exit 55
+        SWEEP_QUICK=1 SWEEP_CPOL_BE=1 SWEEP_BE=1 SWEEP_BE_OUT=1 timeout -k 10 120 ipls-java-api_amd/lib/reduce_sweep 16 4194304 32 32 10 \
+          >> $O/sweep_cpol_be_C.txt 2>&1 || exit 55
+      done
+      ;;
     bpmc)
       cd /tmp
       timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $O/pmc_fetch_B -o run -- \

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(BS) void k_exp(const unsigned long long* const* __r
 // explicitly (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1); full tiles only,
 // partition-major.  The shipped kernel's loads are global_load ... nt (2).
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-template <int CPOL, int R, int BS>
+template <int CPOL, int R, int BS, bool BE = false>
 __global__ __launch_bounds__(BS) void k_cpol(const unsigned long long* const* __restrict__ bufs,
                                              unsigned long long* __restrict__ dst, int64_t dstride, int k,
                                              int tpp) {
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(BS) void k_cpol(const unsigned long long* const* __
       const u4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(r * BS * 16) + lane16, 0, CPOL);
       const u2 w = u2{(unsigned long long)v.x | ((unsigned long long)v.y << 32),
                       (unsigned long long)v.z | ((unsigned long long)v.w << 32)};
-      const d2 x = decode2<false>(w);
+      const d2 x = decode2<BE>(w);
       acc[r].x = acc[r].x + x.x;
       acc[r].y = acc[r].y + x.y;
     }
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(BS) void k_cpol(const unsigned long long* const* __
   char* d = (char*)(dst + q * dstride + base);
 #pragma unroll
   for (int r = 0; r < R; ++r)
-    __builtin_nontemporal_store(encode2<false>(acc[r]), (gu2)(d + (size_t)r * BS * 16 + lane16));
+    __builtin_nontemporal_store(encode2<BE>(acc[r]), (gu2)(d + (size_t)r * BS * 16 + lane16));
 }
 
 __global__ __launch_bounds__(kBlock) void k_copy(const u2* __restrict__ in, u2* __restrict__ out, int64_t n2) {
@@ -342,6 +342,22 @@ int main(int argc, char** argv) {
       ADDSB(16, 1024, 0);
       ADDSB(16, 512, 0);
     }
+  }
+  if (getenv("SWEEP_CPOL_BE") && be && be_out && L % (1024 * 2 * 16) == 0) {   // big-endian through buffer loads
+    ADDSB(16, 1024, 3);   // shipped (global_load ... nt, SEQF = 3)
+#define CPOLB(R, BS)                                                                              \
+    vars.push_back(Var{"cpol 2 BE in+out R=" #R " BS=" #BS,                                        \
+                       [=](hipStream_t s) {                                                        \
+                         const int tpp = (int)(L / ((int64_t)BS * 2 * R));                         \
+                         hipLaunchKernelGGL((k_cpol<2, R, BS, true>), dim3(tpp * P), dim3(BS), 0, s, \
+                                            (const unsigned long long* const*)d_ptrs, dst,         \
+                                            (L + 31) / 32 * 32, K, tpp);                           \
+                       },                                                                          \
+                       alg, {}})
+    CPOLB(16, 1024);
+    CPOLB(16, 512);
+    CPOLB(8, 1024);
+#undef CPOLB
   }
   if (getenv("SWEEP_CPOL") && !be && L % (1024 * 2 * 16) == 0) {   // cache policy of the bucket loads
     ADDSB(16, 1024, 0);   // shipped (global_load ... nt)
