@@ -1302,17 +1302,21 @@ def test_concurrent_failures_keep_their_messages(ipls, O):
         assert_bits_equal(agg.read(1), np.zeros(L), "partition 1 untouched by rejected buckets")
 
 
-def test_concurrent_callers_one_handle(ipls, O):
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_concurrent_callers_one_handle(ipls, O, devices=None):
     """The reference's producer threads, Updater thread and daemon thread all
     reach the accumulators (serialised by PeerData.mtx, PeerData.java:27).
     Four Python threads (ctypes drops the GIL) share one handle, each owning
     its own partitions so the per-partition order is fixed: synchronous host
-    and device folds, queued device folds, pubsub ingest and reads interleave.
-    Every partition must end bit-identical to the oracle's fold in that
-    thread's order."""
+    and device folds, queued device folds, pubsub ingest, hash-only requests
+    through the handle's one Gradient_Buff, and reads interleave.  Every
+    partition must end bit-identical to the oracle's fold in that thread's
+    order.  ``devices=[0, 0, 0]``: the same over a three-shard handle (the
+    persistent shard workers, the Gradient_Buff sequence lock, handle-wide
+    tickets)."""
     import threading
     P, L, T = 8, 30011, 4
-    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
     agg.set_coalesce(3)
     vals = [O.synth_bucket(L, 7, k) for k in range(6)]
     dev = []
@@ -1321,6 +1325,7 @@ def test_concurrent_callers_one_handle(ipls, O):
         dev.append((t, ipls.DeviceBuffer.from_tensor(t)))
     torch.cuda.synchronize()
     msgs = [O.pubsub_message(O.frame_encode(v, 0, 1, 3, b"QmT")) for v in vals]
+    files = [O.be_encode(v) for v in vals]          # full-length `ipfs cat` files (hash-only requests)
     plans = {}
     errors = []
 
@@ -1332,7 +1337,7 @@ def test_concurrent_callers_one_handle(ipls, O):
             for j in range(60):
                 p = mine[j % len(mine)]
                 k = int(rng.integers(0, len(vals)))
-                how = int(rng.integers(0, 4))
+                how = int(rng.integers(0, 5))
                 if how == 0:
                     agg.Update(vals[k], p)
                 elif how == 1:
@@ -1341,9 +1346,11 @@ def test_concurrent_callers_one_handle(ipls, O):
                     t = agg.UpdateAsync(dev[k][1], p)
                     if j % 5 == 0:
                         agg.Wait(t)            # host waits run with the handle's lock released
-                else:
+                elif how == 3:
                     n, st = agg.ingest_pubsub([msgs[k]], partitions=[p])
                     assert n == 1 and st == [0]
+                else:                          # through the handle's one Gradient_Buff (on shard 0)
+                    agg.UpdateIndirect(files[k], p)
                 seq.append((p, k))
                 if j % 17 == 0:
                     agg.read(p)

@@ -181,6 +181,10 @@ for s in $STEPS; do
       timeout -k 10 600 python -u tools/fuzz_stateful.py 6000 1000 > $O/fuzz_stateful_1000.txt 2>&1 || exit 52
       timeout -k 10 600 python -u tools/fuzz_ingest.py 7000 200 > $O/fuzz_ingest_200.txt 2>&1 || exit 53
       ;;
+    stress)   # the four-thread shared-handle test 200 times, one- and three-shard handles
+      timeout -k 10 600 python -u tools/stress_concurrent.py 200 > $O/stress_concurrent_200.txt 2>&1 || exit 56
+      timeout -k 10 600 python -u tools/stress_concurrent.py 200 sharded > $O/stress_concurrent_sharded_200.txt 2>&1 || exit 57
+      ;;
     gloo8)    # the N = 8 bench over gloo with every rank on GPU 0 (rehearsal of the 8-GPU code path and memory)
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29508 bench.py --gpus 8 --dist-backend gloo --steps 10 --warmup 2 \
