@@ -1303,7 +1303,7 @@ def test_concurrent_failures_keep_their_messages(ipls, O):
 
 
 @pytest.mark.parametrize("devices", [None, [0, 0, 0]])
-def test_concurrent_callers_one_handle(ipls, O, devices=None):
+def test_concurrent_callers_one_handle(ipls, O, devices):
     """The reference's producer threads, Updater thread and daemon thread all
     reach the accumulators (serialised by PeerData.mtx, PeerData.java:27).
     Four Python threads (ctypes drops the GIL) share one handle, each owning
