@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--no-strong-leg", action="store_true",
                     help="N>1: skip the fixed-total-work leg (config D split over the ranks)")
     ap.add_argument("--replica-reps", type=int, default=5)
+    ap.add_argument("--no-ulp-leg", action="store_true",
+                    help="N>1: skip the collective-reduce ULP report (dist.reduce over all ranks vs the fixed order)")
     ap.add_argument("--no-multi-leg", action="store_true",
                     help="N>1: skip the single-handle multi-GPU leg (rank 0 drives all N GPUs through the C-ABI)")
     ap.add_argument("--multi-rehearsal", action="store_true",
@@ -279,6 +281,44 @@ def e2e_multi(ipls, torch, dist, group, rank, world, local, L, K, reps, verify) 
             "note": "pinned host BE buckets read zero-copy by one launch per round + AggregatePartition with the BE "
                     "sum written to pinned host memory; algorithmic bytes (K+1)*L*8 per rank per round; "
                     "PCIe Gen5 x16 per GPU ~56 GB/s per direction"}
+
+
+def rccl_reduce_leg(ipls, torch, dist, rank: int, world: int, local: int, L: int, reps: int,
+                    backend: str = "nccl") -> dict:
+    """RCCL's own reduction (ncclReduce(sum) = dist.reduce
+    over the world) of one partial per rank, against the fixed-order fold
+    ((+0.0 + R_0) + R_1 ...) that the replica exchange computes bit-exactly:
+    its max-ULP distance (ipls.distributed.rccl_reduce_ulp, rank 0 folds the
+    gathered partials) and its time.  Every rank's partial is a synthetic
+    bucket (partition 0, peer = rank).  Comparison only: the product exchange
+    stays fixed-order."""
+    from ipls.distributed import rccl_reduce_ulp
+    x = torch.empty(L, dtype=torch.float64, device=torch.device("cuda", local))
+    ipls.synth_fill(ipls.DeviceBuffer.from_tensor(x), 0, rank, ipls.SEED)
+    torch.cuda.synchronize()
+    if backend != "nccl":
+        x = x.cpu()
+    rep = rccl_reduce_ulp(x, rank, world)
+    red = x.clone()
+    dist.reduce(red, dst=0, op=dist.ReduceOp.SUM)     # warm
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.reduce(red, dst=0, op=dist.ReduceOp.SUM)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=x.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t[0].item()) / reps * 1e3
+    if rank != 0:
+        return {}
+    rep.update(reduce_ms=round(ms, 4), L=L, backend=backend,
+               reduce_GBps_in=round(world * L * 8 / ms / 1e6, 1),
+               note="dist.reduce of one L-double partial per rank to rank 0 (RCCL picks the association) vs the "
+                    "fixed rank-order fold from +0.0; max_ulp over all elements; reduce_GBps_in = partial bytes "
+                    "of all ranks / reduce time, max over ranks")
+    return rep
 
 
 def replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, reps, verify, backend="nccl") -> dict:
@@ -1342,7 +1382,8 @@ def main():
         torch.cuda.empty_cache()
         out["be_schedule_ab"] = side(be_schedule_ab, ipls, torch, local, verify=not args.no_verify)
     dog = None
-    if world > 1 and not args.be and not (args.no_replica_leg and args.no_strong_leg and args.no_multi_leg
+    if world > 1 and not args.be and not (args.no_replica_leg and args.no_ulp_leg and args.no_strong_leg
+                                          and args.no_multi_leg
                                           and args.no_e2e):
         # the multi-rank side legs are extra measurements: a watchdog ends a
         # stuck exchange (or a teardown stuck behind a peer that failed in it)
@@ -1360,6 +1401,15 @@ def main():
                 leg = {"error": f"{type(e).__name__}: {e}"}
             if out is not None:
                 out["replica_exchange"] = leg
+        if not args.no_ulp_leg:
+            stage[0] = "rccl_reduce_ulp"
+            try:
+                ul = rccl_reduce_leg(ipls, torch, dist, rank, world, local, L, args.replica_reps,
+                                     args.dist_backend)
+            except Exception as e:                   # reported, never fatal to the main line
+                ul = {"error": f"{type(e).__name__}: {e}"}
+            if out is not None:
+                out["rccl_reduce_ulp"] = ul
         if not args.no_strong_leg and not args.strong:
             stage[0] = "strong_scaling_D"
             del arena, rows

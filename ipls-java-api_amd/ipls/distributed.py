@@ -22,7 +22,8 @@ per replica); k remote partials arrive on k distinct xGMI links.
 
 ``mode="rccl_reduce"`` instead sums all partials with RCCL's own reduction
 (``dist.reduce``). It is faster to write but not bit-identical for more than
-2 contributors, because RCCL picks the association. It is only for comparison.
+2 contributors, because RCCL picks the association. It is only for comparison;
+``rccl_reduce_ulp`` measures how far it lands from the fixed order.
 
 The exchange code is written against two methods of the aggregator,
 ``export_partial`` and ``import_partial``. ``ipls.Aggregator`` implements
@@ -210,6 +211,52 @@ def finish_exchange(ex: Exchange) -> list[int]:
 def _empty(L, device):
     import torch
     return torch.empty(L, dtype=torch.float64, device=device)
+
+
+def ulp_distance(a, b):
+    """Per-element distance in units in the last place between two float64
+    tensors: both bit patterns mapped onto one monotone integer line (a
+    negative double -x maps to -(bits of x)), then subtracted.  +0.0 and -0.0
+    are 0 apart; NaNs are not expected here (the fold inputs are finite)."""
+    import torch
+
+    def line(x):
+        i = x.contiguous().view(torch.int64)
+        return torch.where(i >= 0, i, -(i & 0x7FFFFFFFFFFFFFFF))
+    return (line(a) - line(b)).abs()
+
+
+def rccl_reduce_ulp(partial, rank: int, world: int, *, dst: int = 0, group=None, keep: bool = False) -> dict | None:
+    """how far RCCL's own reduction (``ncclReduce(sum)``, here
+    ``dist.reduce``) lands from the reference's fixed-order fold.
+
+    Every rank contributes one partial of the same partition.  ``dst``
+    receives RCCL's sum, gathers the partials themselves, folds them in rank
+    order from +0.0 (``(+0.0 + R_0) + R_1 ...``, Updater.java:40-44 with a
+    fixed arrival order) and returns the element-wise ULP distance between
+    the two: ``max_ulp`` and how many elements differ.  RCCL picks the
+    association, so only 2 contributors are guaranteed 0 ULP (one add,
+    commutative).  Collective over ``group``: every rank calls it; only
+    ``dst`` gets the report (with both sums as ``sum``/``fixed`` if ``keep``)."""
+    import torch
+    import torch.distributed as dist
+
+    red = partial.clone()
+    dist.reduce(red, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    parts = [torch.empty_like(partial) for _ in range(world)] if rank == dst else None
+    dist.gather(partial, parts, dst=dst, group=group)
+    if rank != dst:
+        return None
+    fixed = torch.zeros_like(partial)                  # +0.0 start (START_ZERO)
+    for r in range(world):                             # ascending rank = the fixed arrival order
+        fixed = fixed + parts[r]                       # one IEEE add per element, as the fold does
+    d = ulp_distance(red, fixed)
+    rep = {"contributors": world, "max_ulp": int(d.max().item()),
+           "elements_differing": int((d != 0).sum().item()), "elements": int(partial.numel()),
+           "bit_identical": bool(torch.equal(red.view(torch.int64), fixed.view(torch.int64)))}
+    if keep:
+        rep.update(sum=red, fixed=fixed)
+    return rep
 
 
 class RankShard:

@@ -285,3 +285,54 @@ def test_rccl_reduce_rejects_a_caller_group():
     plan = ReplicaPlan.build(4, 2, {1: [1]})
     with pytest.raises(ValueError):
         combine_replicas(NumpyAggregator(4, 8), plan, 0, mode="rccl_reduce", group=object())
+
+
+def test_ulp_distance_known_pairs():
+    from ipls.distributed import ulp_distance
+    a = torch.tensor([1.0, -1.0, 0.0, -0.0, 1e16, 5e-324, -5e-324], dtype=torch.float64)
+    b = torch.tensor([np.nextafter(1.0, 2.0), np.nextafter(-1.0, -2.0), -0.0, 0.0,
+                      np.nextafter(np.nextafter(1e16, 2e16), 2e16), -5e-324, 5e-324], dtype=torch.float64)
+    assert ulp_distance(a, b).tolist() == [1, 1, 0, 0, 2, 2, 2]
+
+
+def ulp_worker(rank, world, port, L, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ipls.distributed import rccl_reduce_ulp
+    x = torch.from_numpy(bucket(0, rank, L))
+    rep = rccl_reduce_ulp(x, rank, world, keep=True)
+    q.put((rank, None if rep is None else {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in rep.items()}))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_reduce_ulp_report(world):
+    """the ULP report of the collective's own reduction against
+    the fixed-order fold (here gloo's reduce on the CPU; on the GPU box the
+    bench's N > 1 line runs it over RCCL).  The fixed order is checked against
+    the oracle's fold, the reported distances against a numpy recount."""
+    L = 1031
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=ulp_worker, args=(r, world, port, L, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert all(got[r] is None for r in range(1, world))
+    rep = got[0]
+    exp = np.zeros(L)
+    for r in range(world):
+        O.fold(exp, bucket(0, r, L))
+    assert_bits_equal(rep["fixed"], exp)
+    def line(v):
+        i = v.view(np.int64)
+        return np.where(i >= 0, i, -(i & 0x7FFFFFFFFFFFFFFF))
+    d = np.abs(line(rep["sum"]) - line(exp))
+    assert rep["max_ulp"] == int(d.max()) and rep["elements_differing"] == int((d != 0).sum())
+    assert rep["elements"] == L and rep["contributors"] == world
+    if world == 2:                                  # one add, commutative: no association to choose
+        assert rep["bit_identical"] and rep["max_ulp"] == 0
