@@ -234,7 +234,8 @@ def rccl_reduce_ulp(partial, rank: int, world: int, *, dst: int = 0, group=None,
     receives RCCL's sum, gathers the partials themselves, folds them in rank
     order from +0.0 (``(+0.0 + R_0) + R_1 ...``, Updater.java:40-44 with a
     fixed arrival order) and returns the element-wise ULP distance between
-    the two: ``max_ulp`` and how many elements differ.  RCCL picks the
+    the two: ``max_ulp``, how many elements differ, and the largest error
+    relative to the sum of the partials' magnitudes (in units u = 2^-53).  RCCL picks the
     association, so only 2 contributors are guaranteed 0 ULP (one add,
     commutative).  Collective over ``group``: every rank calls it; only
     ``dst`` gets the report (with both sums as ``sum``/``fixed`` if ``keep``)."""
@@ -251,7 +252,14 @@ def rccl_reduce_ulp(partial, rank: int, world: int, *, dst: int = 0, group=None,
     for r in range(world):                             # ascending rank = the fixed arrival order
         fixed = fixed + parts[r]                       # one IEEE add per element, as the fold does
     d = ulp_distance(red, fixed)
+    # ULPs blow up where the partials cancel (a sum near 0 has tiny ULPs): the
+    # error is also given against the sum of magnitudes, in units of 2^-53
+    mag = torch.zeros_like(partial)
+    for r in range(world):
+        mag = mag + parts[r].abs()
+    err = ((red - fixed).abs() / mag.clamp_min(torch.finfo(torch.float64).tiny)).max().item()
     rep = {"contributors": world, "max_ulp": int(d.max().item()),
+           "max_err_vs_sum_of_magnitudes_u": round(err * 2.0 ** 53, 3),
            "elements_differing": int((d != 0).sum().item()), "elements": int(partial.numel()),
            "bit_identical": bool(torch.equal(red.view(torch.int64), fixed.view(torch.int64)))}
     if keep:

@@ -334,5 +334,9 @@ def test_rccl_reduce_ulp_report(world):
     d = np.abs(line(rep["sum"]) - line(exp))
     assert rep["max_ulp"] == int(d.max()) and rep["elements_differing"] == int((d != 0).sum())
     assert rep["elements"] == L and rep["contributors"] == world
+    mag = sum(np.abs(bucket(0, r, L)) for r in range(world))
+    err = np.abs(rep["sum"] - exp) / np.maximum(mag, np.finfo(np.float64).tiny)
+    assert rep["max_err_vs_sum_of_magnitudes_u"] == pytest.approx(err.max() * 2.0 ** 53, abs=1e-3)
+    assert rep["max_err_vs_sum_of_magnitudes_u"] <= 2 * (world - 1)   # any association: (n-1)u-bounded
     if world == 2:                                  # one add, commutative: no association to choose
         assert rep["bit_identical"] and rep["max_ulp"] == 0
