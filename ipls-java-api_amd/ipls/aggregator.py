@@ -136,7 +136,9 @@ class Aggregator:
             pass
 
     def _chk(self, rc):
-        if rc < 0 and self._lib is not N.lib():   # a variant build keeps its own error slot
+        if rc >= 0:                                # the per-call fast path (UpdateAsync per arrival)
+            return rc
+        if self._lib is not N.lib():               # a variant build keeps its own error slot
             msg = self._lib.ipls_agg_last_error(None)
             raise N.IplsError(rc, msg.decode(errors="replace") if msg else "")
         return N.check(rc, self._h)
@@ -224,8 +226,10 @@ class Aggregator:
         target = N.TGT_AGG if from_clients else N.TGT_REP
         t = ctypes.c_uint64()
         if isinstance(gradient, DeviceBuffer):
-            self._chk(self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr, gradient.n,
-                                                          gradient.kind, ctypes.byref(t)))
+            rc = self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr, gradient.n,
+                                                     N.DEV_BE if gradient.big_endian else N.DEV_F64, ctypes.byref(t))
+            if rc < 0:
+                self._chk(rc)
             return t.value
         if not isinstance(gradient, PinnedBuffer):
             raise TypeError("UpdateAsync takes a PinnedBuffer (ipls_host_alloc memory) or a DeviceBuffer")
