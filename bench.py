@@ -866,7 +866,8 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
                      "verified_checksum_p0": (agg.checksum(0) == want) if verify else None}
     out["note"] = ("one call per arriving bucket (peer-major); each = a fold launch per arrival, "
                    "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), best of "
-                   f"{reps}; algorithmic bytes P*(K+1)*L*8; Python/ctypes caller")
+                   f"{reps}; algorithmic bytes P*(K+1)*L*8; Python caller through "
+                   + ("ipls._fast (CPython extension, csrc/pyfast.c)" if agg._fast is not None else "ctypes"))
     # the same calls from a native caller (what a JNI shim sees): tools/host_e2e.cpp, a child process
     exe = Path(__file__).resolve().parent / "ipls-java-api_amd" / "lib" / "host_e2e"
     if exe.exists():

@@ -159,6 +159,31 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+_fast = None
+
+
+def fast():
+    """ipls._fast (csrc/pyfast.c: the per-arrival accumulate calls without
+    ctypes) when it calls the very library lib() bound -- the in-tree build,
+    one mapping of one file, checked by comparing entry-point addresses --
+    else None, and the callers use the ctypes binding of the same library."""
+    global _fast
+    if _fast is None:
+        _fast = False
+        if LIB_PATH == PKG_ROOT / "lib" / "libipls_agg.so":
+            try:
+                from . import _fast as m
+            except ImportError:
+                m = None
+            if m is not None:
+                L = lib()
+                mine = (ctypes.cast(L.ipls_agg_accumulate_async, ctypes.c_void_p).value,
+                        ctypes.cast(L.ipls_agg_accumulate, ctypes.c_void_p).value)
+                if m.entry_points() == mine:
+                    _fast = m
+    return _fast or None
+
+
 def build_info() -> dict:
     """Provenance of the library this process loads: its sha256 now, and the
     build stamp written next to it at link time (tools/build_stamp.py: git

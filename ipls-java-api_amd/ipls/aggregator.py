@@ -108,6 +108,8 @@ class Aggregator:
         h = ctypes.c_void_p()
         N.check(self._lib.ipls_agg_open(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+        self._hv = h.value                      # the handle's address, for ipls._fast
+        self._fast = N.fast() if library is None else None
         self.model_size = model_size
         self.n_partitions = n_partitions
         self.secure = bool(secure)
@@ -120,6 +122,7 @@ class Aggregator:
     # ---- lifetime ----
     def close(self):
         if getattr(self, "_h", None):
+            self._hv = None
             self._lib.ipls_agg_close(self._h)
             self._h = None
 
@@ -215,6 +218,11 @@ class Aggregator:
                                                     a.size, N.HOST_PAIR if pair else N.HOST_FRAME))
             return
         ptr, n, kind, keep = _operand(gradient)
+        if self._fast is not None:
+            rc = self._fast.accumulate(self._hv, partition, target, ptr, n, kind)
+            if rc < 0:
+                self._chk(rc)
+            return
         self._chk(self._lib.ipls_agg_accumulate(self._h, partition, target, ptr, n, kind))
 
     def UpdateAsync(self, gradient, partition: int, from_clients: bool = True, *, big_endian: bool = True) -> int:
@@ -224,6 +232,12 @@ class Aggregator:
         partition's other queued buckets in one launch (set_coalesce).  Returns
         a ticket; keep the buffer until Wait(ticket)."""
         target = N.TGT_AGG if from_clients else N.TGT_REP
+        if self._fast is not None and isinstance(gradient, DeviceBuffer):
+            t = self._fast.accumulate_async(self._hv, partition, target, gradient.ptr, gradient.n,
+                                            N.DEV_BE if gradient.big_endian else N.DEV_F64)
+            if t < 0:
+                self._chk(t)
+            return t
         t = ctypes.c_uint64()
         if isinstance(gradient, DeviceBuffer):
             rc = self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr, gradient.n,

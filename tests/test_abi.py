@@ -219,3 +219,26 @@ def test_ctypes_signatures_match_the_header():
             elif base in elem and inner is not elem[base]:
                 bad.append(f"{name} arg {i}: C '{c}' bound POINTER({inner.__name__})")
     assert not bad, bad
+
+
+def test_fast_extension_calls_the_bound_library():
+    """ipls._fast (csrc/pyfast.c): the per-arrival accumulate calls without
+    ctypes.  It is linked against the in-tree library, and ipls uses it only
+    when its entry points are the ones ipls._native bound (one mapping of one
+    file); a null handle comes back as the library's error code and message,
+    bad arguments as Python exceptions before any library call."""
+    from ipls import _native as N
+    fast = N.fast()
+    assert fast is not None, "ipls._fast not built (make -C ipls-java-api_amd)"
+    L = N.lib()
+    assert fast.entry_points() == (ctypes.cast(L.ipls_agg_accumulate_async, ctypes.c_void_p).value,
+                                   ctypes.cast(L.ipls_agg_accumulate, ctypes.c_void_p).value)
+    for call in (fast.accumulate_async, fast.accumulate):
+        rc = call(None, 0, N.TGT_AGG, 0, 0, N.DEV_F64)
+        assert rc == N.IPLS_E_INVAL and "null" in N.last_error(None)
+        with pytest.raises(TypeError):
+            call(None, 0, N.TGT_AGG, 0, 0)
+        with pytest.raises(OverflowError):
+            call(None, 2 ** 40, N.TGT_AGG, 0, 0, N.DEV_F64)
+        with pytest.raises(TypeError):
+            call(None, 0, N.TGT_AGG, "not an address", 0, N.DEV_F64)
