@@ -247,6 +247,12 @@ class Aggregator:
             return t.value
         if not isinstance(gradient, PinnedBuffer):
             raise TypeError("UpdateAsync takes a PinnedBuffer (ipls_host_alloc memory) or a DeviceBuffer")
+        if self._fast is not None:
+            t = self._fast.accumulate_async(self._hv, partition, target, gradient.ptr, gradient.nbytes // 8,
+                                            N.HOST_BE if big_endian else N.HOST_F64)
+            if t < 0:
+                self._chk(t)
+            return t
         self._chk(self._lib.ipls_agg_accumulate_async(self._h, partition, target, gradient.ptr,
                                                       gradient.nbytes // 8,
                                                       N.HOST_BE if big_endian else N.HOST_F64, ctypes.byref(t)))
