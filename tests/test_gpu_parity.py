@@ -1695,3 +1695,53 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
     round_shapes = {s for k, s, _, _, _ in shapes if k == ipls.KERNEL_ROUND}
     for shape in ((ipls.SHAPE_BIG, ipls.SHAPE_HALF) if P == 4 else (ipls.SHAPE_HALF,)):
         assert shape in round_shapes, (shape, sorted(round_shapes))
+
+
+def test_fast_extension_and_ctypes_give_the_same_bits(ipls, O):
+    """A default Aggregator takes the per-arrival calls through ipls._fast
+    (csrc/pyfast.c); one bound to another ctypes mapping of the same library
+    (library=...) takes ctypes.  The same arrivals -- queued device buckets
+    (native and big-endian), pinned host buckets, synchronous host and device
+    Updates, both targets -- give the same bits through either, equal to the
+    oracle; errors come back the same way."""
+    from ipls import _native as N
+    P, L = 3, 40003
+    vals = [O.synth_bucket(L, 9, k) for k in range(6)]
+    dv = [dev(v) for v in vals[:3]]
+    bt, bb = dev_be(vals[3])
+    pb = ipls.PinnedBuffer(8 * L)
+    pb.view()[:] = np.frombuffer(O.be_encode(vals[4]), dtype=np.uint8)
+    torch.cuda.synchronize()
+    fast = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    slow = ipls.Aggregator(n_partitions=P, bucket_len=L, library=N.load(N.LIB_PATH))
+    assert fast._fast is not None and fast._fast is N.fast() and slow._fast is None
+    for agg in (fast, slow):
+        agg.set_coalesce(4)
+        t = [agg.UpdateAsync(dv[k][1], p) for p in range(P) for k in range(3)]
+        t.append(agg.UpdateAsync(bb, 1))
+        t.append(agg.UpdateAsync(pb, 2))
+        t.append(agg.UpdateAsync(dv[0][1], 0, from_clients=False))
+        assert t == sorted(t) and len(set(t)) == len(t)
+        agg.Wait(t[-1])
+        agg.Update(vals[5], 0)                                      # host doubles
+        agg.Update(np.frombuffer(O.be_encode(vals[5]), dtype=np.uint8), 2)  # host BE bytes
+        agg.Update(dv[1][1], 1, from_clients=False)                 # device, REP
+        with pytest.raises(ipls.IplsError):
+            agg.Update(vals[5], P)                                  # partition out of range
+        with pytest.raises(ipls.IplsError):
+            agg.UpdateAsync(dv[0][1], -1)
+        agg.sync()
+    ref_agg = [O.reduce([vals[0], vals[1], vals[2]] + extra, L) for extra in ([vals[5]], [vals[3]], [vals[4], vals[5]])]
+    ref_rep = [vals[0], vals[1], None]
+    for p in range(P):
+        a, b = fast.read(p, ipls.TGT_AGG), slow.read(p, ipls.TGT_AGG)
+        assert_bits_equal(a, b)
+        assert_bits_equal(a, ref_agg[p])
+        if ref_rep[p] is not None:
+            assert_bits_equal(fast.read(p, ipls.TGT_REP), slow.read(p, ipls.TGT_REP))
+            assert_bits_equal(fast.read(p, ipls.TGT_REP), O.reduce([ref_rep[p]], L))
+    fast.close()
+    slow.close()
+    pb.close()
+    with pytest.raises(ipls.IplsError):
+        fast.Update(vals[0], 0)                                     # closed handle: null, not a crash
