@@ -298,7 +298,10 @@ def rccl_reduce_leg(ipls, torch, dist, rank: int, world: int, local: int, L: int
     torch.cuda.synchronize()
     if backend != "nccl":
         x = x.cpu()
-    rep = rccl_reduce_ulp(x, rank, world)
+    try:
+        rep = rccl_reduce_ulp(x, rank, world)
+    except Exception as e:     # rank 0's local fold/compare failed: keep the ranks' collectives in step
+        rep = {"error": f"{type(e).__name__}: {e}"}
     red = x.clone()
     dist.reduce(red, dst=0, op=dist.ReduceOp.SUM)     # warm
     dist.barrier()
