@@ -185,6 +185,11 @@ for s in $STEPS; do
       timeout -k 10 600 python -u tools/stress_concurrent.py 200 > $O/stress_concurrent_200.txt 2>&1 || exit 56
       timeout -k 10 600 python -u tools/stress_concurrent.py 200 sharded > $O/stress_concurrent_sharded_200.txt 2>&1 || exit 57
       ;;
+    fastp)    # per-arrival calls: ipls._fast vs ctypes, interleaved, three processes
+      for i in 1 2 3; do
+        timeout -k 10 300 python -u tools/fast_probe.py 10 >> $O/fast_probe.jsonl 2>> $O/fast_probe.err || exit 58
+      done
+      ;;
     gloo8)    # the N = 8 bench over gloo with every rank on GPU 0 (rehearsal of the 8-GPU code path and memory)
       timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29508 bench.py --gpus 8 --dist-backend gloo --steps 10 --warmup 2 \
