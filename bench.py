@@ -830,7 +830,7 @@ def config_a_leg(ipls, reps: int = 20) -> dict:
                     "port of the Updater BE decode + fold and the GetPartitions divide"}
 
 
-def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, verify: bool, reps: int = 3) -> dict:
+def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, verify: bool, reps: int = 7) -> dict:
     """The headline workload folded the way Updater._Update folds its queue
     (Updater.java:115-117): one call per arriving bucket, peers arriving in
     turn (peer 0's P buckets, then peer 1's ...).  'each' is one fold launch
@@ -846,7 +846,7 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
         from oracle import oracle as O   # checker only
         want = O.c_synth_sum_checksum(L, 0, K)
     for mode in ("each", "coalesced"):
-        best = None
+        times = []
         for _ in range(reps):
             agg.reset()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -862,13 +862,14 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
                 agg.Wait(t)
             e1.record(stream)
             agg.sync()
-            ms = e0.elapsed_time(e1)
-            best = ms if best is None else min(best, ms)
+            times.append(e0.elapsed_time(e1))
+        best, med = min(times), float(np.median(times))
         out[mode] = {"ms": round(best, 4), "GBps": round(nbytes / best / 1e6, 1),
                      "frac": round(nbytes / best / 1e6 / HBM_PEAK_GBS, 4),
+                     "ms_median": round(med, 4), "frac_median": round(nbytes / med / 1e6 / HBM_PEAK_GBS, 4),
                      "verified_checksum_p0": (agg.checksum(0) == want) if verify else None}
     out["note"] = ("one call per arriving bucket (peer-major); each = a fold launch per arrival, "
-                   "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), best of "
+                   "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), best (and median) of "
                    f"{reps}; algorithmic bytes P*(K+1)*L*8; Python caller through "
                    + ("ipls._fast (CPython extension, csrc/pyfast.c)" if agg._fast is not None else "ctypes"))
     # the same calls from a native caller (what a JNI shim sees): tools/host_e2e.cpp, a child process
