@@ -16,6 +16,12 @@
 //     inside a tile: each wave's last W value goes through LDS to the next
 //     wave piece, whose lane 63 stores the pair (previous y, its lane 0's x),
 //     so every lane stores one 16-B pair (singles only at the tile's ends)
+//   8 wave pairs (round 3): vectors 2m and 2m+1 of a wave are adjacent 1 KiB
+//     pieces (the wave owns 2 KiB contiguous per pair, the CU still sweeps one
+//     32 KiB window per two vectors), averages first; for 8-mod-16 averages
+//     lane 63 of piece 2m stores (its y, piece 2m+1's lane-0 x), so singles
+//     fall every 2 KiB instead of every 1 KiB, with no LDS and no barrier
+//   9 the wave-pair layout of 8 with the shipped epilogue (the load-pattern cost)
 // Every variant that writes the real layout is checked bit-identical to the
 // shipped k_round (W and averages).
 // Usage: round_epilogue_sweep P L K REPS    (L a multiple of 32768)
@@ -79,8 +85,14 @@ __global__ __launch_bounds__(1024) void k_ep(const u64* const* __restrict__ bufs
   const u64* const* __restrict__ pb = bufs + (size_t)q * k;
   const int tid = threadIdx.x, lane = tid & 63;
   int64_t off[R];
+  if constexpr (V == 8 || V == 9) {
+    const int w = tid >> 6;
 #pragma unroll
-  for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * BS + tid);
+    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)(r >> 1) * 2 * BS + w * 128 + (r & 1) * 64 + lane);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)r * BS + tid);
+  }
   d2 acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = d2{0.0, 0.0};
@@ -107,7 +119,7 @@ __global__ __launch_bounds__(1024) void k_ep(const u64* const* __restrict__ bufs
     ax = cnt == 0.0 ? acc[r].x : acc[r].x / den;
     ay = cnt == 0.0 ? acc[r].y : acc[r].y / den;
   };
-  if constexpr (V == 0 || V == 3 || V == 4 || V == 6) {
+  if constexpr (V == 0 || V == 3 || V == 4 || V == 6 || V == 9) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       st16<V != 3>(dst + off[r], acc[r]);
@@ -165,6 +177,28 @@ __global__ __launch_bounds__(1024) void k_ep(const u64* const* __restrict__ bufs
         if (last && e + 1 < L - 1) st8(avg + e + 1, __builtin_bit_cast(u64, ay));
       }
       if (first && lane == 0) st8(avg + e, __builtin_bit_cast(u64, ax));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) st16<true>(dst + off[r], acc[r]);
+  } else if constexpr (V == 8) {
+#pragma unroll
+    for (int m = 0; m < R; m += 2) {
+      double ax, ay, bx, by;
+      A(m, ax, ay);
+      A(m + 1, bx, by);
+      const int64_t e = off[m], f = off[m + 1];   // f = e + 128
+      if (aligned) {
+        st16<true>(avg + e, d2{ax, ay});
+        if (f + 1 < L - 1) st16<true>(avg + f, d2{bx, by});
+        else st8(avg + f, __builtin_bit_cast(u64, bx));
+        continue;
+      }
+      const double nax = __shfl_down(ax, 1), nbx = __shfl_down(bx, 1);
+      const double b0 = __shfl(bx, 0);
+      if (lane == 0) st8(avg + e, __builtin_bit_cast(u64, ax));
+      st16<true>(avg + e + 1, d2{ay, lane < 63 ? nax : b0});
+      if (lane < 63) st16<true>(avg + f + 1, d2{by, nbx});
+      else if (f + 1 < L - 1) st8(avg + f + 1, __builtin_bit_cast(u64, by));
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) st16<true>(dst + off[r], acc[r]);
@@ -226,10 +260,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&o.d, P * sizeof(PartDesc)));
     CK(hipMemcpy(o.d, pd.data(), P * sizeof(PartDesc), hipMemcpyHostToDevice));
   };
-  Out ship, red, v[8];
+  Out ship, red, v[10];
   make(ship, L - 1, true);
   make(red, L - 1, false);
-  for (int i = 0; i < 8; ++i) make(v[i], i == 6 ? dl : L - 1, i != 5);
+  for (int i = 0; i < 10; ++i) make(v[i], i == 6 ? dl : L - 1, i != 5);
 
   struct Var {
     std::string name;
@@ -247,21 +281,22 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_round<false, kZero, 1, 16, 0, 1024>), dim3(tpp * P), dim3(1024), 0, 0, bp,
                                        ship.d, K, tpp, P, 0, d_cnt);
                   }, {}, round_b});
-  const char* names[8] = {"0 tool copy: W[r], avg[r]", "1 all W, then all avg", "2 all avg, then all W",
+  const char* names[10] = {"0 tool copy: W[r], avg[r]", "1 all W, then all avg", "2 all avg, then all W",
                           "3 W plain stores, avg nt", "4 W nt, avg plain stores", "5 W only (no averages)",
-                          "6 averages 256-B aligned", "7 avg first, LDS pair at wave ends"};
+                          "6 averages 256-B aligned", "7 avg first, LDS pair at wave ends",
+                          "8 wave pairs, avg first, merged pair", "9 wave-pair loads, shipped epilogue"};
 #define V(I)                                                                                                 \
   vars.push_back({names[I], [&] {                                                                            \
                     hipLaunchKernelGGL((k_ep<I>), dim3(tpp * P), dim3(1024), 0, 0, bp, v[I].d, K, tpp, d_cnt); \
                   }, {}, I == 5 ? red_b : round_b});
-  V(0) V(1) V(2) V(3) V(4) V(5) V(6) V(7)
+  V(0) V(1) V(2) V(3) V(4) V(5) V(6) V(7) V(8) V(9)
 #undef V
 
   for (auto& x : vars) x.run();
   CK(hipDeviceSynchronize());
   {
     std::vector<unsigned char> a(na), b(na);
-    for (int i : {0, 1, 2, 3, 4, 7}) {
+    for (int i : {0, 1, 2, 3, 4, 7, 8, 9}) {
       CK(hipMemcpy(a.data(), ship.a, na, hipMemcpyDeviceToHost));
       CK(hipMemcpy(b.data(), v[i].a, na, hipMemcpyDeviceToHost));
       const bool avg_ok = !memcmp(a.data(), b.data(), na);

@@ -6,7 +6,7 @@ round, ACCUM on C, config F's fold, config B's fold, config D's BE in + out
 fold.  Same process, same buckets, interleaved rounds, HIP events on each
 handle's stream; results compared bit for bit.
 Usage: variant_probe.py [ROUNDS] [VARIANT_SO] [CASES]   (needs make -C ipls-java-api_amd variants;
-CASES: comma list of C,Cround,Caccum,F,B,D)"""
+CASES: comma list of C,Cround,Caccum,F,B,D,Dround,Fround,Bround)"""
 import json
 import sys
 from pathlib import Path
@@ -82,7 +82,9 @@ def run(P, L, K, what, rounds, variant="libipls_agg_halfalways.so", be=False):
 
 CASES = {"C": (16, 4194304, 32, "reduce", False), "Cround": (16, 4194304, 32, "round", False),
          "Caccum": (16, 4194304, 32, "accum", False), "F": (16, 8388608, 64, "reduce", False),
-         "B": (16, 1048576, 8, "reduce", False), "D": (64, 4194304, 32, "reduce", True)}
+         "B": (16, 1048576, 8, "reduce", False), "D": (64, 4194304, 32, "reduce", True),
+         "Dround": (64, 4194304, 32, "round", False), "Fround": (16, 8388608, 64, "round", False),
+         "Bround": (16, 1048576, 8, "round", False)}
 
 if __name__ == "__main__":
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
