@@ -61,6 +61,31 @@ class DeviceBuffer:
         return N.DEV_BE if self.big_endian else N.DEV_F64
 
 
+def _bucket_table(buckets, lengths, p_first: int):
+    """(flat pointer list, k) of a batched call's bucket table: ``buckets[q]``
+    are the k device buckets of partition ``p_first + q``.  The C-ABI takes
+    bare pointers and reads L_p doubles from each (include/ipls_agg.h), so a
+    DeviceBuffer shorter than its partition is refused here, before any
+    launch could read past it.  Raw integer addresses are the caller's
+    contract; partitions out of range are left to the library's range check."""
+    n_parts = len(buckets)
+    k = len(buckets[0]) if n_parts else 0
+    flat = []
+    for q, row in enumerate(buckets):
+        if len(row) != k:
+            raise ValueError("every partition needs the same number of buckets")
+        p = p_first + q
+        need = lengths[p] if 0 <= p < len(lengths) else 0
+        for b in row:
+            if isinstance(b, DeviceBuffer):
+                if b.n < need:
+                    raise ValueError(f"partition {p} needs buckets of {need} doubles, a DeviceBuffer holds {b.n}")
+                flat.append(b.ptr)
+            else:
+                flat.append(int(b))
+    return flat, k
+
+
 def _host_operand(x, big_endian: bool):
     """(pointer, n_doubles, kind, keepalive) for a host operand."""
     if isinstance(x, (bytes, bytearray, memoryview)):
@@ -349,13 +374,7 @@ class Aggregator:
         """One launch over len(buckets) partitions; buckets[q] is the list of
         device pointers (ints or DeviceBuffers) for partition p_first+q."""
         n_parts = len(buckets)
-        k = len(buckets[0]) if n_parts else 0
-        flat = []
-        for row in buckets:
-            if len(row) != k:
-                raise ValueError("every partition needs the same number of buckets")
-            for b in row:
-                flat.append(b.ptr if isinstance(b, DeviceBuffer) else int(b))
+        flat, k = _bucket_table(buckets, self.lengths, p_first)
         arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
         kind = N.DEV_BE if big_endian else N.DEV_F64
         self._chk(self._lib.ipls_agg_reduce_batch(self._h, p_first, n_parts, arr, k, kind,
@@ -366,10 +385,14 @@ class Aggregator:
         """Batched fold into caller device buffers ``dsts[q]`` (one per
         partition); ``big_endian_out`` fuses the update_file byte pack."""
         n_parts = len(buckets)
-        k = len(buckets[0]) if n_parts else 0
-        flat = [b.ptr if isinstance(b, DeviceBuffer) else int(b) for row in buckets for b in row]
-        if len(flat) != n_parts * k or len(dsts) != n_parts:
+        if len(dsts) != n_parts:
             raise ValueError("need k buckets and one destination per partition")
+        flat, k = _bucket_table(buckets, self.lengths, p_first)
+        for q, d in enumerate(dsts):
+            p = p_first + q
+            if isinstance(d, DeviceBuffer) and 0 <= p < self.n_partitions and d.n < self.lengths[p]:
+                raise ValueError(f"partition {p} needs a destination of {self.lengths[p]} doubles, "
+                                 f"the DeviceBuffer holds {d.n}")
         arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
         darr = (ctypes.c_void_p * max(1, n_parts))(*[d.ptr if isinstance(d, DeviceBuffer) else int(d) for d in dsts])
         self._chk(self._lib.ipls_agg_reduce_batch_out(
@@ -384,16 +407,17 @@ class Aggregator:
         (IPLS.java:1159-1174).  Returns the averaged values of the partitions
         (host array, or ``out`` when a DeviceBuffer is given), or None."""
         n_parts = len(buckets)
-        k = len(buckets[0]) if n_parts else 0
-        flat = []
-        for row in buckets:
-            if len(row) != k:
-                raise ValueError("every partition needs the same number of buckets")
-            flat.extend(b.ptr if isinstance(b, DeviceBuffer) else int(b) for b in row)
+        flat, k = _bucket_table(buckets, self.lengths, p_first)
         arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
         kind = N.DEV_BE if big_endian else N.DEV_F64
         ap, ak, res = None, N.HOST_F64, None
         if isinstance(out, DeviceBuffer):
+            if n_parts and 0 <= p_first and p_first + n_parts <= self.n_partitions:
+                last = p_first + n_parts - 1
+                need = self.offsets[last] + self.lengths[last] - 1 - self.offsets[p_first]
+                if out.n < need:
+                    raise ValueError(f"the averages of partitions {p_first}..{last} need {need} doubles, "
+                                     f"the DeviceBuffer holds {out.n}")
             ap, ak, res = out.ptr, N.DEV_F64, out
         elif with_average:
             last = p_first + n_parts - 1
@@ -533,10 +557,7 @@ class Aggregator:
         folds buckets resident on its GPU into its partial sums (an aggregator
         of the partition other than its owner, IPLS.java:1402-1431)."""
         n_parts = len(buckets)
-        k = len(buckets[0]) if n_parts else 0
-        flat = [b.ptr if isinstance(b, DeviceBuffer) else int(b) for row in buckets for b in row]
-        if len(flat) != n_parts * k:
-            raise ValueError("every partition needs the same number of buckets")
+        flat, k = _bucket_table(buckets, self.lengths, p_first)
         arr = (ctypes.c_void_p * max(1, len(flat)))(*flat)
         self._chk(self._lib.ipls_agg_reduce_partial(self._h, slot, p_first, n_parts, arr, k,
                                                     N.DEV_BE if big_endian else N.DEV_F64, start_mode))

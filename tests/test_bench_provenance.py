@@ -90,3 +90,24 @@ def test_device_text_capacity_checks():
     with pytest.raises(ValueError):
         out(4096, 9, 10)
     assert out(4096, 10, 10) == (4096, 10)
+
+
+def test_bucket_table_size_checks():
+    """The batched calls' bucket tables carry bare pointers, and the kernels
+    read L_p doubles from each: a DeviceBuffer shorter than its partition is
+    refused before any call (raw addresses stay the caller's contract)."""
+    from ipls.aggregator import _bucket_table
+    import ipls
+    lengths = [100, 100, 97]
+    rows = [[ipls.DeviceBuffer(4096 * (q * 2 + k + 1), lengths[q]) for k in range(2)] for q in range(3)]
+    flat, k = _bucket_table(rows, lengths, 0)
+    assert k == 2 and flat == [4096 * i for i in range(1, 7)]
+    flat, k = _bucket_table([[1, 2], [3, ipls.DeviceBuffer(8, 97)]], lengths, 1)   # raw ints pass through
+    assert (flat, k) == ([1, 2, 3, 8], 2)
+    with pytest.raises(ValueError, match="partition 1 needs buckets of 100"):
+        _bucket_table([[ipls.DeviceBuffer(8, 99)]], lengths, 1)
+    with pytest.raises(ValueError, match="same number of buckets"):
+        _bucket_table([[1, 2], [3]], lengths, 0)
+    assert _bucket_table([], lengths, 0) == ([], 0)
+    # a partition out of range is the library's IPLS_E_RANGE, not a size error here
+    assert _bucket_table([[ipls.DeviceBuffer(8, 1)]], lengths, 5) == ([8], 1)

@@ -896,6 +896,12 @@ def test_aggregate_round_big_shape_device_out(ipls, O, shift):
     torch.cuda.synchronize()   # fills and the poison ran on the null stream; the handle's is non-blocking
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     agg.Update(O.synth_bucket(L, 3, 77), 3, from_clients=False)    # one partition with REP
+    # undersized operands are refused before any launch (bare pointers at the C-ABI)
+    with pytest.raises(ValueError, match="averages"):
+        agg.aggregate_round(0, rows, out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1) - 1))
+    with pytest.raises(ValueError, match="needs buckets"):
+        agg.aggregate_round(0, rows[:3] + [rows[3][:2] + [ipls.DeviceBuffer(rows[3][2].ptr, L - 1)]],
+                            out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1)))
     agg.aggregate_round(0, rows, out=ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, P * (L - 1)))
     torch.cuda.synchronize()
     full = out.cpu().numpy()
