@@ -22,6 +22,11 @@
 #ifndef IPLS_ROT
 #define IPLS_ROT 0
 #endif
+// IPLS_ROUND_PAIRS=1: the fused round's wave-pair tile layout (reduce_tiles);
+// the =0 build (the round-2 layout) is the A/B variant
+#ifndef IPLS_ROUND_PAIRS
+#define IPLS_ROUND_PAIRS 1
+#endif
 
 namespace ipls {
 
@@ -212,8 +217,21 @@ __device__ __forceinline__ void reduce_tiles(
 #else
     constexpr int rot = 0;
 #endif
+    // PAIRS (the fused round): a wave's vectors 2m and 2m+1 are adjacent 1 KiB
+    // pieces, so a wave owns 2 KiB contiguous per pair (the CU still sweeps one
+    // window of each bucket per two vectors), and an averages run at 8 mod 16
+    // needs single 8-B stores every 2 KiB instead of every 1 KiB (epilogue).
+    // Same elements, same fold: bit-identical; +0.3 to +0.8 points on config
+    // C's round in three processes (profiles/r03/an/pairs2_probe.jsonl).
+    constexpr bool PAIRS = FIN && IPLS_ROUND_PAIRS && (R % 2 == 0);
+    if constexpr (PAIRS) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)((r + rot) & (R - 1)) * kBlock + tid);
+      for (int r = 0; r < R; ++r)
+        off[r] = base + 2 * ((int64_t)(r >> 1) * 2 * kBlock + (tid >> 6) * 128 + (r & 1) * 64 + (tid & 63));
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) off[r] = base + 2 * ((int64_t)((r + rot) & (R - 1)) * kBlock + tid);
+    }
 
     // SEQ: one peer per step, each of its R vectors loaded, decoded and added
     // before the next is issued (a scheduling fence between them).  This is
@@ -302,6 +320,20 @@ __device__ __forceinline__ void reduce_tiles(
           if (avg_aligned) {
             if (e + 1 < L - 1) __builtin_nontemporal_store(encode2<false>(d2{ax, ay}), (gu2)(avg + e));
             else st8(avg + e, __builtin_bit_cast(unsigned long long, ax));
+          } else if constexpr (PAIRS) {
+            // piece r pairs its lane-63 y with piece r+1's lane-0 x (r even);
+            // piece r+1 directly follows piece r, so singles fall every 2 KiB
+            const int lane = tid & 63;
+            const double nx = __shfl_down(ax, 1);
+            if ((r & 1) == 0) {
+              const double nb = acc[r + 1].x + (rep && lane == 0 ? __builtin_bit_cast(double, ld8(rep + off[r + 1])) : 0.0);
+              const double b0 = __shfl(cnt == 0.0 ? nb : nb / den, 0);
+              if (lane == 0) st8(avg + e, __builtin_bit_cast(unsigned long long, ax));
+              __builtin_nontemporal_store(encode2<false>(d2{ay, lane < 63 ? nx : b0}), (gu2)(avg + e + 1));
+            } else {
+              if (lane < 63) __builtin_nontemporal_store(encode2<false>(d2{ay, nx}), (gu2)(avg + e + 1));
+              else if (e + 1 < L - 1) st8(avg + e + 1, __builtin_bit_cast(unsigned long long, ay));
+            }
           } else {
             // avg + e is 8 mod 16: lane t writes the aligned pair (e+1, e+2) =
             // (its y, lane t+1's x); the wave's first x and last y go alone.
