@@ -38,6 +38,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "aggregated-gradient GB/s (device-resident), 32 peers×4M doubles/partition"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 XGMI_LINK_GBS = 153.0       # one xGMI link, per direction (7 links per GPU)
+PCIE_GBS = 56.0             # PCIe Gen5 x16 per direction, measured (tools/h2d_bench.hip, profiles/r01/h2d_bench.txt)
 
 CONFIGS = {
     # name: (partitions per GPU, bucket length incl. count slot, peers)
@@ -89,6 +90,10 @@ def parse():
     ap.add_argument("--watchdog-selftest", action="store_true",
                     help="CPU only: run the N>1 watchdog over a gloo exchange that never completes "
                          "(tests/test_bench_watchdog.py); exits with Watchdog.EXIT_CODE")
+    ap.add_argument("--plumbing-selftest", action="store_true",
+                    help="CPU only: the N>1 launch plumbing over gloo (tests/test_bench_spawn.py)")
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1,
+                    help="with --plumbing-selftest: this rank exits with code 7 after joining the group")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearsal of the N>1 code on one GPU (ranks share cuda:0, partials "
                          "travel through host memory); numbers are not a measurement")
@@ -229,6 +234,89 @@ def host_inclusive(ipls, agg_cls, L: int, K: int, reps: int, device: int) -> dic
                       f"staged H2D) + finalize + D2H of the BE sum (into pinned memory, pageable for the pageable "
                       f"leg), algorithmic bytes (K+1)*L*8 per round, Python/ctypes caller",
             "pcie_ceiling": "~56 GB/s per direction measured (tools/h2d_bench.hip, profiles/r01/h2d_bench.txt)"}
+
+
+def f_stream_leg(ipls, torch, device: int, P: int = 16, L: int = 8388608, K: int = 64, ring: int = 16,
+                 lag: int = 4, producers: int = 8, verify: bool = True) -> dict:
+    """Config F end to end at F's own shape (BASELINE configs[4], one GPU's
+    slice): 16 partitions x 64 peers x 8,388,608 big-endian doubles start as
+    host IPFS bytes and every partition's BE sum ends in host memory.
+
+    The `ipfs cat` bytes of all 1,024 buckets (68.7 GB) sit in pageable host
+    memory -- the stand-in for the network.  They land, one arrival at a time,
+    in a bounded ring of `ring` pinned 64 MiB slots (direct ByteBuffers in
+    the Java drop-in), copied by `producers` host threads
+    the way a socket read fills the buffer.  Each landed slot is one
+    Updater._Update (ipls_agg_accumulate_async on pinned memory: the fold
+    reads the slot over PCIe, zero copy, Updater.java:115-117 after
+    GetParameters' BE decode, MyIPFSClass.java:444-455); a slot is refilled
+    once its fold's ticket completed (`lag` folds in flight).  After a
+    partition's 64 arrivals, AggregatePartition writes its update_file bytes
+    (BE sum, MyIPFSClass.java:105-116) to a pinned sum buffer.  Timed from the
+    first landing to the last sum in host memory; bytes = P*(K+1)*L*8."""
+    from concurrent.futures import ThreadPoolExecutor
+    nb = 8 * L
+    N = P * K
+    t_prep = time.perf_counter()
+    pool = torch.empty(N * nb, dtype=torch.uint8)           # pageable host bytes: every bucket's `ipfs cat`
+    tmp = torch.empty(nb, dtype=torch.uint8, device=torch.device("cuda", device))
+    for i in range(N):
+        ipls.synth_fill(ipls.DeviceBuffer(int(tmp.data_ptr()), L, big_endian=True), i // K, i % K, ipls.SEED)
+        pool[i * nb:(i + 1) * nb].copy_(tmp)
+    del tmp
+    pool_np = pool.numpy()
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, device=device)
+    slots = [ipls.PinnedBuffer(nb) for _ in range(ring)]
+    sums = [ipls.PinnedBuffer(nb) for _ in range(P)]
+    for b in slots + sums:                                  # fault the pinned pages in before timing
+        b.view()[::4096] = 0
+    prep_s = time.perf_counter() - t_prep
+    exe = ThreadPoolExecutor(producers)
+
+    def land(i):
+        np.copyto(slots[i % ring].view(), pool_np[i * nb:(i + 1) * nb])
+
+    fills = {i: exe.submit(land, i) for i in range(min(ring, N))}
+    tickets = {}
+    t0 = time.perf_counter()
+    for i in range(N):
+        p, k = divmod(i, K)
+        fills.pop(i).result()
+        tickets[i] = agg.UpdateAsync(slots[i % ring], p)
+        j = i - lag                                          # the oldest fold allowed to be still running
+        if j in tickets:
+            agg.Wait(tickets.pop(j))
+            if j + ring < N:
+                fills[j + ring] = exe.submit(land, j + ring)   # its slot is free again
+        if k == K - 1:
+            agg.AggregatePartition(p, sum_out=sums[p])        # waits for p's folds; BE sum -> pinned
+            for jj in sorted(tickets):                        # every earlier fold is done now
+                del tickets[jj]
+                if jj + ring < N:
+                    fills[jj + ring] = exe.submit(land, jj + ring)
+    dt = time.perf_counter() - t0
+    exe.shutdown()
+    nbytes = P * (K + 1) * L * 8
+    ok = None
+    if verify:
+        from oracle import oracle as O   # checker only
+        good = sum(int(ipls.checksum_dev(ipls.DeviceBuffer(sums[p].ptr, L, big_endian=True))
+                       == O.c_synth_sum_checksum(L, p, K)) for p in range(P))
+        ok = f"{good}/{P}"
+    agg.close()
+    for b in slots + sums:
+        b.close()
+    del pool, pool_np
+    return {"workload": f"{P} x {K} x {L // 1048576}M streamed: {P} partitions x {K} peers x {L} BE doubles from "
+                        f"host bytes through a ring of {ring} pinned slots, BE sums to pinned host memory",
+            "GBps": round(nbytes / dt / 1e9, 2), "seconds": round(dt, 3), "algorithmic_bytes": nbytes,
+            "frac_of_pcie": round(nbytes / dt / 1e9 / PCIE_GBS, 4), "pcie_ceiling_GBps": PCIE_GBS,
+            "peak_pinned_host_bytes": (ring + P) * nb, "host_source_bytes": N * nb,
+            "verified_partitions": ok, "prep_s": round(prep_s, 1),
+            "note": f"{producers} host threads land the bytes (a memcpy from pageable memory, as a socket read fills "
+                    f"a direct ByteBuffer); per arrival one ipls_agg_accumulate_async zero-copy fold over PCIe, "
+                    f"<= {lag + 1} folds in flight; per partition ipls_agg_finalize with the BE sum into pinned "
+                    f"memory; Python caller"}
 
 
 def e2e_multi(ipls, torch, dist, group, rank, world, local, L, K, reps, verify) -> dict:
@@ -1198,18 +1286,96 @@ def watchdog_selftest(args) -> None:
         print(json.dumps(out), flush=True)
 
 
+def spawn_ranks(n: int) -> int:
+    """`python3 bench.py --gpus N` with N > 1 and no launcher (WORLD_SIZE
+    unset): start the N rank processes here, one per GPU, the way torchrun
+    would -- each child is this same command with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT in its environment.  The parent
+    never touches the GPU (no torch import, no HIP call) and never execs: the
+    children are subprocesses, their stdout is this process's stdout (rank 0
+    prints the JSON line), and the parent exits with the worst child code.
+    A child that fails ends the others (by their own PIDs), so a run that lost
+    a rank is a failed run -- never a one-GPU line."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IPLS_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    first_bad = None
+    while any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            if first_bad is None and p.poll() not in (None, 0):
+                first_bad = r
+                print(f"bench.py: rank {r} exited with code {p.returncode}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop_all()
+        time.sleep(0.1)
+    for p in procs:
+        p.wait()
+    rcs = [p.returncode for p in procs]
+    if first_bad is not None:
+        rc = rcs[first_bad]
+        return rc if rc > 0 else 1           # killed by a signal: still a failure
+    return max((c if c >= 0 else 1) for c in rcs)
+
+
+def plumbing_selftest(args) -> None:
+    """CPU rehearsal of the N>1 launch plumbing (no GPU, tests/test_bench_spawn.py):
+    every rank joins a gloo group, records what the group saw, and rank 0 prints
+    the line with that record (`rccl`, the same keys as a GPU run's).
+    --selftest-fail-rank R makes rank R exit with code 7 right after joining,
+    the shape of a rank that found no GPU."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if rank == args.selftest_fail_rank:
+        os._exit(7)
+    me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
+          "spawned_by_bench": os.environ.get("IPLS_BENCH_SPAWNED") == "1"}
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "selftest": "plumbing",
+                          "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                                   "ranks": ranks}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not launched:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.watchdog_selftest:
         return watchdog_selftest(args)
+    if args.plumbing_selftest:
+        return plumbing_selftest(args)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if args.dist_backend == "nccl" and torch.cuda.device_count() < world:
+        # counted before any HIP call (device_count does not initialise the runtime on this image)
+        sys.exit(f"bench.py: {world} ranks need {world} GPUs, {torch.cuda.device_count()} visible")
     if not torch.cuda.is_available():
         sys.exit("bench.py needs an MI355X (no HIP device visible)")
     if args.dist_backend == "gloo":
@@ -1291,14 +1457,27 @@ def main():
     total_bytes = bytes_step * args.steps * world
     value = total_bytes / dt_max / 1e9
 
+    # every partition of the last timed launch against the oracle's checksum
+    # of its fixed-order sum; at N > 1 each rank checks its own block and rank
+    # 0 gathers the counts
     verified = None
-    if not args.no_verify and rank == 0:
+    ver_parts = None
+    if not args.no_verify:
         from oracle import oracle as O   # checker only: the oracle's checksum of the fixed-order sum
-        if args.be:
-            got = ipls.checksum_dev(ipls.DeviceBuffer(dsts[0], L, big_endian=True))
-        else:
-            got = agg.checksum(0)
-        verified = got == O.c_synth_sum_checksum(L, p0, K)
+        ok = 0
+        for q in range(P):
+            if args.be:
+                got = ipls.checksum_dev(ipls.DeviceBuffer(dsts[q], L, big_endian=True))
+            else:
+                got = agg.checksum(q)
+            ok += int(got == O.c_synth_sum_checksum(L, p0 + q, K))
+        counts = [(ok, P)]
+        if world > 1:
+            counts = [None] * world
+            dist.all_gather_object(counts, (ok, P), group=side_group)
+        good, total = sum(c[0] for c in counts), sum(c[1] for c in counts)
+        verified = good == total
+        ver_parts = f"{good}/{total}"
 
     # the rest of an aggregation round on the same handle (round_leg)
     round_info = None
@@ -1345,7 +1524,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_step,
                 "kernel_ms": round(kern_ms, 4),
             },
-            "verified_checksum_p0": verified,
+            "verified": verified,
+            "verified_partitions": ver_parts,
             "build": build,
         }
         if rccl is not None:
@@ -1379,8 +1559,9 @@ def main():
             if isinstance(out["other_configs"]["F"], dict) and not args.no_e2e:
                 # config F is the end-to-end case: its buckets start as host IPFS bytes
                 _, LF, KF = CONFIGS["F"]
-                out["other_configs"]["F"]["host_inclusive"] = side(host_inclusive, ipls, ipls.Aggregator, LF, KF, 2,
-                                                                   local)
+                # the whole slice streamed from host bytes through a bounded pinned ring
+                out["other_configs"]["F"]["host_inclusive"] = side(f_stream_leg, ipls, torch, local,
+                                                                   verify=not args.no_verify)
     if world == 1 and args.be_schedule_ab and out is not None:
         if "arena" in locals():
             del arena, rows
@@ -1432,7 +1613,7 @@ def main():
             torch.cuda.empty_cache()
             _, LF, KF = CONFIGS["F"]
             try:
-                el = e2e_multi(ipls, torch, dist, side_group, rank, world, local, LF // 4, KF, args.e2e_reps,
+                el = e2e_multi(ipls, torch, dist, side_group, rank, world, local, LF, KF, args.e2e_reps,
                                not args.no_verify)
             except Exception as e:                   # reported, never fatal to the main line
                 el = {"error": f"{type(e).__name__}: {e}"}

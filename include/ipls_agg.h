@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define IPLS_AGG_ABI_VERSION 2
+#define IPLS_AGG_ABI_VERSION 3
 
 /* ---- error codes (Java exception the reference would raise) ---- */
 #define IPLS_OK           0
@@ -203,17 +203,61 @@ int ipls_agg_set_coalesce(ipls_agg *h, int max_group);
  * owns the buffer (one per handle, like one Updater thread per peer). */
 int ipls_agg_update_indirect(ipls_agg *h, int p, int target, const void *bytes, int64_t n_bytes);
 
+/* ---- PeerData.Other_Replica_Gradients (PeerData.java:140-141) ----
+ * The downloads of OTHER aggregators' buckets of partition p, kept per key
+ * (p, aggregator) in a java.util.HashMap<Pair<Integer,String>, double[]>.
+ *
+ * The aggregator index contract.  The reference key is the aggregator's
+ * peer-ID String.  Here `aggregator` is any int32 the caller maps 1:1 from
+ * that String (e.g. its index in the Java side's table of known peers, or an
+ * interned ID): two keys are the same key exactly when (p, aggregator) are
+ * equal.  `key_hash` is the reference key's hashCode,
+ *     new org.javatuples.Pair<>(p, peerId).hashCode()
+ * (Java computes it directly; ipls_java_pair_hash computes it from the ID's
+ * UTF-8 bytes).  It fixes where the key sits in the HashMap, and so the order
+ * in which Collect_Replicas folds the stored arrays: floating-point addition
+ * does not associate, so that order decides the bits of REP[p] once a
+ * partition has two or more stored arrays.  ipls_agg_other_replica (no hash)
+ * takes the peer ID to be Integer.toString(aggregator). */
+
+/* new Pair<Integer,String>(p, id).hashCode() (javatuples 1.2, pom.xml:66-68) of a
+ * peer ID given as UTF-8 bytes: 31 + 31*(31 + p) + id.hashCode() in wrapping
+ * int32 arithmetic, String.hashCode over the ID's UTF-16 units.  IPLS_E_FORMAT
+ * for malformed UTF-8.  No handle, no GPU. */
+int ipls_java_pair_hash(int32_t p, const uint8_t *id, int64_t len, int32_t *hash);
+
 /* Download_Scheduler.download_gradients, a bucket of ANOTHER aggregator of
  * partition p (Download_Scheduler.java:245-268): kept per (p, aggregator) in
  * Other_Replica_Gradients -- the first download becomes the stored array
- * (its own length n, -0.0 kept), later ones fold into it for j < n.  A later
- * download longer than the stored array returns IPLS_E_RANGE, nothing folded. */
+ * (its own length n, -0.0 kept) and the key is put into the map model with
+ * key_hash; later ones fold into it for j < n and leave its position as it
+ * is (a later call with another key_hash for a stored key: IPLS_E_INVAL).  A
+ * later download longer than the stored array returns IPLS_E_RANGE, nothing
+ * folded.  Other_Replica_Gradients_Received counts the downloads. */
+int ipls_agg_other_replica_keyed(ipls_agg *h, int p, int32_t aggregator, int32_t key_hash, const void *src,
+                                 int64_t n, int src_kind);
+/* The same with the peer ID Integer.toString(aggregator). */
 int ipls_agg_other_replica(ipls_agg *h, int p, int32_t aggregator, const void *src, int64_t n,
                            int src_kind);
 
+/* Other_Replica_Gradients.remove(new Pair<>(p, aggregator)) and the same
+ * remove on Other_Replica_Gradients_Received: the stored array and its
+ * download count are discarded (the HashMap keeps its capacity).  Returns 1
+ * if the key was stored, 0 if not (no-op).  The reference removes the key when
+ * that aggregator's own partial sum has arrived, so its downloaded buckets
+ * are not counted twice: Download_Scheduler.java:215-217 (already in
+ * Received_Replicas), :329-332 and :438-440 (its partial-update file
+ * downloaded).  GlobalGradientPool.java:90-93 builds its key from the
+ * frame's List<String> of origins, which never equals a stored
+ * Pair<Integer,String>: that remove is a no-op in the reference
+ * (INTEGRATION.md §2). */
+int ipls_agg_other_replica_drop(ipls_agg *h, int p, int32_t aggregator);
+
 /* Collect_Replicas (IPLS.java:1217-1241): REP[p][j] = REP[p][j] + Other[(p,a)][j]
- * for every stored (p, a), in ascending (p, a) order (the reference iterates a
- * HashMap; this is the canonical order), then clears the store.
+ * for every stored key, in the order of new ArrayList<>(keySet()) of the JDK
+ * HashMap (ascending bin of the key hashes under the map's capacity, then
+ * insertion order within a bin), then clears the store
+ * (Other_Replica_Gradients = new HashMap<>(): capacity reset).
  * participants (nullable, P ints) receives the per-partition download counts
  * (PeerData.Participants).  Returns the number of stored arrays folded, or
  * IPLS_E_RANGE (nothing folded) if one is longer than its partition. */
@@ -372,12 +416,22 @@ int ipls_agg_reduce_partial(ipls_agg *h, int slot, int p_first, int n_parts, con
  * partials, so an owner reads over all its links at once); the partials are
  * then logically +0.0 again.  Returns the number of partials folded.
  * A pair of devices without peer access is not an error: such a partial is
- * first copied into an owner-side buffer (hipMemcpyPeerAsync on the owner's
- * stream) and the same fold reads that copy, in the same slot order, so the
- * result is bit-identical.  Setting IPLS_PEER_STAGED=1 in the environment
- * before ipls_agg_open forces this path for every cross-shard read (the
- * combine and the Gradient_Buff of ipls_agg_update_indirect) -- a test
- * switch; ipls_launch_info.staged counts the staged partials. */
+ * first copied into an owner-side buffer (hipMemcpyPeerAsync on the SLOT's
+ * stream, after the slot's folds, so copies from different GPUs run at once;
+ * the partial's `ready` event is then re-recorded on that stream and the
+ * owner waits on it) and the same fold reads that copy, in the same slot
+ * order, so the result is bit-identical.  Memory: each such owner-side
+ * buffer is L_p doubles per (slot, partition) pair that was ever staged,
+ * allocated on the owner at the first staged combine and kept until
+ * ipls_agg_close -- up to (G-1) extra copies of every partition an owner
+ * holds on a node without peer access; it is not reserved at open, so an
+ * out-of-memory shows up as IPLS_E_NOMEM from this call.  Setting
+ * IPLS_PEER_STAGED=1 in the environment before ipls_agg_open forces this
+ * path for every cross-shard read (the combine and the Gradient_Buff of
+ * ipls_agg_update_indirect) -- a test switch; ipls_launch_info.staged counts
+ * the staged partials.  The staged path has run only with shards sharing one
+ * GPU (a copy within one device); between two distinct GPUs it is unmeasured
+ * on hardware. */
 int ipls_agg_combine_partials(ipls_agg *h, int p_first, int n_parts);
 
 /* ---- publish-side codec (a9) ----

@@ -139,7 +139,7 @@ struct ipls_dev {
   unsigned long long* d_merge = nullptr;  // storage-merge accumulator, grown on demand
   int64_t merge_cap = 0;
   // PeerData.Other_Replica_Gradients / _Received, keyed (partition, aggregator);
-  // std::map order = the canonical (ascending) Collect_Replicas order
+  // Collect_Replicas folds them in the order the front's HashMap model gives
   struct OtherRep {
     unsigned long long* d = nullptr;
     int64_t n = 0;
@@ -1625,10 +1625,41 @@ int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, i
   return IPLS_OK;
 }
 
-int dev_collect_replicas(ipls_dev* h, int32_t* participants) {
+int dev_other_replica_drop(ipls_dev* h, int p, int32_t aggregator) {
+  if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
+  IPLS_LOCK(h);
+  if (int rc = check_part(h, p)) return rc;
+  auto it = h->other.find(std::make_pair(p, aggregator));
+  if (it == h->other.end()) return 0;   // containsKey false: nothing to remove
+  // Other_Replica_Gradients.remove(key) + Other_Replica_Gradients_Received.remove(key)
+  // (Download_Scheduler.java:215-217, 329-332, 438-440).  Folds into the array
+  // may still be queued on the stream: free it only after them.
+  HIP_TRY(h, dev_use(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  hipFree(it->second.d);
+  h->other.erase(it);
+  return 1;
+}
+
+int dev_collect_replicas(ipls_dev* h, int32_t* participants, const int32_t* order, int n_order) {
   if (!h) return fail(nullptr, IPLS_E_INVAL, "null handle");
   IPLS_LOCK(h);
   HIP_TRY(h, dev_use(h->device));
+  // the fold order: `new ArrayList<>(Other_Replica_Gradients.keySet())`
+  // (IPLS.java:1218), given by the front's model of the JDK HashMap
+  // (java_hashmap.hpp) as engine-local (p, aggregator) pairs -- every stored
+  // key exactly once
+  if (n_order != (int)h->other.size() || (n_order > 0 && !order))
+    return fail(h, IPLS_E_INVAL, "collect order lists %d keys, the store holds %zu", n_order, h->other.size());
+  std::vector<std::map<std::pair<int, int32_t>, ipls_dev::OtherRep>::iterator> seq;
+  seq.reserve(n_order);
+  for (int i = 0; i < n_order; ++i) {
+    auto it = h->other.find(std::make_pair((int)order[2 * i], order[2 * i + 1]));
+    if (it == h->other.end() || std::find(seq.begin(), seq.end(), it) != seq.end())
+      return fail(h, IPLS_E_INVAL, "collect order key (%d, %d) is not a stored key", order[2 * i] + h->p_lo,
+                  order[2 * i + 1]);
+    seq.push_back(it);
+  }
   // REP[p] is a double[L_p]: a longer stored array overruns it (IPLS.java:1225).
   for (auto& kv : h->other)
     if (kv.second.n > h->len[kv.first.first])
@@ -1638,15 +1669,15 @@ int dev_collect_replicas(ipls_dev* h, int32_t* participants) {
   if (participants)
     for (int q = 0; q < h->P; ++q) participants[q] = 0;
   int folded = 0;
-  for (auto& kv : h->other) {   // IPLS.java:1222-1234: REP[p][j] = REP[p][j] + Other[j], j < Other.length
-    const int p = kv.first.first;
-    const int64_t n = kv.second.n;
-    if (participants) participants[p] += kv.second.received;   // PeerData.Participants (:1228-1233)
+  for (auto& it : seq) {   // IPLS.java:1222-1234: REP[p][j] = REP[p][j] + Other[j], j < Other.length
+    const int p = it->first.first;
+    const int64_t n = it->second.n;
+    if (participants) participants[p] += it->second.received;   // PeerData.Participants (:1228-1233)
     if (n > 0) {
       if (int rc = materialize(h, p, IPLS_TGT_REP)) return rc;
       hipLaunchKernelGGL((k_fold_n<false, false>), dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)),
                          dim3(kBlock), 0, h->stream, (unsigned long long*)(h->arena + h->rep_off[p]),
-                         kv.second.d, n);
+                         it->second.d, n);
       HIP_TRY(h, hipGetLastError());
     }
     ++folded;

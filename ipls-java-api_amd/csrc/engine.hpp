@@ -49,7 +49,9 @@ int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64
 int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** gbuf, int64_t* glen);
 int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind);
 int dev_other_check(ipls_dev* h);
-int dev_collect_replicas(ipls_dev* h, int32_t* participants);
+int dev_other_replica_drop(ipls_dev* h, int p, int32_t aggregator);
+// order: n_order engine-local (p, aggregator) pairs, every stored key once
+int dev_collect_replicas(ipls_dev* h, int32_t* participants, const int32_t* order, int n_order);
 int dev_reduce_batch(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                      int start_mode, int target);
 int dev_reduce_batch_out(ipls_dev* h, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,

@@ -42,6 +42,7 @@
 
 #include "../../include/ipls_agg.h"
 #include "engine.hpp"
+#include "java_hashmap.hpp"
 #include "pubsub_host.hpp"
 
 namespace {
@@ -65,22 +66,17 @@ struct Partial {
 class ShardPool {
  public:
   explicit ShardPool(int n) : w_(n) {
-    for (int s = 1; s < n; ++s) {
-      w_[s] = std::make_unique<W>();
-      w_[s]->th = std::thread([w = w_[s].get()] { run(w); });
+    try {
+      for (int s = 1; s < n; ++s) {
+        w_[s] = std::make_unique<W>();
+        w_[s]->th = std::thread([w = w_[s].get()] { run(w); });
+      }
+    } catch (...) {   // a later thread could not start: end the ones already running, then report
+      stop_all();
+      throw;
     }
   }
-  ~ShardPool() {
-    for (auto& w : w_)
-      if (w) {
-        {
-          std::lock_guard<std::mutex> lk(w->m);
-          w->stop = true;
-        }
-        w->cv.notify_one();
-        w->th.join();
-      }
-  }
+  ~ShardPool() { stop_all(); }
   void post(int s, std::function<void()> fn) {
     W* w = w_[s].get();
     {
@@ -98,6 +94,17 @@ class ShardPool {
     std::deque<std::function<void()>> q;
     bool stop = false;
   };
+  void stop_all() noexcept {
+    for (auto& w : w_)
+      if (w && w->th.joinable()) {
+        {
+          std::lock_guard<std::mutex> lk(w->m);
+          w->stop = true;
+        }
+        w->cv.notify_one();
+        w->th.join();
+      }
+  }
   static void run(W* w) {
     for (;;) {
       std::function<void()> fn;
@@ -143,6 +150,13 @@ struct ipls_agg {
   uint64_t ticket_next = 1;
   std::vector<std::deque<std::pair<uint64_t, uint64_t>>> tickets;
   std::vector<std::vector<Partial>> part;   // [slot][p]
+  // PeerData.Other_Replica_Gradients' key set as the JDK HashMap holds it (one
+  // map for the whole peer, PeerData.java:140): which (p, aggregator) keys are
+  // stored, their Pair hashCodes, insertion order and the table capacity --
+  // the order Collect_Replicas folds them in (java_hashmap.hpp).  The arrays
+  // themselves live on the partitions' shards.
+  std::mutex rep_mu;
+  ipls::JavaHashOrder rep_order;
 
   int S() const { return (int)sh.size(); }
 };
@@ -644,31 +658,87 @@ int ipls_agg_update_indirect(ipls_agg* H, int p, int target, const void* bytes, 
   return rc;
 }
 
-int ipls_agg_other_replica(ipls_agg* H, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
+int ipls_java_pair_hash(int32_t p, const uint8_t* id, int64_t len, int32_t* hash) {
+  if (!hash || len < 0 || (len > 0 && !id)) return ferr(nullptr, IPLS_E_INVAL, "bad peer-ID bytes");
+  int32_t sh;
+  if (!ipls::java_string_hash(id, len, &sh)) return ferr(nullptr, IPLS_E_FORMAT, "peer ID is not valid UTF-8");
+  *hash = ipls::java_pair_hash_of(p, sh);
+  return IPLS_OK;
+}
+
+int ipls_agg_other_replica_keyed(ipls_agg* H, int p, int32_t aggregator, int32_t key_hash, const void* src,
+                                 int64_t n, int src_kind) {
   KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
   if (!part_ok(H, p)) return range_err(H, p);
   int q;
   const int s = route(H, p, &q);
-  return fwd(H, s, dev_other_replica(H->sh[s], q, aggregator, src, n, src_kind));
+  std::lock_guard<std::mutex> lk(H->rep_mu);
+  const ipls::JavaHashOrder::Key key{p, aggregator};
+  int32_t h0 = 0;
+  const bool had = H->rep_order.hash_of(key, &h0);
+  if (had && h0 != key_hash)
+    return ferr(H, IPLS_E_INVAL, "key hash %d of (%d, %d) differs from the one it was stored with (%d)", key_hash, p,
+                aggregator, h0);
+  if (int rc = fwd(H, s, dev_other_replica(H->sh[s], q, aggregator, src, n, src_kind))) return rc;
+  if (!had) H->rep_order.put_new(key, key_hash);   // Other_Replica_Gradients.put (Download_Scheduler.java:266)
+  return IPLS_OK;
+}
+
+int ipls_agg_other_replica(ipls_agg* H, int p, int32_t aggregator, const void* src, int64_t n, int src_kind) {
+  // the aggregator's ID is taken to be Integer.toString(aggregator)
+  return ipls_agg_other_replica_keyed(H, p, aggregator, ipls::java_pair_hash_of(p, ipls::java_index_id_hash(aggregator)),
+                                      src, n, src_kind);
+}
+
+int ipls_agg_other_replica_drop(ipls_agg* H, int p, int32_t aggregator) {
+  KeepDevice keep_device;
+  if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
+  if (!part_ok(H, p)) return range_err(H, p);
+  int q;
+  const int s = route(H, p, &q);
+  std::lock_guard<std::mutex> lk(H->rep_mu);
+  const int rc = fwd(H, s, dev_other_replica_drop(H->sh[s], q, aggregator));
+  if (rc > 0) H->rep_order.remove({p, aggregator});
+  return rc;
 }
 
 int ipls_agg_collect_replicas(ipls_agg* H, int32_t* participants) {
   KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
-  if (H->S() == 1) return fwd(H, 0, dev_collect_replicas(H->sh[0], participants));
+  std::lock_guard<std::mutex> lk(H->rep_mu);
+  // new ArrayList<>(Other_Replica_Gradients.keySet()) (IPLS.java:1218), cut
+  // per shard as engine-local (p, aggregator) pairs in that order (only the
+  // order within a partition changes a result; partitions live on one shard)
+  std::vector<std::vector<int32_t>> per(H->S());
+  for (const auto& k : H->rep_order.order()) {
+    const int s = H->owner[k.first];
+    per[s].push_back(k.first - H->lo[s]);
+    per[s].push_back(k.second);
+  }
+  if (H->S() == 1) {
+    const int rc = fwd(H, 0, dev_collect_replicas(H->sh[0], participants, per[0].data(), (int)per[0].size() / 2));
+    if (rc >= 0) H->rep_order.clear();   // Other_Replica_Gradients = new HashMap<>() (:1238)
+    return rc;
+  }
   const std::vector<int> ss = nonempty_shards(H);
   for (int s : ss)   // the length rule over every shard before anything is folded
     if (int rc = fwd(H, s, dev_other_check(H->sh[s]))) return rc;
   std::vector<std::vector<int32_t>> cnt(H->S());
-  std::vector<int> folded(H->S(), 0);
+  std::vector<int> folded(H->S(), -1);
   const int rc = par_shards(H, ss, [&](int s) {
     cnt[s].assign(H->lo[s + 1] - H->lo[s], 0);
-    const int r = dev_collect_replicas(H->sh[s], participants ? cnt[s].data() : nullptr);
+    const int r = dev_collect_replicas(H->sh[s], participants ? cnt[s].data() : nullptr, per[s].data(),
+                                       (int)per[s].size() / 2);
     if (r >= 0) folded[s] = r;
     return r;
   });
-  if (rc < 0) return rc;
+  if (rc < 0) {   // the shards that did collect cleared their stores: so does the model, for their keys
+    for (const auto& k : H->rep_order.order())
+      if (folded[H->owner[k.first]] >= 0) H->rep_order.remove(k);
+    return rc;
+  }
+  H->rep_order.clear();
   int total = 0;
   for (int s : ss) {
     total += folded[s];

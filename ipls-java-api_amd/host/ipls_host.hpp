@@ -227,10 +227,26 @@ class IPLS {
 
   // Download_Scheduler.download_gradients (:245-268): a bucket another
   // aggregator of Partition will fold, kept in Other_Replica_Gradients.
-  void Other_Replica_Gradients(int Partition, int32_t Aggregator, const std::vector<double>& gradients) {
-    check(ipls_agg_other_replica(h_.get(), Partition, Aggregator, gradients.data(), (int64_t)gradients.size(),
-                                 IPLS_HOST_F64),
+  // Aggregator is the int the caller maps 1:1 from the aggregator's peer ID;
+  // AggregatorId is that ID, whose Pair<>(Partition, AggregatorId).hashCode()
+  // fixes the key's place in the HashMap and so the Collect_Replicas order
+  // (IPLS.java:1218).
+  void Other_Replica_Gradients(int Partition, int32_t Aggregator, const std::string& AggregatorId,
+                               const std::vector<double>& gradients) {
+    int32_t key_hash = 0;
+    check(ipls_java_pair_hash(Partition, (const uint8_t*)AggregatorId.data(), (int64_t)AggregatorId.size(),
+                              &key_hash),
+          nullptr);
+    check(ipls_agg_other_replica_keyed(h_.get(), Partition, Aggregator, key_hash, gradients.data(),
+                                       (int64_t)gradients.size(), IPLS_HOST_F64),
           h_.get());
+  }
+
+  // Other_Replica_Gradients.remove(new Pair<>(Partition, Aggregator)) and the
+  // _Received count (Download_Scheduler.java:215-217, 329-332, 438-440): the
+  // aggregator's own partial arrived.  True if the key was stored.
+  bool Other_Replica_Gradients_remove(int Partition, int32_t Aggregator) {
+    return check(ipls_agg_other_replica_drop(h_.get(), Partition, Aggregator), h_.get()) == 1;
   }
 
   // Collect_Replicas (IPLS.java:1217-1241): fold every stored array into

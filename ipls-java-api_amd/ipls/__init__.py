@@ -12,8 +12,8 @@ from ._native import (  # noqa: F401
     IplsError, build_info, lib,
 )
 from .aggregator import (  # noqa: F401
-    Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, encode_secure, frame_encode, frame_parse, pair_encode,
-    pair_parse, shard_plan, synth_fill,
+    Aggregator, DeviceBuffer, PinnedBuffer, checksum_dev, encode_secure, frame_encode, frame_parse, java_pair_hash,
+    pair_encode, pair_parse, shard_plan, synth_fill,
 )
 
 SEED = 0x1B5_2026  # synthetic workload seed

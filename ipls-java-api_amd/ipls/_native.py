@@ -25,7 +25,7 @@ HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON, HOST_PAIR = 0, 1,
 HOST_TEXT, DEV_TEXT = 7, 8
 KERNEL_REDUCE, KERNEL_ROUND, KERNEL_FOLD1, KERNEL_REDUCE_SCALAR = 1, 2, 3, 4
 SHAPE_BIG, SHAPE_MID, SHAPE_SMALL, SHAPE_HALF = 1, 2, 3, 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1
 
@@ -100,6 +100,9 @@ SIGNATURES = {
     "ipls_agg_set_coalesce": (_i, [_vp, _i]),
     "ipls_agg_flush": (_i, [_vp]),
     "ipls_agg_other_replica": (_i, [_vp, _i, _i32, _vp, _i64, _i]),
+    "ipls_agg_other_replica_keyed": (_i, [_vp, _i, _i32, _i32, _vp, _i64, _i]),
+    "ipls_agg_other_replica_drop": (_i, [_vp, _i, _i32]),
+    "ipls_java_pair_hash": (_i, [_i32, _vp, _i64, _P(_i32)]),
     "ipls_agg_collect_replicas": (_i, [_vp, _P(_i32)]),
     "ipls_agg_ingest_pubsub": (_i, [_vp, _i, _P(_vp), _P(_i64), _i, _i, _P(_i32), _P(_i32)]),
     "ipls_agg_blend": (_i, [_vp, _i, _i, _vp, _i64, _i, ctypes.c_double, ctypes.c_double]),

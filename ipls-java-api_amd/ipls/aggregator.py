@@ -353,17 +353,31 @@ class Aggregator:
         """Aggregated = 0.25*Weights before the async publish (Updater.java:197-199)."""
         self._chk(self._lib.ipls_agg_scale(self._h, partition, N.TGT_AGG, N.TGT_WEIGHTS, 0.25))
 
-    def OtherReplicaGradients(self, partition: int, aggregator: int, gradients):
+    def OtherReplicaGradients(self, partition: int, aggregator: int, gradients, *, key_hash: int | None = None):
         """Download_Scheduler.download_gradients (Download_Scheduler.java:245-268):
-        a bucket that another aggregator of ``partition`` (an integer id) will
-        also fold.  The first one becomes Other_Replica_Gradients[(p, a)], later
-        ones fold into it."""
+        a bucket that another aggregator of ``partition`` will also fold.  The
+        first one becomes Other_Replica_Gradients[(p, a)], later ones fold into
+        it.  ``aggregator`` is the int the caller maps 1:1 from the aggregator's
+        peer-ID String; ``key_hash`` is ``new Pair<>(p, peerId).hashCode()``
+        (java_pair_hash), which places the key in the HashMap and so fixes the
+        Collect_Replicas order.  Without it the peer ID is str(aggregator)."""
         ptr, n, kind, keep = _operand(gradients)
-        self._chk(self._lib.ipls_agg_other_replica(self._h, partition, aggregator, ptr, n, kind))
+        if key_hash is None:
+            self._chk(self._lib.ipls_agg_other_replica(self._h, partition, aggregator, ptr, n, kind))
+        else:
+            self._chk(self._lib.ipls_agg_other_replica_keyed(self._h, partition, aggregator,
+                                                             ctypes.c_int32(key_hash).value, ptr, n, kind))
+
+    def OtherReplicaDrop(self, partition: int, aggregator: int) -> bool:
+        """Other_Replica_Gradients.remove(new Pair<>(p, a)) with its received
+        count (Download_Scheduler.java:215-217, 329-332, 438-440): that
+        aggregator's own partial arrived, so its downloaded buckets are not
+        collected.  True if the key was stored."""
+        return self._chk(self._lib.ipls_agg_other_replica_drop(self._h, partition, aggregator)) == 1
 
     def Collect_Replicas(self):
         """IPLS.java:1217-1241: fold every stored Other_Replica_Gradients array
-        into REP (ascending (partition, aggregator) order) and clear the store.
+        into REP in the JDK HashMap's key-set order and clear the store.
         Returns (arrays folded, per-partition download counts = Participants)."""
         part = (ctypes.c_int32 * max(1, self.n_partitions))()
         k = self._chk(self._lib.ipls_agg_collect_replicas(self._h, part))
@@ -712,6 +726,17 @@ def shard_plan(n_partitions: int, n_shards: int) -> list[int]:
     out = (ctypes.c_int32 * max(1, n_partitions))()
     N.check(N.lib().ipls_shard_plan(n_partitions, n_shards, out))
     return list(out)[:n_partitions]
+
+
+def java_pair_hash(p: int, peer_id: str) -> int:
+    """new org.javatuples.Pair<Integer,String>(p, peer_id).hashCode() (the key
+    hash of Other_Replica_Gradients, PeerData.java:140), computed by the
+    library from the ID's UTF-8 bytes."""
+    b = peer_id.encode("utf-8")
+    buf = (ctypes.c_uint8 * max(1, len(b))).from_buffer_copy(b or b"\0")
+    out = ctypes.c_int32()
+    N.check(N.lib().ipls_java_pair_hash(p, ctypes.addressof(buf), len(b), ctypes.byref(out)))
+    return out.value
 
 
 def synth_fill(buf: DeviceBuffer, p: int, k: int, seed: int, stream: int = 0):

@@ -10,6 +10,8 @@
 
 import java.nio.ByteBuffer;
 
+import org.javatuples.Pair;
+
 public final class NativeAggregator implements AutoCloseable {
     static { System.loadLibrary("ipls_jni"); }   // links libipls_agg.so
 
@@ -101,9 +103,23 @@ public final class NativeAggregator implements AutoCloseable {
     }
 
     /** Download_Scheduler.download_gradients (:254-266): another aggregator's
-     *  bucket for partition p, kept per (p, aggregator) until collectReplicas(). */
-    public void otherReplica(int p, int aggregator, ByteBuffer catBytes) {
-        otherReplicaDirect(handle, p, aggregator, catBytes, catBytes.position(), catBytes.remaining() / 8);
+     *  bucket for partition p, kept per (p, aggregator) until collectReplicas().
+     *  aggregator: an int mapped 1:1 from the aggregator's peer-ID String (e.g.
+     *  its index in a peer table); aggregatorId: that String, whose
+     *  new Pair<>(p, aggregatorId).hashCode() places the key in the native
+     *  model of the HashMap Other_Replica_Gradients (PeerData.java:140) and so
+     *  fixes the Collect_Replicas fold order (IPLS.java:1218). */
+    public void otherReplica(int p, int aggregator, String aggregatorId, ByteBuffer catBytes) {
+        otherReplicaDirect(handle, p, aggregator, new Pair<Integer, String>(p, aggregatorId).hashCode(), catBytes,
+                           catBytes.position(), catBytes.remaining() / 8);
+    }
+
+    /** Other_Replica_Gradients.remove(new Pair<>(p, aggregatorId)) together with
+     *  Other_Replica_Gradients_Received.remove: that aggregator's partial sum
+     *  arrived (Download_Scheduler.java:215-217, 329-332, 438-440).  Returns
+     *  whether the key was stored. */
+    public boolean dropOtherReplica(int p, int aggregator) {
+        return otherReplicaDrop(handle, p, aggregator);
     }
 
     /** IPLS.Collect_Replicas (IPLS.java:1217-1241); returns Participants per partition. */
@@ -279,7 +295,9 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void commitPartial(long h, int p, int workers, byte[] out);
     private static native void accumulatePair(long h, int p, int target, byte[] file);
     private static native byte[] mergeFiles(long h, byte[][] files, boolean partialUpdates);
-    private static native void otherReplicaDirect(long h, int p, int aggregator, ByteBuffer buf, int pos, long n);
+    private static native void otherReplicaDirect(long h, int p, int aggregator, int keyHash, ByteBuffer buf, int pos,
+                                                  long n);
+    private static native boolean otherReplicaDrop(long h, int p, int aggregator);
     private static native int collectReplicas(long h, int[] participants);
     private static native void getPartitionsWire(long h, ByteBuffer direct, int pos, long nBytes);
     private static native ByteBuffer hostAllocDirect(int bytes);

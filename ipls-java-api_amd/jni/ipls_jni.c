@@ -380,11 +380,21 @@ JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_otherReplicaDirect(JNIEnv *env, jclass c, jlong h, jint p, jint a,
-                                                                  jobject buf, jint pos, jlong n) {
+                                                                  jint keyHash, jobject buf, jint pos, jlong n) {
     (void)c;
     void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
-    CHECK(ipls_agg_other_replica(H(h), p, a, src, n, IPLS_HOST_BE), H(h));
+    CHECK(ipls_agg_other_replica_keyed(H(h), p, a, keyHash, src, n, IPLS_HOST_BE), H(h));
+}
+
+JNIEXPORT jboolean JNICALL Java_NativeAggregator_otherReplicaDrop(JNIEnv *env, jclass c, jlong h, jint p, jint a) {
+    (void)c;
+    const int rc = ipls_agg_other_replica_drop(H(h), p, a);
+    if (rc < 0) {
+        throw_for(env, rc, H(h));
+        return JNI_FALSE;
+    }
+    return rc == 1 ? JNI_TRUE : JNI_FALSE;
 }
 
 JNIEXPORT jint JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass c, jlong h, jintArray out) {

@@ -126,33 +126,187 @@ def gradient_buff_len(model_size: int, n_partitions: int) -> int:
     return int(np.int32(np.int64(model_size).astype(np.int32) // np.int32(n_partitions))) + 2
 
 
-def other_replica_add(store: dict, partition: int, aggregator, g: np.ndarray) -> None:
+def _i32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+def java_string_hash(s: str) -> int:
+    """java.lang.String.hashCode(): s[0]*31^(n-1) + ... + s[n-1] over the
+    UTF-16 code units, wrapping int32 arithmetic (the JDK's published rule)."""
+    h = 0
+    units = s.encode("utf-16-be")
+    for i in range(0, len(units), 2):
+        h = (31 * h + ((units[i] << 8) | units[i + 1])) & 0xFFFFFFFF
+    return _i32(h)
+
+
+def java_pair_hash(p: int, peer_id: str) -> int:
+    """new org.javatuples.Pair<Integer,String>(p, peer_id).hashCode(): javatuples
+    1.2 (pom.xml:66-68) Tuple.hashCode = 31 * 1 + valueList.hashCode(), with
+    valueList = Arrays.asList(p, peer_id) and List.hashCode = fold of
+    31 * h + e.hashCode() from 1; Integer.hashCode(p) = p."""
+    lst = 1
+    for e in (p & 0xFFFFFFFF, java_string_hash(peer_id) & 0xFFFFFFFF):
+        lst = (31 * lst + e) & 0xFFFFFFFF
+    return _i32(31 * 1 + lst)
+
+
+class JavaHashMap:
+    """java.util.HashMap's table as JDK 8 keeps it (the pom compiles for 1.8,
+    pom.xml:118-122), restated from the published source: an array of bins,
+    each a chain in link order; hash = h ^ (h >>> 16), bin = hash & (n - 1);
+    the table is made with 16 bins at the first put after construction and
+    doubled (resize) when ++size > 0.75 n, or when a put makes a chain 9 long
+    while n < 64 (treeifyBin); a resize splits every chain into its lo
+    (hash & oldCap == 0) and hi halves, each in chain order, at j and
+    j + oldCap; a new key is appended at its chain's tail; remove unlinks;
+    iteration walks the bins in index order and each chain in link order.
+    A chain that reaches 9 at n >= 64 becomes a red-black tree (TreeNode
+    order); that case is flagged (``tree_bin``), not restated.
+
+    This simulates the table itself, independently of the library's model
+    (java_hashmap.hpp orders keys by (bin, insertion)), so the two check each
+    other."""
+
+    def __init__(self):
+        self.table = None          # list of chains: [[key, hash, value], ...]
+        self.size = 0
+        self.threshold = 0
+        self.tree_bin = False
+
+    @staticmethod
+    def spread(h: int) -> int:
+        h &= 0xFFFFFFFF
+        return h ^ (h >> 16)
+
+    def _resize(self):
+        old = self.table
+        if old is None:
+            self.table = [[] for _ in range(16)]
+            self.threshold = 12
+            return
+        n = len(old)
+        new = [[] for _ in range(2 * n)]
+        for j, chain in enumerate(old):
+            new[j] = [e for e in chain if self.spread(e[1]) & n == 0]
+            new[j + n] = [e for e in chain if self.spread(e[1]) & n != 0]
+        self.table = new
+        self.threshold *= 2
+
+    def _find(self, key, h):
+        if self.table is None:
+            return None
+        for e in self.table[self.spread(h) & (len(self.table) - 1)]:
+            if e[1] == h and e[0] == key:
+                return e
+        return None
+
+    def put(self, key, h: int, value) -> None:
+        if self.table is None:
+            self._resize()
+        e = self._find(key, h)
+        if e is not None:
+            e[2] = value
+            return
+        chain = self.table[self.spread(h) & (len(self.table) - 1)]
+        before = len(chain)
+        chain.append([key, h, value])
+        if before >= 8:                                   # binCount >= TREEIFY_THRESHOLD - 1
+            if len(self.table) < 64:
+                self._resize()
+            else:
+                self.tree_bin = True
+        self.size += 1
+        if self.size > self.threshold:
+            self._resize()
+
+    def get(self, key, h: int):
+        e = self._find(key, h)
+        return None if e is None else e[2]
+
+    def remove(self, key, h: int) -> bool:
+        if self.table is None:
+            return False
+        chain = self.table[self.spread(h) & (len(self.table) - 1)]
+        for i, e in enumerate(chain):
+            if e[1] == h and e[0] == key:
+                del chain[i]
+                self.size -= 1
+                return True
+        return False
+
+    def keys(self) -> list:
+        return [] if self.table is None else [e[0] for chain in self.table for e in chain]
+
+    def __len__(self):
+        return self.size
+
+
+class ReplicaStore:
+    """PeerData.Other_Replica_Gradients + Other_Replica_Gradients_Received
+    (PeerData.java:140-141): one JavaHashMap keyed (p, aggregator) with the
+    Pair hashCode of (p, peer ID); value [array, received]."""
+
+    def __init__(self):
+        self.map = JavaHashMap()
+        self.hashes = {}
+
+    def __len__(self):
+        return len(self.map)
+
+
+def index_key_hash(p: int, aggregator: int) -> int:
+    """The key hash of an aggregator known only by its index: the peer ID is
+    Integer.toString(aggregator) (ipls_agg_other_replica without a hash)."""
+    return java_pair_hash(p, str(aggregator))
+
+
+def other_replica_add(store: ReplicaStore, partition: int, aggregator, g: np.ndarray,
+                      key_hash: int | None = None) -> None:
     """Download_Scheduler.java:254-266: the first download of (p, a) becomes the
-    stored array (GetParameters(Hash) -> new double[n]); later ones fold into it
-    for j < len(g) (IndexError where Java overruns the stored array)."""
+    stored array (Other_Replica_Gradients.put(key, GetParameters(Hash)) -> new
+    double[n]); later ones fold into it for j < len(g) (IndexError where Java
+    overruns the stored array) and bump Other_Replica_Gradients_Received."""
     key = (partition, aggregator)
-    if key not in store:
-        store[key] = [np.array(g, dtype=np.float64, copy=True), 1]
+    h = index_key_hash(partition, aggregator) if key_hash is None else key_hash
+    cur = store.map.get(key, h)
+    if cur is None:
+        store.map.put(key, h, [np.array(g, dtype=np.float64, copy=True), 1])
+        store.hashes[key] = h
         return
-    arr = store[key][0]
+    arr = cur[0]
     if len(g) > len(arr):
         raise IndexError("ArrayIndexOutOfBoundsException (Download_Scheduler.java:257)")
     arr[:len(g)] = arr[:len(g)] + g
-    store[key][1] += 1
+    cur[1] += 1
 
 
-def collect_replicas(rep: list, store: dict, participants: list | None = None) -> int:
-    """IPLS.Collect_Replicas, IPLS.java:1217-1241, in ascending (p, a) key order:
-    REP[p][j] = REP[p][j] + Other[(p, a)][j] for j < len(Other); store cleared."""
+def other_replica_drop(store: ReplicaStore, partition: int, aggregator) -> bool:
+    """Other_Replica_Gradients.remove(key) and Other_Replica_Gradients_Received
+    .remove(key) (Download_Scheduler.java:215-217, 329-332, 438-440)."""
+    key = (partition, aggregator)
+    if key not in store.hashes:
+        return False
+    store.map.remove(key, store.hashes.pop(key))
+    return True
+
+
+def collect_replicas(rep: list, store: ReplicaStore, participants: list | None = None) -> int:
+    """IPLS.Collect_Replicas, IPLS.java:1217-1241: for the keys of
+    new ArrayList<>(Other_Replica_Gradients.keySet()) in that order,
+    REP[p][j] = REP[p][j] + Other[(p, a)][j] for j < len(Other) and
+    Participants[p] += the download count; then the store is a new HashMap."""
     n = 0
-    for key in sorted(store):
+    for key in store.map.keys():
         p = key[0]
-        arr, received = store[key]
+        arr, received = store.map.get(key, store.hashes[key])
         rep[p][:len(arr)] = rep[p][:len(arr)] + arr
         if participants is not None:
             participants[p] += received
         n += 1
-    store.clear()
+    store.map = JavaHashMap()
+    store.hashes = {}
     return n
 
 

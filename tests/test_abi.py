@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for s in declared_symbols():
         assert hasattr(L, s), f"{s} declared in include/ipls_agg.h but not exported"
         assert s in N.SIGNATURES, f"{s} has no ctypes signature"
-    assert L.ipls_agg_abi_version() == N.ABI_VERSION == 2
+    assert L.ipls_agg_abi_version() == N.ABI_VERSION == 3
 
 
 def test_header_constants_match_binding():

@@ -1088,12 +1088,12 @@ def test_update_indirect_gradient_buff(ipls, O):
 def test_other_replica_gradients_and_collect(ipls, O):
     """Download_Scheduler.java:245-268 + IPLS.Collect_Replicas (:1217-1241):
     per-(partition, aggregator) arrays, FIRST-started (so -0.0 survives), folded
-    into REP in ascending key order after what REP already holds."""
+    into REP in the JDK HashMap's key order after what REP already holds."""
     M, P = 80001, 2
     agg = ipls.Aggregator(M, P, max_peers=4)
     Ls = agg.lengths
     rep = [np.zeros(L) for L in Ls]
-    store = {}
+    store = O.ReplicaStore()
     own_rep = O.synth_bucket(Ls[0], 0, 50)
     agg.Update(own_rep, 0, from_clients=False)                 # a replica that did answer
     rep[0] = O.reduce([own_rep], Ls[0])
@@ -1113,6 +1113,125 @@ def test_other_replica_gradients_and_collect(ipls, O):
     for p in range(P):
         assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}]")
     assert agg.Collect_Replicas() == (0, [0, 0])               # the store was cleared
+    agg.close()
+
+
+def test_replica_drop_when_its_partial_arrives(ipls, O):
+    """VERDICT r3 next 2 (Download_Scheduler.java:215-217, 329-332, 438-440):
+    buckets of two other aggregators of one partition are downloaded; one of
+    them then publishes its partial sum, which the Updater's replica branch
+    folds into REP (Updater.java:40-44), and its stored downloads are removed,
+    so Collect_Replicas folds only the other aggregator's -- nothing counted
+    twice.  Bit-exact vs the oracle; the drop of an absent key is a no-op."""
+    L, P = 70001, 2
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    store = O.ReplicaStore()
+    rep = [np.zeros(L) for _ in range(P)]
+    ids = {11: "12D3KooWAggregatorB", 12: "12D3KooWAggregatorC"}
+    for a, ks in ((11, (70, 71)), (12, (72, 73, 74))):
+        for k in ks:
+            g = O.synth_bucket(L, 0, k)
+            kh = ipls.java_pair_hash(0, ids[a])
+            assert kh == O.java_pair_hash(0, ids[a])
+            agg.OtherReplicaGradients(0, a, g, key_hash=kh)
+            O.other_replica_add(store, 0, a, g, key_hash=kh)
+    partial_b = O.reduce([O.synth_bucket(L, 0, k) for k in (70, 71, 75)], L)   # B's own published partial
+    agg.Update(partial_b, 0, from_clients=False)                                 # replica branch -> REP
+    rep[0] = rep[0] + partial_b
+    assert agg.OtherReplicaDrop(0, 11) is True and O.other_replica_drop(store, 0, 11)
+    assert agg.OtherReplicaDrop(0, 11) is False                                  # already gone
+    assert agg.OtherReplicaDrop(1, 12) is False                                  # never stored for p 1
+    parts_ref = [0] * P
+    n_ref = O.collect_replicas(rep, store, parts_ref)
+    n, parts = agg.Collect_Replicas()
+    assert (n, parts) == (n_ref, parts_ref) == (1, [3, 0])                       # only C's 3 downloads
+    assert_bits_equal(agg.read(0, ipls.TGT_REP), rep[0], "REP[0] after drop + collect")
+    # without the drop B's downloads would have been folded as well
+    twice = partial_b + O.reduce([O.synth_bucket(L, 0, k) for k in (70, 71)], L, ipls.START_FIRST) \
+        + O.reduce([O.synth_bucket(L, 0, k) for k in (72, 73, 74)], L, ipls.START_FIRST)
+    assert not np.array_equal(twice.view(np.uint64), rep[0].view(np.uint64))
+    agg.close()
+
+
+def _ids_with_non_ascending_order(O, p, n):
+    """n peer IDs whose Pair(p, id) hashes fall in bins 13, 7, 2 of a 16-bin
+    HashMap: stored in that order, they iterate in reverse -- neither
+    ascending index nor insertion order."""
+    ids, i = [], 0
+    for target in (13, 7, 2)[:n]:
+        while True:
+            cand = f"QmPeer{i:04d}"
+            i += 1
+            if O.JavaHashMap.spread(O.java_pair_hash(p, cand)) & 15 == target:
+                ids.append(cand)
+                break
+    return ids
+
+
+def test_collect_replicas_in_java_hashmap_order(ipls, O):
+    """VERDICT r3 next 3 (IPLS.java:1218-1227, PeerData.java:140): three stored
+    arrays on partition 0 and two on partition 1 (whose REP already holds a
+    replica's partial), keyed by peer IDs whose HashMap order differs from
+    both ascending index and insertion order.  The GPU result matches the
+    oracle's table simulation bit for bit, and differs from the ascending
+    order's bits (so the order is what the test checks)."""
+    L, P = 60007, 2
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    store = O.ReplicaStore()
+    rep = [np.zeros(L) for _ in range(P)]
+    scale = [1e16, 1.0, -1e16]                 # cancellation: any other order changes the bits
+    pre = O.synth_bucket(L, 1, 90) * 3.0
+    agg.Update(pre, 1, from_clients=False)
+    rep[1] = rep[1] + pre
+    plan = {0: _ids_with_non_ascending_order(O, 0, 3), 1: _ids_with_non_ascending_order(O, 1, 2)}
+    arrays = {}
+    for p, ids in plan.items():
+        for a, pid in enumerate(ids):
+            g = O.synth_bucket(L, p, 80 + a) * scale[a]
+            kh = O.java_pair_hash(p, pid)
+            agg.OtherReplicaGradients(p, a, g, key_hash=kh)
+            O.other_replica_add(store, p, a, g, key_hash=kh)
+            arrays[(p, a)] = g
+    order = store.map.keys()
+    assert order != sorted(order)
+    asc = [r.copy() for r in rep]
+    for (p, a) in sorted(arrays):
+        asc[p] = asc[p] + arrays[(p, a)]
+    n_ref = O.collect_replicas(rep, store, [0] * P)
+    n, parts = agg.Collect_Replicas()
+    assert n == n_ref == 5 and parts == [3, 2]
+    for p in range(P):
+        assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}] (HashMap order)")
+    assert any(not np.array_equal(asc[p].view(np.uint64), rep[p].view(np.uint64)) for p in range(P))
+    agg.close()
+
+
+def test_collect_replicas_order_after_resize_and_drops(ipls, O):
+    """Enough keys to resize the map (13 keys > 0.75 x 16, 25 > 0.75 x 32),
+    drops in between (the capacity stays), keys re-stored after a drop (they go
+    to the tail of their bin), and a collect that resets the map: every REP
+    matches the oracle's JDK table simulation bit for bit."""
+    L, P = 4099, 4
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    store = O.ReplicaStore()
+    rep = [np.zeros(L) for _ in range(P)]
+    rng = np.random.default_rng(5)
+    for rnd in range(2):
+        for i in range(60):
+            p, a = int(rng.integers(0, P)), int(rng.integers(0, 9))
+            if rng.integers(0, 5) == 0:
+                assert agg.OtherReplicaDrop(p, a) == O.other_replica_drop(store, p, a)
+                continue
+            g = O.synth_bucket(L, p, i) * float(10.0 ** rng.integers(-8, 9))
+            kh = O.java_pair_hash(p, f"12D3KooW{a}{'x' * a}")
+            agg.OtherReplicaGradients(p, a, g, key_hash=kh)
+            O.other_replica_add(store, p, a, g, key_hash=kh)
+        assert len(store.map.table) >= 32 and not store.map.tree_bin
+        exp_parts = [0] * P
+        n_ref = O.collect_replicas(rep, store, exp_parts)
+        assert agg.Collect_Replicas() == (n_ref, exp_parts)
+        for p in range(P):
+            assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"round {rnd} REP[{p}]")
     agg.close()
 
 
@@ -1530,7 +1649,10 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
         assert_bits_equal(agg.read(p, tg), M[T[tg]][p], f"step {what}: p{p} {T[tg]}")
 
     gbuf = np.zeros(L)          # the Updater's one Gradient_Buff (synthetic geometry: L doubles)
-    store = {}                  # Other_Replica_Gradients
+    store = O.ReplicaStore()    # Other_Replica_Gradients
+    # aggregator peer IDs: odd seeds pass the Pair hash of a real-looking ID
+    # (ipls_agg_other_replica_keyed), even seeds the index-as-ID default
+    peer_ids = [f"12D3KooW{seed}x{i}{'Q' * (i % 3)}" for i in range(5)]
     msgs = [O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmS")) for g in pool]
     script = list(prefix)
     for step in range(len(script) + steps):
@@ -1626,9 +1748,13 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
             gbuf[:n] = g[:n]
             M["agg"][p] = M["agg"][p] + gbuf
         elif op == 14:                                      # Download_Scheduler: another aggregator's bucket
-            a = int(rng.integers(0, 3))
-            agg.OtherReplicaGradients(p, a, g)
-            O.other_replica_add(store, p, a, g)
+            a = int(rng.integers(0, 5))
+            if rng.integers(0, 4) == 0:                     # its partial arrived: Other_Replica_Gradients.remove
+                assert agg.OtherReplicaDrop(p, a) == O.other_replica_drop(store, p, a)
+            else:
+                kh = O.java_pair_hash(p, peer_ids[a]) if seed % 2 else None
+                agg.OtherReplicaGradients(p, a, g, key_hash=kh)
+                O.other_replica_add(store, p, a, g, key_hash=kh)
         elif op == 15:                                      # Collect_Replicas
             n, part = agg.Collect_Replicas()
             exp_part = [0] * P

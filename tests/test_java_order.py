@@ -1,0 +1,139 @@
+"""The Collect_Replicas order (IPLS.java:1218-1227): the key order of the JDK
+HashMap<Pair<Integer,String>, double[]> Other_Replica_Gradients
+(PeerData.java:140).  CPU only.
+
+- String / javatuples Pair hash codes: the oracle's restatement against
+  published Java values, and the library's ipls_java_pair_hash against the
+  oracle (UTF-8 including supplementary characters; malformed bytes refused).
+- The library front's order model (csrc/java_hashmap.hpp: bin under the
+  current capacity, then insertion order) against the oracle's simulation of
+  the JDK table itself (oracle.JavaHashMap: chains, resize splits, removes),
+  over random put/remove/clear streams built to collide, resize and trigger
+  treeifyBin's resize below 64 bins.
+Parity unpinned: no JDK here; the restatements follow the published JDK 8 and
+javatuples 1.2 sources."""
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+    return oracle
+
+CSRC = ROOT / "ipls-java-api_amd" / "csrc"
+DRIVER = ROOT / "tests" / "cpp" / "build" / "java_order_driver"
+
+
+def test_java_string_hash_known_values(O):
+    # values any JDK prints for "...".hashCode()
+    assert O.java_string_hash("") == 0
+    assert O.java_string_hash("hello") == 99162322
+    assert O.java_string_hash("Aa") == O.java_string_hash("BB") == 2112
+    assert O.java_string_hash("polygenelubricants") == -2147483648
+    assert O.java_string_hash("a") == 97
+
+
+def test_pair_hash_formula(O):
+    # Arrays.asList(p, s).hashCode() = 31*(31*1 + p) + s.hashCode(); Tuple adds 31*1
+    for p, s in ((0, ""), (3, "hello"), (-7, "QmXyz"), (2**31 - 1, "polygenelubricants")):
+        lst = (31 * (31 + p) + O.java_string_hash(s)) & 0xFFFFFFFF
+        want = (31 + lst) & 0xFFFFFFFF
+        want = want - (1 << 32) if want >= 1 << 31 else want
+        assert O.java_pair_hash(p, s) == want
+
+
+def test_library_pair_hash_matches_oracle(O):
+    import ipls
+    from ipls import _native as N
+    rng = np.random.default_rng(3)
+    alphabet = "abcXYZ0189-_Qm" + "é€" + "\U0001F600"     # 1-, 2-, 3- and 4-byte UTF-8 (a surrogate pair in Java)
+    for i in range(300):
+        s = "".join(alphabet[j] for j in rng.integers(0, len(alphabet), int(rng.integers(0, 60))))
+        p = int(rng.integers(-1000, 1 << 20))
+        assert ipls.java_pair_hash(p, s) == O.java_pair_hash(p, s), (p, s)
+    lib = ipls.lib()
+    out = ctypes.c_int32()
+    for bad in (b"\xff", b"\xc0\x80", b"a\xe2\x82", b"\xed\xa0\x80"):   # invalid, overlong, truncated, surrogate
+        buf = (ctypes.c_uint8 * len(bad)).from_buffer_copy(bad)
+        assert lib.ipls_java_pair_hash(0, ctypes.addressof(buf), len(bad), ctypes.byref(out)) == N.IPLS_E_FORMAT
+
+
+def test_integer_keyed_hashmap_facts(O):
+    """Well-known JDK 8 iteration facts, with Integer keys (hashCode = value):
+    small keys iterate ascending whatever the insertion order; 16 and 0 share
+    bin 0 of a 16-bin table and iterate in insertion order; the 13th key
+    doubles the table, after which 16 and 0 separate."""
+    m = O.JavaHashMap()
+    for k in (9, 3, 12, 0, 5):
+        m.put(k, k, None)
+    assert m.keys() == [0, 3, 5, 9, 12]
+    m = O.JavaHashMap()
+    m.put(16, 16, None)
+    m.put(0, 0, None)
+    assert m.keys() == [16, 0]
+    for k in range(1, 11):                      # 12 keys: still 16 bins
+        m.put(k, k, None)
+    assert len(m.table) == 16 and m.keys()[:2] == [16, 0]
+    m.put(11, 11, None)                         # 13 > 12: resize to 32
+    assert len(m.table) == 32 and m.keys() == list(range(12)) + [16]
+
+
+def _build_driver():
+    DRIVER.parent.mkdir(parents=True, exist_ok=True)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    f"-I{CSRC}", str(ROOT / "tests" / "cpp" / "java_order_driver.cpp"), "-o", str(DRIVER)],
+                   check=True)
+
+
+@pytest.mark.parametrize("seed,nbits", [(1, 32), (2, 6), (3, 5), (4, 9), (5, 32)])
+def test_front_model_matches_jdk_table_simulation(O, seed, nbits):
+    """Random streams of put / remove / collect over (p, aggregator) keys; with
+    few hash bits (nbits) many keys collide, chains reach 9 below 64 bins
+    (treeifyBin resizes) and removes leave holes.  After every 'o' the model's
+    order must equal the simulated table's iteration order (skipped only once
+    a tree bin appears, which neither side restates)."""
+    _build_driver()
+    rng = np.random.default_rng(seed)
+    cmds, expect = [], []
+    m, hashes = O.JavaHashMap(), {}
+    for step in range(3000):
+        r = rng.integers(0, 20)
+        p, a = int(rng.integers(0, 40)), int(rng.integers(0, 25))
+        if r < 12:
+            h = int(rng.integers(0, 1 << nbits)) if nbits < 32 else O.java_pair_hash(p, f"12D3KooW{a}")
+            h = hashes.get((p, a), h)
+            cmds.append(f"p {p} {a} {h}")
+            if (p, a) not in hashes:
+                hashes[(p, a)] = h
+                m.put((p, a), h, None)
+        elif r < 17:
+            cmds.append(f"r {p} {a}")
+            if (p, a) in hashes:
+                m.remove((p, a), hashes.pop((p, a)))
+        elif r < 19:
+            cmds.append("o")
+            expect.append((len(m.table) if m.table else 0, int(m.tree_bin), m.keys()))
+        else:
+            cmds.append("o")
+            expect.append((len(m.table) if m.table else 0, int(m.tree_bin), m.keys()))
+            cmds.append("c")
+            m, hashes = O.JavaHashMap(), {}
+    out = subprocess.run([str(DRIVER)], input="\n".join(cmds) + "\n", capture_output=True, text=True, timeout=120,
+                         check=True).stdout.splitlines()
+    assert len(out) == len(expect)
+    compared = 0
+    for line, (cap, tree, keys) in zip(out, expect):
+        f = line.split()
+        assert int(f[0]) == cap and int(f[1]) == tree, (line[:80], cap, tree)
+        if tree:
+            continue
+        got = [tuple(int(x) for x in kv.split(":")) for kv in f[2:]]
+        assert got == keys
+        compared += 1
+    assert compared > 50

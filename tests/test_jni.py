@@ -156,7 +156,7 @@ def test_direct_buffer_checks_before_the_library(jvm):
                        ("accumulateAsyncDirect", (L64(0), 0, 0, heap, 0, L64(1), 1)),
                        ("updateIndirect", (L64(0), 0, 0, buf, 8, L64(57))),
                        ("setWeightsDirect", (L64(0), 0, heap, 0, L64(1))),
-                       ("otherReplicaDirect", (L64(0), 0, 1, buf, 0, L64(9))),
+                       ("otherReplicaDirect", (L64(0), 0, 1, 0, buf, 0, L64(9))),
                        ("getPartitionsWire", (L64(0), heap, 0, L64(8))),
                        # counts whose byte size overflows a jlong (8 * n wraps to a small or
                        # negative value) are rejected before any multiplication
@@ -164,7 +164,7 @@ def test_direct_buffer_checks_before_the_library(jvm):
                        ("accumulateDirect", (L64(0), 0, 0, buf, 8, L64((1 << 63) - 1), 1)),
                        ("accumulateAsyncDirect", (L64(0), 0, 0, buf, 0, L64((1 << 61) + 1), 1)),
                        ("setWeightsDirect", (L64(0), 0, buf, 0, L64(1 << 62))),
-                       ("otherReplicaDirect", (L64(0), 0, 1, buf, 0, L64(1 << 61))),
+                       ("otherReplicaDirect", (L64(0), 0, 1, 0, buf, 0, L64(1 << 61))),
                        ("updateIndirect", (L64(0), 0, 0, buf, 65, L64(0)))]:          # pos past the end
         _, exc = jvm.call(name, *args)
         assert exc == "java/lang/IllegalArgumentException", (name, exc)
@@ -304,6 +304,43 @@ def test_jni_exceptions_leave_state_unchanged(jvm, gpu, O):
     parts_ok = jvm.ints([0, 0])
     n, exc = jvm.call("collectReplicas", h, parts_ok, res=ctypes.c_int32)
     assert exc is None and n == 0
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
+def test_jni_replica_store_drop_and_hashmap_order(jvm, gpu, O):
+    """otherReplicaDirect with the Pair hash the Java side computes
+    (NativeAggregator.otherReplica), otherReplicaDrop when an aggregator's
+    partial arrived, collectReplicas in the HashMap order: REP equals the
+    oracle's bit for bit and the counts are the Participants."""
+    M, P = 30002, 2
+    h = _open(jvm, M, P)
+    L = O.partition_len(M, P, 0)
+    store = O.ReplicaStore()
+    ids = ["12D3KooWQmAlpha", "12D3KooWQmBeta", "12D3KooWQmGamma"]
+    for i, (a, k) in enumerate([(0, 1), (1, 2), (2, 3), (0, 4), (2, 5)]):
+        g = O.synth_bucket(L, 0, k) * (1e15 if a == 1 else 1.0)
+        buf, mem = jvm.direct(8 * L)
+        mem[:] = np.frombuffer(O.be_encode(g), dtype=np.uint8)
+        kh = O.java_pair_hash(0, ids[a])
+        _, exc = jvm.call("otherReplicaDirect", h, 0, a, kh, buf, 0, L64(L))
+        assert exc is None
+        O.other_replica_add(store, 0, a, g, key_hash=kh)
+    r, exc = jvm.call("otherReplicaDrop", h, 0, 2, res=ctypes.c_bool)
+    assert exc is None and r is True and O.other_replica_drop(store, 0, 2)
+    r, exc = jvm.call("otherReplicaDrop", h, 1, 2, res=ctypes.c_bool)
+    assert exc is None and r is False
+    r, exc = jvm.call("otherReplicaDrop", h, 9, 2, res=ctypes.c_bool)
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    rep = [np.zeros(O.partition_len(M, P, p)) for p in range(P)]
+    exp = [0, 0]
+    n_ref = O.collect_replicas(rep, store, exp)
+    parts = jvm.ints([0, 0])
+    n, exc = jvm.call("collectReplicas", h, parts, res=ctypes.c_int32)
+    assert exc is None and n == n_ref == 2 and list(jvm.data(parts, np.int32)) == exp == [3, 0]
+    out = jvm.bytes_(b"\0" * (8 * L))
+    _, exc = jvm.call("finalizePartition", h, 0, out)              # W = AGG (+0.0) + REP
+    assert exc is None and jvm.data(out, np.uint8).tobytes() == O.be_encode(0.0 + rep[0])
     jvm.call("close", h)
 
 
