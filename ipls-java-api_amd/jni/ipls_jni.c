@@ -10,12 +10,27 @@
  * NULL for a heap buffer, so the Java wrappers pass position() and the byte
  * count, and the shim adds the position and checks both against capacity.
  *
+ * Heap arrays are never held in a critical region across a library call.
+ * GetPrimitiveArrayCritical would hand the library the Java heap itself, but
+ * the region then spans the call -- host copies, a device fold, a wait on the
+ * GPU -- and a JVM blocks its garbage collector for as long as a critical
+ * region is open.  So every heap array (double[], byte[], byte[][]) is
+ * copied out with Get<T>ArrayRegion into a per-thread staging buffer before
+ * the call, and outputs are written there and copied back with
+ * Set<T>ArrayRegion after it: one host memcpy, no GC stall.  The zero-copy
+ * route is the direct-ByteBuffer natives (hostAlloc memory), which the hot
+ * paths use.  Every library call goes through LIB(): a
+ * test build (-DIPLS_JNI_CALL_HOOK=fj_library_call) reports each one to the
+ * fake JVM, which fails the test if a critical region is open at that point.
+ *
  * Built against the JDK's <jni.h> on the Java side's build host (make -C
  * ipls-java-api_amd jni).  This image has no JDK: tests/test_jni.py compiles
  * it with -Wall -Wextra -Werror against tests/jni/jni.h and drives every
  * native through tests/jni/fake_jvm.c.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <jni.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -46,7 +61,61 @@ static void throw_iae(JNIEnv *env, const char *what) {
     throw_msg(env, "java/lang/IllegalArgumentException", what);
 }
 
+#ifdef IPLS_JNI_CALL_HOOK
+void IPLS_JNI_CALL_HOOK(const char *call);
+#define LIB(x) (IPLS_JNI_CALL_HOOK(#x), (x))
+#else
+#define LIB(x) (x)
+#endif
+
 #define H(x) ((ipls_agg *)(intptr_t)(x))
+
+/* ---- per-thread staging for heap arrays (freed when the thread ends) ---- */
+struct stage { void *p[2]; size_t cap[2]; };
+static pthread_key_t g_stage_key;
+static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
+static void stage_free(void *v) {
+    struct stage *st = (struct stage *)v;
+    free(st->p[0]);
+    free(st->p[1]);
+    free(st);
+}
+static void stage_init(void) { (void)pthread_key_create(&g_stage_key, stage_free); }
+
+/* Staging slot `slot` (0 or 1) of at least `bytes` bytes, or NULL with an
+ * OutOfMemoryError pending. */
+static void *stage(JNIEnv *env, int slot, size_t bytes) {
+    (void)pthread_once(&g_stage_once, stage_init);
+    struct stage *st = (struct stage *)pthread_getspecific(g_stage_key);
+    if (!st) {
+        st = (struct stage *)calloc(1, sizeof *st);
+        if (!st || pthread_setspecific(g_stage_key, st) != 0) {
+            free(st);
+            throw_msg(env, "java/lang/OutOfMemoryError", "JNI staging buffer");
+            return NULL;
+        }
+    }
+    if (bytes == 0) bytes = 1;
+    if (st->cap[slot] < bytes) {
+        void *q = realloc(st->p[slot], bytes);
+        if (!q) { throw_msg(env, "java/lang/OutOfMemoryError", "JNI staging buffer"); return NULL; }
+        st->p[slot] = q;
+        st->cap[slot] = bytes;
+    }
+    return st->p[slot];
+}
+
+/* A copy of the whole double[] / byte[] in staging slot `slot`. */
+static void *copy_doubles(JNIEnv *env, jdoubleArray a, jsize n, int slot) {
+    double *d = (double *)stage(env, slot, (size_t)n * 8);
+    if (d && n > 0) (*env)->GetDoubleArrayRegion(env, a, 0, n, d);
+    return d;
+}
+static void *copy_bytes(JNIEnv *env, jbyteArray a, jsize n, int slot) {
+    jbyte *d = (jbyte *)stage(env, slot, (size_t)n);
+    if (d && n > 0) (*env)->GetByteArrayRegion(env, a, 0, n, d);
+    return d;
+}
 #define CHECK(rc, h) do { int rc_ = (rc); if (rc_ < 0) { throw_for(env, rc_, (h)); } } while (0)
 
 /* The bytes [pos, pos + count * elem) of a direct buffer, or NULL with an
@@ -68,7 +137,7 @@ static void *direct_span(JNIEnv *env, jobject buf, jint pos, jlong count, jlong 
 /* L_p (or -1 with the exception pending). */
 static int64_t part_len(JNIEnv *env, jlong h, jint p) {
     int64_t L = 0;
-    int rc = ipls_agg_partition_len(H(h), p, &L);
+    int rc = LIB(ipls_agg_partition_len(H(h), p, &L));
     if (rc < 0) { throw_for(env, rc, H(h)); return -1; }
     return L;
 }
@@ -87,7 +156,7 @@ static int need_len(JNIEnv *env, jarray a, int64_t need, const char *what) {
 
 static jlong open_cfg(JNIEnv *env, ipls_agg_cfg *cfg) {
     ipls_agg *h = NULL;
-    int rc = ipls_agg_open(cfg, &h);
+    int rc = LIB(ipls_agg_open(cfg, &h));
     if (rc < 0) { throw_for(env, rc, NULL); return 0; }
     return (jlong)(intptr_t)h;
 }
@@ -122,7 +191,7 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_openDevices(JNIEnv *env, jclass c,
 
 JNIEXPORT void JNICALL Java_NativeAggregator_close(JNIEnv *env, jclass c, jlong h) {
     (void)env; (void)c;
-    ipls_agg_close(H(h));
+    LIB(ipls_agg_close(H(h)));
 }
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_partitionLen(JNIEnv *env, jclass c, jlong h, jint p) {
@@ -133,14 +202,14 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_partitionLen(JNIEnv *env, jclass c
 JNIEXPORT jlong JNICALL Java_NativeAggregator_partitionOffset(JNIEnv *env, jclass c, jlong h, jint p) {
     (void)c;
     int64_t off = 0;
-    CHECK(ipls_agg_partition_offset(H(h), p, &off), H(h));
+    CHECK(LIB(ipls_agg_partition_offset(H(h), p, &off)), H(h));
     return (jlong)off;
 }
 
 JNIEXPORT jint JNICALL Java_NativeAggregator_partitionDevice(JNIEnv *env, jclass c, jlong h, jint p) {
     (void)c;
     int32_t d = -1;
-    CHECK(ipls_agg_partition_device(H(h), p, &d, NULL), H(h));
+    CHECK(LIB(ipls_agg_partition_device(H(h), p, &d, NULL)), H(h));
     return d;
 }
 
@@ -149,7 +218,7 @@ JNIEXPORT jintArray JNICALL Java_NativeAggregator_shardPlan(JNIEnv *env, jclass 
     if (partitions <= 0) { throw_iae(env, "partitions must be > 0"); return NULL; }
     int32_t *o = (int32_t *)malloc(sizeof(int32_t) * (size_t)partitions);
     if (!o) { throw_msg(env, "java/lang/OutOfMemoryError", "shard plan"); return NULL; }
-    int rc = ipls_shard_plan(partitions, shards, o);
+    int rc = LIB(ipls_shard_plan(partitions, shards, o));
     jintArray res = NULL;
     if (rc < 0) {
         throw_for(env, rc, NULL);
@@ -165,10 +234,9 @@ JNIEXPORT void JNICALL Java_NativeAggregator_loadModel(JNIEnv *env, jclass c, jl
     (void)c;
     if (!a) { throw_iae(env, "null model"); return; }
     jsize n = (*env)->GetArrayLength(env, a);
-    void *p = (*env)->GetPrimitiveArrayCritical(env, a, NULL);
-    int rc = ipls_agg_load_model(H(h), p, n, IPLS_HOST_F64);
-    (*env)->ReleasePrimitiveArrayCritical(env, a, p, JNI_ABORT);
-    CHECK(rc, H(h));
+    void *p = copy_doubles(env, a, n, 0);
+    if (!p) return;
+    CHECK(LIB(ipls_agg_load_model(H(h), p, n, IPLS_HOST_F64)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_split(JNIEnv *env, jclass c, jlong h, jdoubleArray flat, jint part,
@@ -177,11 +245,11 @@ JNIEXPORT void JNICALL Java_NativeAggregator_split(JNIEnv *env, jclass c, jlong 
     const int64_t L = part_len(env, h, part);
     if (L < 0 || !need_len(env, out, L, "split output") || !need_len(env, flat, 0, "null gradients")) return;
     jsize n = (*env)->GetArrayLength(env, flat);
-    void *src = (*env)->GetPrimitiveArrayCritical(env, flat, NULL);
-    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    int rc = ipls_agg_split(H(h), src, n, IPLS_HOST_F64, part, dst, IPLS_HOST_F64);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, flat, src, JNI_ABORT);
+    void *src = copy_doubles(env, flat, n, 0);
+    double *dst = src ? (double *)stage(env, 1, (size_t)L * 8) : NULL;
+    if (!dst) return;
+    int rc = LIB(ipls_agg_split(H(h), src, n, IPLS_HOST_F64, part, dst, IPLS_HOST_F64));
+    if (rc >= 0) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)L, dst);
     CHECK(rc, H(h));
 }
 
@@ -191,10 +259,11 @@ JNIEXPORT void JNICALL Java_NativeAggregator_updateGradient(JNIEnv *env, jclass 
     if (!flat) return;   /* Gradients == null: no-op (IPLS.java:1738) */
     if (!owned) { throw_iae(env, "null auth list"); return; }
     jsize n = (*env)->GetArrayLength(env, flat), no = (*env)->GetArrayLength(env, owned);
-    jint *own = (*env)->GetIntArrayElements(env, owned, NULL);   /* before the critical region */
-    void *src = (*env)->GetPrimitiveArrayCritical(env, flat, NULL);
-    int rc = ipls_agg_update_gradient(H(h), src, n, IPLS_HOST_F64, (const int32_t *)own, no);
-    (*env)->ReleasePrimitiveArrayCritical(env, flat, src, JNI_ABORT);
+    void *src = copy_doubles(env, flat, n, 0);
+    if (!src) return;
+    jint *own = (*env)->GetIntArrayElements(env, owned, NULL);
+    if (!own) return;   /* OutOfMemoryError pending */
+    int rc = LIB(ipls_agg_update_gradient(H(h), src, n, IPLS_HOST_F64, (const int32_t *)own, no));
     (*env)->ReleaseIntArrayElements(env, owned, own, JNI_ABORT);
     CHECK(rc, H(h));
 }
@@ -204,10 +273,9 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
     (void)c;
     if (!g) return;   /* Gradient == null: the Updater loops do nothing (Updater.java:115) */
     jsize n = (*env)->GetArrayLength(env, g);
-    void *src = (*env)->GetPrimitiveArrayCritical(env, g, NULL);
-    int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_F64);
-    (*env)->ReleasePrimitiveArrayCritical(env, g, src, JNI_ABORT);
-    CHECK(rc, H(h));
+    void *src = copy_doubles(env, g, n, 0);
+    if (!src) return;
+    CHECK(LIB(ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_F64)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
@@ -215,7 +283,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclas
     (void)c;
     void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
-    CHECK(ipls_agg_accumulate(H(h), p, tgt, src, n, kind), H(h));
+    CHECK(LIB(ipls_agg_accumulate(H(h), p, tgt, src, n, kind)), H(h));
 }
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_accumulateAsyncDirect(JNIEnv *env, jclass c, jlong h, jint p,
@@ -225,18 +293,18 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_accumulateAsyncDirect(JNIEnv *env,
     void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return 0;
     uint64_t t = 0;
-    CHECK(ipls_agg_accumulate_async(H(h), p, tgt, src, n, kind, &t), H(h));
+    CHECK(LIB(ipls_agg_accumulate_async(H(h), p, tgt, src, n, kind, &t)), H(h));
     return (jlong)t;
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_waitTicket(JNIEnv *env, jclass c, jlong h, jlong ticket) {
     (void)c;
-    CHECK(ipls_agg_wait(H(h), (uint64_t)ticket), H(h));
+    CHECK(LIB(ipls_agg_wait(H(h), (uint64_t)ticket)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_flushQueued(JNIEnv *env, jclass c, jlong h) {
     (void)c;
-    CHECK(ipls_agg_flush(H(h)), H(h));
+    CHECK(LIB(ipls_agg_flush(H(h))), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
@@ -244,7 +312,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_updateIndirect(JNIEnv *env, jclass 
     (void)c;
     void *src = direct_span(env, buf, pos, nBytes, 1);
     if (!src) return;
-    CHECK(ipls_agg_update_indirect(H(h), p, tgt, src, nBytes), H(h));
+    CHECK(LIB(ipls_agg_update_indirect(H(h), p, tgt, src, nBytes)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateFrame(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
@@ -252,16 +320,14 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulateFrame(JNIEnv *env, jclass
     (void)c;
     if (!frame) { throw_iae(env, "null frame"); return; }
     jsize n = (*env)->GetArrayLength(env, frame);
-    void *src = (*env)->GetPrimitiveArrayCritical(env, frame, NULL);
-    int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_FRAME);
-    (*env)->ReleasePrimitiveArrayCritical(env, frame, src, JNI_ABORT);
-    CHECK(rc, H(h));
+    void *src = copy_bytes(env, frame, n, 0);
+    if (!src) return;
+    CHECK(LIB(ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_FRAME)), H(h));
 }
 
-/* ThreadReceiver: a batch of pubsub texts.  The local refs are taken before
- * any critical region opens (no other JNI call is allowed inside one); the
- * texts stay pinned by the JVM for the call (the library copies them to the
- * GPU before returning). */
+/* ThreadReceiver: a batch of pubsub texts.  The texts are copied into one
+ * staging arena (GetByteArrayRegion: no critical region, so the JVM's GC
+ * keeps running while the library copies them to the GPU and folds them). */
 JNIEXPORT jint JNICALL Java_NativeAggregator_ingestTexts(JNIEnv *env, jclass c, jlong h, jint tgt,
                                                          jobjectArray msgs, jint layers, jintArray parts,
                                                          jintArray status) {
@@ -269,35 +335,45 @@ JNIEXPORT jint JNICALL Java_NativeAggregator_ingestTexts(JNIEnv *env, jclass c, 
     const jsize n = msgs ? (*env)->GetArrayLength(env, msgs) : 0;
     if (parts && (*env)->GetArrayLength(env, parts) < n) { throw_iae(env, "partitions shorter than the texts"); return 0; }
     if (status && (*env)->GetArrayLength(env, status) < n) { throw_iae(env, "status shorter than the texts"); return 0; }
-    jbyteArray *arr = calloc((size_t)n + 1, sizeof *arr);
     const uint8_t **ptr = calloc((size_t)n + 1, sizeof *ptr);
     int64_t *len = calloc((size_t)n + 1, sizeof *len);
+    int64_t *off = calloc((size_t)n + 1, sizeof *off);
     int32_t *st = calloc((size_t)n + 1, sizeof *st);
     jint *pp = NULL;
     int rc = IPLS_E_NOMEM;
-    if (!arr || !ptr || !len || !st) goto out;
-    /* one local ref per text is live at once: more than the 16 a native frame is guaranteed */
-    if ((*env)->EnsureLocalCapacity(env, n + 8) < 0) { free(arr); free(ptr); free(len); free(st); return 0; }
+    if (!ptr || !len || !off || !st) { throw_msg(env, "java/lang/OutOfMemoryError", "ingestTexts"); goto out; }
+    /* pass 1: lengths and arena offsets (one local ref at a time) */
+    int64_t total = 0;
     for (jsize i = 0; i < n; ++i) {
-        arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, msgs, i);
-        len[i] = arr[i] ? (*env)->GetArrayLength(env, arr[i]) : 0;
+        jbyteArray t = (jbyteArray)(*env)->GetObjectArrayElement(env, msgs, i);
+        len[i] = t ? (*env)->GetArrayLength(env, t) : 0;
+        off[i] = t ? total : -1;
+        total += (len[i] + 63) / 64 * 64;
+        if (t) (*env)->DeleteLocalRef(env, t);
     }
-    if (parts) pp = (*env)->GetIntArrayElements(env, parts, NULL);
-    for (jsize i = 0; i < n; ++i)
-        ptr[i] = arr[i] ? (*env)->GetPrimitiveArrayCritical(env, arr[i], NULL) : NULL;
-    rc = ipls_agg_ingest_pubsub(H(h), tgt, ptr, len, n, layers, (const int32_t *)pp, st);
-    for (jsize i = n; i-- > 0;)
-        if (ptr[i]) (*env)->ReleasePrimitiveArrayCritical(env, arr[i], (void *)ptr[i], JNI_ABORT);
+    uint8_t *arena = (uint8_t *)stage(env, 0, (size_t)total);
+    if (!arena) goto out;
+    /* pass 2: the copies */
+    for (jsize i = 0; i < n; ++i) {
+        if (off[i] < 0) continue;
+        jbyteArray t = (jbyteArray)(*env)->GetObjectArrayElement(env, msgs, i);
+        if (len[i] > 0) (*env)->GetByteArrayRegion(env, t, 0, (jsize)len[i], (jbyte *)(arena + off[i]));
+        (*env)->DeleteLocalRef(env, t);
+        ptr[i] = arena + off[i];
+    }
+    if (parts) {
+        pp = (*env)->GetIntArrayElements(env, parts, NULL);
+        if (!pp) goto out;   /* OutOfMemoryError pending */
+    }
+    rc = LIB(ipls_agg_ingest_pubsub(H(h), tgt, ptr, len, n, layers, (const int32_t *)pp, st));
     if (pp) (*env)->ReleaseIntArrayElements(env, parts, pp, JNI_ABORT);
     if (status && rc >= 0) (*env)->SetIntArrayRegion(env, status, 0, n, (const jint *)st);
-    for (jsize i = 0; i < n; ++i)
-        if (arr[i]) (*env)->DeleteLocalRef(env, arr[i]);
+    CHECK(rc, H(h));
 out:
-    free(arr);
     free(ptr);
     free(len);
+    free(off);
     free(st);
-    CHECK(rc, H(h));
     return rc;
 }
 
@@ -308,9 +384,12 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jcla
         const int64_t L = part_len(env, h, p);
         if (L < 0 || !need_len(env, sum, 8 * L, "commit_update bytes")) return;
     }
-    void *dst = sum ? (*env)->GetPrimitiveArrayCritical(env, sum, NULL) : NULL;
-    int rc = ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL);
-    if (sum) (*env)->ReleasePrimitiveArrayCritical(env, sum, dst, 0);
+    int64_t L = 0;
+    if (sum && LIB(ipls_agg_partition_len(H(h), p, &L)) < 0) { throw_for(env, IPLS_E_RANGE, H(h)); return; }
+    jbyte *dst = sum ? (jbyte *)stage(env, 0, (size_t)L * 8) : NULL;
+    if (sum && !dst) return;
+    int rc = LIB(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL));
+    if (sum && rc >= 0) (*env)->SetByteArrayRegion(env, sum, 0, (jsize)(8 * L), dst);
     CHECK(rc, H(h));
 }
 
@@ -321,7 +400,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartitionDirect(JNIEnv *env
     if (L < 0) return;
     void *dst = direct_span(env, sum, pos, L, 8);
     if (!dst) return;
-    CHECK(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL), H(h));
+    CHECK(LIB(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclass c, jlong h, jint p, jobject buf,
@@ -329,7 +408,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsDirect(JNIEnv *env, jclas
     (void)c;
     void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
-    CHECK(ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_BE), H(h));
+    CHECK(LIB(ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_BE)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass c, jlong h, jint p,
@@ -337,19 +416,20 @@ JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass
     (void)c;
     if (!frame) { throw_iae(env, "null frame"); return; }
     jsize n = (*env)->GetArrayLength(env, frame);
-    void *src = (*env)->GetPrimitiveArrayCritical(env, frame, NULL);
-    int rc = ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_FRAME);
-    (*env)->ReleasePrimitiveArrayCritical(env, frame, src, JNI_ABORT);
-    CHECK(rc, H(h));
+    void *src = copy_bytes(env, frame, n, 0);
+    if (!src) return;
+    CHECK(LIB(ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_FRAME)), H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c, jlong h, jdoubleArray out) {
     (void)c;
     if (!out) { throw_iae(env, "null output"); return; }
     jsize n = (*env)->GetArrayLength(env, out);   /* the library checks n against the model size */
-    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    int rc = ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    /* copied in first: elements past the model keep their values when copied back */
+    double *dst = (double *)copy_doubles(env, out, n, 0);
+    if (!dst) return;
+    int rc = LIB(ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64));
+    if (rc >= 0) (*env)->SetDoubleArrayRegion(env, out, 0, n, dst);
     CHECK(rc, H(h));
 }
 
@@ -358,14 +438,16 @@ JNIEXPORT void JNICALL Java_NativeAggregator_aggregateRound(JNIEnv *env, jclass 
     (void)c;
     /* the averages of [p0, p0+np): flat offsets off[p0] .. off[p_last] + L_last - 1 */
     int64_t o0 = 0, ol = 0, Ll = 0;
-    int rc = np > 0 ? ipls_agg_partition_offset(H(h), p0, &o0) : IPLS_E_RANGE;
-    if (rc >= 0) rc = ipls_agg_partition_offset(H(h), p0 + np - 1, &ol);
-    if (rc >= 0) rc = ipls_agg_partition_len(H(h), p0 + np - 1, &Ll);
+    int rc = np > 0 ? LIB(ipls_agg_partition_offset(H(h), p0, &o0)) : IPLS_E_RANGE;
+    if (rc >= 0) rc = LIB(ipls_agg_partition_offset(H(h), p0 + np - 1, &ol));
+    if (rc >= 0) rc = LIB(ipls_agg_partition_len(H(h), p0 + np - 1, &Ll));
     if (rc < 0) { throw_for(env, rc, H(h)); return; }
     if (out && !need_len(env, out, ol + Ll - 1 - o0, "averages")) return;
-    void *dst = out ? (*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
-    rc = ipls_agg_aggregate_round(H(h), p0, np, NULL, 0, IPLS_DEV_F64, dst, IPLS_HOST_F64);
-    if (out) (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    const int64_t na = ol + Ll - 1 - o0;
+    double *dst = out ? (double *)stage(env, 0, (size_t)na * 8) : NULL;
+    if (out && !dst) return;
+    rc = LIB(ipls_agg_aggregate_round(H(h), p0, np, NULL, 0, IPLS_DEV_F64, dst, IPLS_HOST_F64));
+    if (out && rc >= 0) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)na, dst);
     CHECK(rc, H(h));
 }
 
@@ -374,7 +456,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_promoteFuture(JNIEnv *env, jclass c
     if (!parts) { throw_iae(env, "null partition list"); return; }
     jsize n = (*env)->GetArrayLength(env, parts);
     jint *ps = (*env)->GetIntArrayElements(env, parts, NULL);
-    int rc = ipls_agg_promote_future(H(h), (const int32_t *)ps, n);
+    int rc = LIB(ipls_agg_promote_future(H(h), (const int32_t *)ps, n));
     (*env)->ReleaseIntArrayElements(env, parts, ps, JNI_ABORT);
     CHECK(rc, H(h));
 }
@@ -384,12 +466,12 @@ JNIEXPORT void JNICALL Java_NativeAggregator_otherReplicaDirect(JNIEnv *env, jcl
     (void)c;
     void *src = direct_span(env, buf, pos, n, 8);
     if (!src) return;
-    CHECK(ipls_agg_other_replica_keyed(H(h), p, a, keyHash, src, n, IPLS_HOST_BE), H(h));
+    CHECK(LIB(ipls_agg_other_replica_keyed(H(h), p, a, keyHash, src, n, IPLS_HOST_BE)), H(h));
 }
 
 JNIEXPORT jboolean JNICALL Java_NativeAggregator_otherReplicaDrop(JNIEnv *env, jclass c, jlong h, jint p, jint a) {
     (void)c;
-    const int rc = ipls_agg_other_replica_drop(H(h), p, a);
+    const int rc = LIB(ipls_agg_other_replica_drop(H(h), p, a));
     if (rc < 0) {
         throw_for(env, rc, H(h));
         return JNI_FALSE;
@@ -404,13 +486,13 @@ JNIEXPORT jint JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass
     if (out) {
         int64_t L;
         const jsize n = (*env)->GetArrayLength(env, out);
-        if (n == 0 || ipls_agg_partition_len(H(h), n, &L) == IPLS_OK) {
+        if (n == 0 || LIB(ipls_agg_partition_len(H(h), n, &L)) == IPLS_OK) {
             throw_iae(env, "participants array shorter than the number of partitions");
             return 0;
         }
     }
     jint *ps = out ? (*env)->GetIntArrayElements(env, out, NULL) : NULL;
-    int rc = ipls_agg_collect_replicas(H(h), (int32_t *)ps);
+    int rc = LIB(ipls_agg_collect_replicas(H(h), (int32_t *)ps));
     if (ps) (*env)->ReleaseIntArrayElements(env, out, ps, 0);
     CHECK(rc, H(h));
     return rc;
@@ -418,7 +500,7 @@ JNIEXPORT jint JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass
 
 JNIEXPORT jlong JNICALL Java_NativeAggregator_commitPartialLen(JNIEnv *env, jclass c, jlong h, jint p, jint w) {
     (void)c;
-    int64_t n = ipls_agg_commit_partial(H(h), p, w, NULL, 0);
+    int64_t n = LIB(ipls_agg_commit_partial(H(h), p, w, NULL, 0));
     if (n < 0) { throw_for(env, (int)n, H(h)); return 0; }
     return (jlong)n;
 }
@@ -428,10 +510,11 @@ JNIEXPORT void JNICALL Java_NativeAggregator_commitPartial(JNIEnv *env, jclass c
     (void)c;
     if (!out) { throw_iae(env, "null output"); return; }
     jsize n = (*env)->GetArrayLength(env, out);   /* passed as the capacity: the library checks it */
-    void *dst = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    int64_t rc = ipls_agg_commit_partial(H(h), p, w, (uint8_t *)dst, n);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
+    jbyte *dst = (jbyte *)stage(env, 0, (size_t)n);
+    if (!dst) return;
+    int64_t rc = LIB(ipls_agg_commit_partial(H(h), p, w, (uint8_t *)dst, n));
     if (rc < 0) throw_for(env, (int)rc, H(h));
+    else (*env)->SetByteArrayRegion(env, out, 0, (jsize)rc, dst);
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulatePair(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
@@ -439,10 +522,9 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulatePair(JNIEnv *env, jclass 
     (void)c;
     if (!file) { throw_iae(env, "null file"); return; }
     jsize n = (*env)->GetArrayLength(env, file);
-    void *src = (*env)->GetPrimitiveArrayCritical(env, file, NULL);
-    int rc = ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_PAIR);
-    (*env)->ReleasePrimitiveArrayCritical(env, file, src, JNI_ABORT);
-    CHECK(rc, H(h));
+    void *src = copy_bytes(env, file, n, 0);
+    if (!src) return;
+    CHECK(LIB(ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_PAIR)), H(h));
 }
 
 JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclass c, jlong h, jobjectArray files,
@@ -450,30 +532,38 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclas
     (void)c;
     jsize k = files ? (*env)->GetArrayLength(env, files) : 0;
     if (k < 1) { throw_iae(env, "need at least one file"); return NULL; }
-    jbyteArray *arr = (jbyteArray *)calloc((size_t)k, sizeof(jbyteArray));
     const uint8_t **ptrs = (const uint8_t **)calloc((size_t)k, sizeof(uint8_t *));
     int64_t *lens = (int64_t *)calloc((size_t)k, sizeof(int64_t));
+    int64_t *offs = (int64_t *)calloc((size_t)k, sizeof(int64_t));
     jbyteArray res = NULL;
     uint8_t *out = NULL;
-    jsize got = 0;
-    if (!arr || !ptrs || !lens) { throw_msg(env, "java/lang/OutOfMemoryError", "mergeFiles"); goto done; }
-    if ((*env)->EnsureLocalCapacity(env, k + 8) < 0) goto done;   /* OutOfMemoryError pending */
-    for (; got < k; ++got) {   /* copies: several arrays cannot be held critical across a JNI call */
-        arr[got] = (jbyteArray)(*env)->GetObjectArrayElement(env, files, got);
-        if (!arr[got]) { throw_iae(env, "null file"); goto done; }
-        lens[got] = (*env)->GetArrayLength(env, arr[got]);
-        ptrs[got] = (const uint8_t *)(*env)->GetByteArrayElements(env, arr[got], NULL);
-        if (!ptrs[got]) { ++got; goto done; }   /* OutOfMemoryError pending */
+    if (!ptrs || !lens || !offs) { throw_msg(env, "java/lang/OutOfMemoryError", "mergeFiles"); goto done; }
+    int64_t total = 0;
+    for (jsize i = 0; i < k; ++i) {   /* lengths first, one local ref at a time */
+        jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, files, i);
+        if (!a) { throw_iae(env, "null file"); goto done; }
+        lens[i] = (*env)->GetArrayLength(env, a);
+        offs[i] = total;
+        total += (lens[i] + 63) / 64 * 64;
+        (*env)->DeleteLocalRef(env, a);
+    }
+    uint8_t *arena = (uint8_t *)stage(env, 0, (size_t)total);
+    if (!arena) goto done;
+    for (jsize i = 0; i < k; ++i) {   /* copies (GetByteArrayRegion): no array stays pinned across the merge */
+        jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, files, i);
+        if (lens[i] > 0) (*env)->GetByteArrayRegion(env, a, 0, (jsize)lens[i], (jbyte *)(arena + offs[i]));
+        (*env)->DeleteLocalRef(env, a);
+        ptrs[i] = arena + offs[i];
     }
     int64_t cap = 8 * (lens[0] / 8);
     if (partial) {
         int32_t w; int64_t off;
-        int64_t n0 = ipls_pair_parse(ptrs[0], lens[0], &w, &off);
+        int64_t n0 = LIB(ipls_pair_parse(ptrs[0], lens[0], &w, &off));
         cap = n0 < 0 ? 0 : 8 * n0;
     }
     out = (uint8_t *)malloc((size_t)(cap > 0 ? cap : 1));
     if (!out) { throw_msg(env, "java/lang/OutOfMemoryError", "mergeFiles"); goto done; }
-    int64_t nb = ipls_agg_merge_files(H(h), ptrs, lens, k, partial ? IPLS_HOST_PAIR : IPLS_HOST_BE, out, cap);
+    int64_t nb = LIB(ipls_agg_merge_files(H(h), ptrs, lens, k, partial ? IPLS_HOST_PAIR : IPLS_HOST_BE, out, cap));
     if (nb < 0) {
         throw_for(env, (int)nb, H(h));
     } else {
@@ -481,12 +571,7 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclas
         if (res) (*env)->SetByteArrayRegion(env, res, 0, (jsize)nb, (const jbyte *)out);
     }
 done:
-    for (jsize i = 0; i < got; ++i)
-        if (ptrs[i]) (*env)->ReleaseByteArrayElements(env, arr[i], (jbyte *)ptrs[i], JNI_ABORT);
-    if (arr)
-        for (jsize i = 0; i <= got && i < k; ++i)
-            if (arr[i]) (*env)->DeleteLocalRef(env, arr[i]);
-    free(out); free(lens); free(ptrs); free(arr);
+    free(out); free(offs); free(lens); free(ptrs);
     return res;
 }
 
@@ -495,14 +580,14 @@ JNIEXPORT void JNICALL Java_NativeAggregator_getPartitionsWire(JNIEnv *env, jcla
     (void)c;
     void *dst = direct_span(env, buf, pos, nBytes, 1);
     if (!dst) return;
-    CHECK(ipls_agg_get_partitions(H(h), dst, nBytes / 8, IPLS_HOST_BE_CANON), H(h));
+    CHECK(LIB(ipls_agg_get_partitions(H(h), dst, nBytes / 8, IPLS_HOST_BE_CANON)), H(h));
 }
 
 JNIEXPORT jobject JNICALL Java_NativeAggregator_hostAllocDirect(JNIEnv *env, jclass c, jint bytes) {
     (void)c;
     if (bytes < 0) { throw_iae(env, "negative size"); return NULL; }
     void *p = NULL;
-    int rc = ipls_host_alloc((size_t)bytes, &p);
+    int rc = LIB(ipls_host_alloc((size_t)bytes, &p));
     if (rc < 0) { throw_for(env, rc, NULL); return NULL; }
     return (*env)->NewDirectByteBuffer(env, p, bytes);
 }
@@ -525,7 +610,7 @@ JNIEXPORT void JNICALL Java_NativeAggregator_reduceBatchDevice(JNIEnv *env, jcla
     jlong *held;
     const void *const *b = dev_ptrs(env, ptrs, np, k, &held);
     if (!b) return;
-    int rc = ipls_agg_reduce_batch(H(h), p0, np, b, k, kind, start, target);
+    int rc = LIB(ipls_agg_reduce_batch(H(h), p0, np, b, k, kind, start, target));
     (*env)->ReleaseLongArrayElements(env, ptrs, held, JNI_ABORT);
     CHECK(rc, H(h));
 }
@@ -537,14 +622,14 @@ JNIEXPORT void JNICALL Java_NativeAggregator_reducePartialDevice(JNIEnv *env, jc
     jlong *held;
     const void *const *b = dev_ptrs(env, ptrs, np, k, &held);
     if (!b) return;
-    int rc = ipls_agg_reduce_partial(H(h), slot, p0, np, b, k, kind, start);
+    int rc = LIB(ipls_agg_reduce_partial(H(h), slot, p0, np, b, k, kind, start));
     (*env)->ReleaseLongArrayElements(env, ptrs, held, JNI_ABORT);
     CHECK(rc, H(h));
 }
 
 JNIEXPORT jint JNICALL Java_NativeAggregator_combinePartials(JNIEnv *env, jclass c, jlong h, jint p0, jint np) {
     (void)c;
-    int rc = ipls_agg_combine_partials(H(h), p0, np);
+    int rc = LIB(ipls_agg_combine_partials(H(h), p0, np));
     CHECK(rc, H(h));
     return rc;
 }
@@ -557,12 +642,12 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_publishPartial(JNIEnv *env, j
     jsize ol = origin ? (*env)->GetArrayLength(env, origin) : 0;
     jbyte *o = origin ? (*env)->GetByteArrayElements(env, origin, NULL) : NULL;
     jbyteArray res = NULL;
-    int64_t n = ipls_agg_publish_partial(H(h), p, tgt, a, b, pid, (const uint8_t *)o, ol, NULL, 0, IPLS_HOST_TEXT);
+    int64_t n = LIB(ipls_agg_publish_partial(H(h), p, tgt, a, b, pid, (const uint8_t *)o, ol, NULL, 0, IPLS_HOST_TEXT));
     uint8_t *text = n >= 0 ? (uint8_t *)malloc((size_t)(n > 0 ? n : 1)) : NULL;
     if (n >= 0 && !text) {
         throw_msg(env, "java/lang/OutOfMemoryError", "publish text");
     } else if (n >= 0) {
-        n = ipls_agg_publish_partial(H(h), p, tgt, a, b, pid, (const uint8_t *)o, ol, text, n, IPLS_HOST_TEXT);
+        n = LIB(ipls_agg_publish_partial(H(h), p, tgt, a, b, pid, (const uint8_t *)o, ol, text, n, IPLS_HOST_TEXT));
     }
     if (o) (*env)->ReleaseByteArrayElements(env, origin, o, JNI_ABORT);
     if (n < 0) {
@@ -587,8 +672,8 @@ JNIEXPORT jlong JNICALL Java_NativeAggregator_publishPartialsLayout(JNIEnv *env,
     jlong *o = (*env)->GetLongArrayElements(env, offs, NULL);
     int64_t total = -1;
     if (pp && l && o)
-        total = ipls_agg_publish_partials(H(h), (const int32_t *)pp, n, IPLS_TGT_AGG, 0, NULL, 3, NULL, originLen, NULL,
-                                          0, IPLS_HOST_TEXT, (int64_t *)l, (int64_t *)o);
+        total = LIB(ipls_agg_publish_partials(H(h), (const int32_t *)pp, n, IPLS_TGT_AGG, 0, NULL, 3, NULL, originLen, NULL,
+                                          0, IPLS_HOST_TEXT, (int64_t *)l, (int64_t *)o));
     if (o) (*env)->ReleaseLongArrayElements(env, offs, o, 0);
     if (l) (*env)->ReleaseLongArrayElements(env, lens, l, 0);
     if (pp) (*env)->ReleaseIntArrayElements(env, parts, pp, JNI_ABORT);
@@ -614,8 +699,8 @@ JNIEXPORT void JNICALL Java_NativeAggregator_publishPartialsDirect(JNIEnv *env, 
     jbyte *o = origin ? (*env)->GetByteArrayElements(env, origin, NULL) : NULL;
     int64_t rc = IPLS_E_NOMEM;
     if (pp && bb && (o || !origin))
-        rc = ipls_agg_publish_partials(H(h), (const int32_t *)pp, n, tgt, a, (const int32_t *)bb, pid,
-                                       (const uint8_t *)o, ol, dst, cap, IPLS_HOST_TEXT, NULL, NULL);
+        rc = LIB(ipls_agg_publish_partials(H(h), (const int32_t *)pp, n, tgt, a, (const int32_t *)bb, pid,
+                                       (const uint8_t *)o, ol, dst, cap, IPLS_HOST_TEXT, NULL, NULL));
     if (o) (*env)->ReleaseByteArrayElements(env, origin, o, JNI_ABORT);
     if (bb) (*env)->ReleaseIntArrayElements(env, b, bb, JNI_ABORT);
     if (pp) (*env)->ReleaseIntArrayElements(env, parts, pp, JNI_ABORT);

@@ -14,7 +14,11 @@
  *   - no call other than the release / DeleteLocalRef / ExceptionCheck family
  *     while an exception is pending,
  *   - every Get*ArrayElements / GetPrimitiveArrayCritical released,
- *   - no *ArrayRegion write past the array's end.
+ *   - no *ArrayRegion access past the array's end,
+ *   - no critical region open when the shim calls into libipls_agg (the shim,
+ *     built with -DIPLS_JNI_CALL_HOOK=fj_library_call, reports every library
+ *     call here): such a call may wait on the GPU, and a real JVM cannot
+ *     collect garbage while a critical region is held.
  * tests/test_jni.py drives it through ctypes.
  */
 #include <stdint.h>
@@ -199,6 +203,39 @@ static void JNICALL SetIntArrayRegion(JNIEnv *env, jintArray a, jsize s, jsize l
     (void)env;
     region(a, K_INTS, s, l, b, "SetIntArrayRegion");
 }
+static void JNICALL SetDoubleArrayRegion(JNIEnv *env, jdoubleArray a, jsize s, jsize l, const jdouble *b) {
+    (void)env;
+    region(a, K_DOUBLES, s, l, b, "SetDoubleArrayRegion");
+}
+
+static void region_out(jarray a, int kind, jsize start, jsize len, void *buf, const char *fn) {
+    guarded_call(fn);
+    if (!a || a->kind != kind || start < 0 || len < 0 || start + len > a->n) {
+        violation(fn);   /* a JVM throws ArrayIndexOutOfBoundsException here */
+        return;
+    }
+    memcpy(buf, (char *)a->data + (size_t)start * esize(kind), (size_t)len * esize(kind));
+}
+static void JNICALL GetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize s, jsize l, jbyte *b) {
+    (void)env;
+    region_out(a, K_BYTES, s, l, b, "GetByteArrayRegion");
+}
+static void JNICALL GetDoubleArrayRegion(JNIEnv *env, jdoubleArray a, jsize s, jsize l, jdouble *b) {
+    (void)env;
+    region_out(a, K_DOUBLES, s, l, b, "GetDoubleArrayRegion");
+}
+
+/* The shim's report of a call into libipls_agg (IPLS_JNI_CALL_HOOK). */
+static int g_library_calls;
+JNIEXPORT void fj_library_call(const char *call) {
+    ++g_library_calls;
+    if (g_critical) {
+        char m[160];
+        snprintf(m, sizeof m, "critical region held across a library call: %.100s", call);
+        violation(m);
+    }
+}
+JNIEXPORT int fj_library_calls(void) { return g_library_calls; }
 
 static void *JNICALL GetPrimitiveArrayCritical(JNIEnv *env, jarray a, jboolean *c) {
     (void)env;
@@ -244,7 +281,8 @@ static const struct JNINativeInterface_ g_table = {
     FindClass, ThrowNew, ExceptionCheck, DeleteLocalRef, GetArrayLength, GetObjectArrayElement,
     NewByteArray, NewIntArray, GetByteArrayElements, GetIntArrayElements, GetLongArrayElements,
     ReleaseByteArrayElements, ReleaseIntArrayElements, ReleaseLongArrayElements, SetByteArrayRegion,
-    SetIntArrayRegion, GetPrimitiveArrayCritical, ReleasePrimitiveArrayCritical, NewDirectByteBuffer,
+    SetIntArrayRegion, SetDoubleArrayRegion, GetByteArrayRegion, GetDoubleArrayRegion, GetPrimitiveArrayCritical,
+    ReleasePrimitiveArrayCritical, NewDirectByteBuffer,
     GetDirectBufferAddress, GetDirectBufferCapacity, EnsureLocalCapacity,
 };
 static JNIEnv g_env = &g_table;
@@ -286,3 +324,20 @@ JNIEXPORT void fj_reset_violations(void) {
     g_violations = 0; g_critical = 0; g_pinned = 0; g_last_violation[0] = 0;
     g_local_cap = 16; g_locals = 0;   /* a new native frame */
 }
+
+/* The critical-region rule itself: a library call reported while a region
+ * is open must count as a violation (tests/test_jni.py checks the rule can
+ * fire, so its silence on the shim means something).  Returns the
+ * violations it recorded. */
+JNIEXPORT int fj_selftest_critical_rule(void) {
+    jobject a = fj_new_doubles(NULL, 4);
+    fj_reset_violations();
+    void *p = GetPrimitiveArrayCritical(&g_env, a, NULL);
+    fj_library_call("ipls_agg_accumulate(...)");
+    ReleasePrimitiveArrayCritical(&g_env, a, p, JNI_ABORT);
+    const int v = g_violations;
+    fj_reset_violations();
+    fj_free(a);
+    return v;
+}
+

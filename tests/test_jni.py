@@ -30,6 +30,7 @@ _j = None
 def build():
     BUILD.mkdir(parents=True, exist_ok=True)
     subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-Wall", "-Wextra", "-Werror", "-fPIC", "-shared",
+                    "-DIPLS_JNI_CALL_HOOK=fj_library_call",
                     f"-I{ROOT / 'tests' / 'jni'}", f"-I{ROOT / 'include'}",
                     str(ROOT / "tests" / "jni" / "fake_jvm.c"), str(ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c"),
                     f"-L{AGG}", "-lipls_agg", f"-Wl,-rpath,{AGG}", "-o", str(LIB)], check=True)
@@ -49,7 +50,8 @@ class JVM:
             ("fj_data", vp, [vp]), ("fj_len", ctypes.c_int32, [vp]), ("fj_free", None, [vp]),
             ("fj_exception", ctypes.c_char_p, []), ("fj_exception_msg", ctypes.c_char_p, []), ("fj_clear", None, []),
             ("fj_violations", ctypes.c_int, []), ("fj_last_violation", ctypes.c_char_p, []),
-            ("fj_reset_violations", None, [])]:
+            ("fj_reset_violations", None, []), ("fj_library_calls", ctypes.c_int, []),
+            ("fj_selftest_critical_rule", ctypes.c_int, [])]:
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         self.L = L
@@ -134,6 +136,22 @@ def test_shim_builds_with_werror_and_exports_every_native(jvm):
     out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"Java_NativeAggregator_(\w+)", out))
     assert natives == exported, natives ^ exported
+
+
+def test_no_critical_region_across_a_library_call(jvm):
+    """the shim never holds a GetPrimitiveArrayCritical
+    region while it calls into the library (a call that may wait on the GPU
+    would block a real JVM's GC for that long).  The fake JVM fails any call
+    made with a region open (JVM.call checks fj_violations after every
+    native); this checks the rule can fire, that the shim reports its library
+    calls, and that it has no critical region left at all."""
+    assert jvm.L.fj_selftest_critical_rule() >= 1
+    before = jvm.L.fj_library_calls()
+    r, exc = jvm.call("shardPlan", 4, 2, res=ctypes.c_void_p)
+    assert exc is None and jvm.L.fj_library_calls() > before
+    shim = (ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c").read_text()
+    code = "\n".join(ln for ln in shim.splitlines() if not ln.lstrip().startswith(("*", "/*")))
+    assert "GetPrimitiveArrayCritical" not in code
 
 
 def test_shard_plan_native(jvm):
@@ -476,6 +494,7 @@ def test_shim_under_asan():
     exe = BUILD / "asan_driver"
     subprocess.run(["gcc", "-std=c11", "-O1", "-g", "-Wall", "-Wextra", "-Werror",
                     "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all",
+                    "-DIPLS_JNI_CALL_HOOK=fj_library_call",
                     f"-I{ROOT / 'tests' / 'jni'}", f"-I{ROOT / 'include'}",
                     str(ROOT / "tests" / "jni" / "asan_driver.c"), str(ROOT / "tests" / "jni" / "fake_jvm.c"),
                     str(ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c"),
