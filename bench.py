@@ -979,7 +979,8 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
     return out
 
 
-def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: float) -> dict:
+def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: float, build: dict | None = None,
+              config: str = "C") -> dict:
     """The rest of an aggregation round on the same handle, one launch each:
     AggregatePartition for all partitions (k_finalize: read AGG, write W ->
     16 B/element) and GetPartitions into a device buffer (k_divide: read W,
@@ -1017,9 +1018,16 @@ def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: f
     fused_ms = fe[0].elapsed_time(fe[reps]) / reps
     fused_same = bool(torch.equal(flat.view(torch.int64), ref_flat.view(torch.int64)))
     fused_bytes = P * (K + 1) * L * 8 + 8 * (n_el - P)   # K buckets in, W out, averages out
+    # HBM bytes per launch from the committed PMC passes of this build (as roofline.traffic)
+    fin_t, fin_prov = pmc_traffic(f"{config}-finalize", build or {})
+    div_t, div_prov = pmc_traffic(f"{config}-divide", build or {})
     info = {
         "finalize_ms": round(fin_ms, 4), "finalize_GBps": round(16 * n_el / fin_ms / 1e6, 1),
+        "finalize_frac": round(16 * n_el / fin_ms / 1e6 / HBM_PEAK_GBS, 4),
+        "finalize_algorithmic_bytes": 16 * n_el, "finalize_traffic": fin_t, "finalize_traffic_provenance": fin_prov,
         "divide_ms": round(div_ms, 4), "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
+        "divide_frac": round(16 * (n_el - P) / div_ms / 1e6 / HBM_PEAK_GBS, 4),
+        "divide_algorithmic_bytes": 16 * (n_el - P), "divide_traffic": div_t, "divide_traffic_provenance": div_prov,
         "round_ms": round(kern_ms + fin_ms + div_ms, 4),
         "fused_round_ms": round(fused_ms, 4),
         "fused_round_GBps": round(fused_bytes / fused_ms / 1e6, 1),
@@ -1483,7 +1491,7 @@ def main():
     round_info = None
     if not args.be:
         try:
-            round_info = round_leg(ipls, torch, agg, rows, P, L, K, stream, kern_ms)
+            round_info = round_leg(ipls, torch, agg, rows, P, L, K, stream, kern_ms, build, args.config)
         except Exception as e:   # a side measurement never costs the headline line
             round_info = {"error": f"{type(e).__name__}: {e}"}
 

@@ -209,8 +209,22 @@ def build_info() -> dict:
         info.update(git_rev=None, sources_dirty=None, kernel_src_sha256=None, stamp_matches_so=None)
     else:
         info.update(git_rev=rec.get("git_rev"), sources_dirty=rec.get("sources_dirty"),
-                    kernel_src_sha256=rec.get("kernel_src_sha256"),
+                    kernel_src_sha256=rec.get("kernel_src_sha256"), built_utc=rec.get("built_utc"),
                     stamp_matches_so=rec.get("so_sha256") == info["so_sha256"])
+        # the library's sources travel with the tree: recompute their hash here
+        # and compare it with the one recorded at link time
+        try:
+            import importlib.util
+            root = LIB_PATH.resolve().parent.parent.parent
+            spec = importlib.util.spec_from_file_location("_ipls_build_stamp", root / "tools" / "build_stamp.py")
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            now = mod.lib_src_sha256(root)
+            info["lib_src_sha256"] = rec.get("lib_src_sha256")
+            info["sources_match"] = rec.get("lib_src_sha256") == now if rec.get("lib_src_sha256") else None
+        except Exception as e:   # noqa: BLE001 -- provenance never costs the caller
+            info["sources_match"] = None
+            info["sources_match_error"] = f"{type(e).__name__}: {e}"
     return info
 
 

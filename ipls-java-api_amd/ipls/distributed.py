@@ -217,13 +217,19 @@ def ulp_distance(a, b):
     """Per-element distance in units in the last place between two float64
     tensors: both bit patterns mapped onto one monotone integer line (a
     negative double -x maps to -(bits of x)), then subtracted.  +0.0 and -0.0
-    are 0 apart; NaNs are not expected here (the fold inputs are finite)."""
+    are 0 apart; NaNs are not expected here (the fold inputs are finite).
+    Values of opposite sign far apart (|x| >= 2.0 on both sides) are more
+    than 2^63 - 1 ULP apart: the distance saturates there instead of
+    wrapping in int64."""
     import torch
 
     def line(x):
         i = x.contiguous().view(torch.int64)
         return torch.where(i >= 0, i, -(i & 0x7FFFFFFFFFFFFFFF))
-    return (line(a) - line(b)).abs()
+    la, lb = line(a), line(b)
+    d = la - lb                                              # wraps on overflow
+    over = (((la ^ lb) < 0) & ((la ^ d) < 0)) | (d == torch.iinfo(torch.int64).min)
+    return torch.where(over, torch.full_like(d, torch.iinfo(torch.int64).max), d.abs())
 
 
 def rccl_reduce_ulp(partial, rank: int, world: int, *, dst: int = 0, group=None, keep: bool = False) -> dict | None:

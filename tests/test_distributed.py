@@ -295,6 +295,22 @@ def test_ulp_distance_known_pairs():
     assert ulp_distance(a, b).tolist() == [1, 1, 0, 0, 2, 2, 2]
 
 
+def test_ulp_distance_saturates_for_far_opposite_signs():
+    """opposite signs with |x| >= 2.0 are more than 2^63 - 1 ULP
+    apart; the int64 difference must saturate, not wrap to a small or
+    negative count."""
+    from ipls.distributed import ulp_distance
+    big = 2 ** 63 - 1
+    a = torch.tensor([3.0, -1e300, 2.0, -2.0, 1.0, np.inf], dtype=torch.float64)
+    b = torch.tensor([-3.0, 1e300, -2.0, 2.0, -1.0, -np.inf], dtype=torch.float64)
+    d = ulp_distance(a, b).tolist()
+    assert d[:4] == [big] * 4
+    one = int(np.float64(1.0).view(np.int64))
+    assert d[4] == 2 * one                       # 1.0 and -1.0: 2 x 0x3FF0... fits in int64
+    assert d[5] == big
+    assert all(x >= 0 for x in d)
+
+
 def ulp_worker(rank, world, port, L, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

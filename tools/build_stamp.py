@@ -39,6 +39,19 @@ def kernel_src_sha256(csrc: Path = CSRC) -> str:
     return h.hexdigest()
 
 
+def lib_src_sha256(root: Path = ROOT) -> str:
+    """sha256 over every source the library is linked from (csrc/*, the
+    header, the Makefile), in name order.  The sources travel to the GPU box
+    with the tree, so the box can recompute it and check that the shipped
+    .so was built from exactly the sources beside it (ipls.build_info)."""
+    h = hashlib.sha256()
+    files = sorted(p for p in (root / "ipls-java-api_amd" / "csrc").iterdir() if p.is_file())
+    files += [root / "include" / "ipls_agg.h", root / "ipls-java-api_amd" / "Makefile"]
+    for p in files:
+        h.update(str(p.relative_to(root)).encode() + b"\0" + p.read_bytes())
+    return h.hexdigest()
+
+
 def _git(*args):
     try:
         r = subprocess.run(["git", "-C", str(ROOT), *args], capture_output=True, text=True, timeout=30)
@@ -55,6 +68,7 @@ def main():
         "so": lib.name,
         "so_sha256": sha256_file(lib),
         "kernel_src_sha256": kernel_src_sha256(),
+        "lib_src_sha256": lib_src_sha256(),
         "git_rev": rev,
         "sources_dirty": None if dirty is None else bool(dirty),
         "built_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
