@@ -1179,8 +1179,9 @@ def pmc_traffic(workload_key: str, build: dict):
     every entry carries the build record (ipls.build_info()) of the process the
     counters came from.  Returns (traffic or None, provenance).  The traffic is
     reported only when the entry was taken on this very library (same .so
-    sha256), or on a library built from the same kernel sources (kernel-source
-    sha256 of ipls_kernels.hpp + engine.hip; the .so differs in host code only);
+    sha256), on a library with the same device code (sha256 of the .so's
+    .hip_fatbin section: the same kernel ISA, host code changed), or on one
+    built from the same kernel sources (ipls_kernels.hpp + engine.hip);
     otherwise None with traffic_stale = True."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     prov = {"source": "profiles/pmc_traffic.json", "entry": workload_key, "traffic_stale": True, "match": None}
@@ -1195,6 +1196,8 @@ def pmc_traffic(workload_key: str, build: dict):
     prov.update(entry_git_rev=eb.get("git_rev"), entry_so_sha256=eb.get("so_sha256"), profile=e.get("source"))
     if eb.get("so_sha256") and eb.get("so_sha256") == build.get("so_sha256"):
         prov.update(traffic_stale=False, match="so_sha256")
+    elif eb.get("device_code_sha256") and eb.get("device_code_sha256") == build.get("device_code_sha256"):
+        prov.update(traffic_stale=False, match="device_code_sha256")    # same kernel ISA, host code changed
     elif eb.get("kernel_src_sha256") and eb.get("kernel_src_sha256") == build.get("kernel_src_sha256"):
         prov.update(traffic_stale=False, match="kernel_src_sha256")
     else:

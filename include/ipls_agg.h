@@ -258,8 +258,12 @@ int ipls_agg_other_replica_drop(ipls_agg *h, int p, int32_t aggregator);
  * HashMap (ascending bin of the key hashes under the map's capacity, then
  * insertion order within a bin), then clears the store
  * (Other_Replica_Gradients = new HashMap<>(): capacity reset).
- * participants (nullable, P ints) receives the per-partition download counts
- * (PeerData.Participants).  Returns the number of stored arrays folded, or
+ * participants (nullable, P ints) receives, per partition, what the reference
+ * adds to PeerData.Participants[p]: its put / replace sits inside the element
+ * loop (IPLS.java:1229-1234), so every stored key adds its download count
+ * (Other_Replica_Gradients_Received) once per element -- received * length,
+ * wrapping like Java int.  The Java side adds a nonzero entry to its map
+ * (put if absent, else +=).  Returns the number of stored arrays folded, or
  * IPLS_E_RANGE (nothing folded) if one is longer than its partition. */
 int ipls_agg_collect_replicas(ipls_agg *h, int32_t *participants);
 

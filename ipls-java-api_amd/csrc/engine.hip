@@ -1672,7 +1672,11 @@ int dev_collect_replicas(ipls_dev* h, int32_t* participants, const int32_t* orde
   for (auto& it : seq) {   // IPLS.java:1222-1234: REP[p][j] = REP[p][j] + Other[j], j < Other.length
     const int p = it->first.first;
     const int64_t n = it->second.n;
-    if (participants) participants[p] += it->second.received;   // PeerData.Participants (:1228-1233)
+    // PeerData.Participants (IPLS.java:1229-1234): the put / replace sits INSIDE
+    // the j loop, so the reference adds the key's download count once per
+    // element -- received * n in all, in wrapping int arithmetic
+    if (participants)
+      participants[p] = (int32_t)((uint32_t)participants[p] + (uint32_t)it->second.received * (uint32_t)n);
     if (n > 0) {
       if (int rc = materialize(h, p, IPLS_TGT_REP)) return rc;
       hipLaunchKernelGGL((k_fold_n<false, false>), dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)),

@@ -250,7 +250,8 @@ class IPLS {
   }
 
   // Collect_Replicas (IPLS.java:1217-1241): fold every stored array into
-  // Replicas_Gradients and clear the store; returns PeerData.Participants.
+  // Replicas_Gradients and clear the store; returns the per-partition
+  // increments of PeerData.Participants (received x length per key, :1229-1234).
   std::vector<int32_t> Collect_Replicas() {
     std::vector<int32_t> participants((size_t)cfg_._PARTITIONS);
     check(ipls_agg_collect_replicas(h_.get(), participants.data()), h_.get());

@@ -221,6 +221,7 @@ def build_info() -> dict:
             spec.loader.exec_module(mod)
             now = mod.lib_src_sha256(root)
             info["lib_src_sha256"] = rec.get("lib_src_sha256")
+            info["device_code_sha256"] = mod.device_code_sha256(LIB_PATH)
             info["sources_match"] = rec.get("lib_src_sha256") == now if rec.get("lib_src_sha256") else None
         except Exception as e:   # noqa: BLE001 -- provenance never costs the caller
             info["sources_match"] = None

@@ -378,7 +378,9 @@ class Aggregator:
     def Collect_Replicas(self):
         """IPLS.java:1217-1241: fold every stored Other_Replica_Gradients array
         into REP in the JDK HashMap's key-set order and clear the store.
-        Returns (arrays folded, per-partition download counts = Participants)."""
+        Returns (arrays folded, per-partition Participants increments: each
+        stored key adds received x its length, IPLS.java:1229-1234 updating
+        Participants inside the element loop)."""
         part = (ctypes.c_int32 * max(1, self.n_partitions))()
         k = self._chk(self._lib.ipls_agg_collect_replicas(self._h, part))
         return k, list(part)[:self.n_partitions]

@@ -122,7 +122,10 @@ public final class NativeAggregator implements AutoCloseable {
         return otherReplicaDrop(handle, p, aggregator);
     }
 
-    /** IPLS.Collect_Replicas (IPLS.java:1217-1241); returns Participants per partition. */
+    /** IPLS.Collect_Replicas (IPLS.java:1217-1241); returns, per partition, what the
+     *  reference adds to PeerData.Participants (received x length per key: its
+     *  put/replace runs once per element, :1229-1234).  The caller applies a
+     *  nonzero entry with Participants.merge(p, v, Integer::sum). */
     public int[] collectReplicas() {
         int[] participants = new int[partitions];
         collectReplicas(handle, participants);

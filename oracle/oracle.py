@@ -295,15 +295,18 @@ def other_replica_drop(store: ReplicaStore, partition: int, aggregator) -> bool:
 def collect_replicas(rep: list, store: ReplicaStore, participants: list | None = None) -> int:
     """IPLS.Collect_Replicas, IPLS.java:1217-1241: for the keys of
     new ArrayList<>(Other_Replica_Gradients.keySet()) in that order,
-    REP[p][j] = REP[p][j] + Other[(p, a)][j] for j < len(Other) and
-    Participants[p] += the download count; then the store is a new HashMap."""
+    REP[p][j] = REP[p][j] + Other[(p, a)][j] for j < len(Other); then the
+    store is a new HashMap.  Participants (IPLS.java:1229-1234) is updated
+    inside the j loop: put(p, received) if absent, else += received, once per
+    ELEMENT -- so each key adds received * len(Other), in Java int
+    arithmetic (wrapping at 2^32); an empty array adds nothing."""
     n = 0
     for key in store.map.keys():
         p = key[0]
         arr, received = store.map.get(key, store.hashes[key])
         rep[p][:len(arr)] = rep[p][:len(arr)] + arr
         if participants is not None:
-            participants[p] += received
+            participants[p] = _i32(participants[p] + received * len(arr))   # received, len(arr) times
         n += 1
     store.map = JavaHashMap()
     store.hashes = {}

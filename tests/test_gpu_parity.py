@@ -1109,7 +1109,7 @@ def test_other_replica_gradients_and_collect(ipls, O):
     parts_ref = [0] * P
     n_ref = O.collect_replicas(rep, store, parts_ref)
     n, parts = agg.Collect_Replicas()
-    assert (n, parts) == (n_ref, parts_ref) == (3, [3, 2])
+    assert (n, parts) == (n_ref, parts_ref) == (3, [3 * Ls[0], 2 * Ls[1]])   # received x length (IPLS.java:1229-1234)
     for p in range(P):
         assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}]")
     assert agg.Collect_Replicas() == (0, [0, 0])               # the store was cleared
@@ -1144,7 +1144,7 @@ def test_replica_drop_when_its_partial_arrives(ipls, O):
     parts_ref = [0] * P
     n_ref = O.collect_replicas(rep, store, parts_ref)
     n, parts = agg.Collect_Replicas()
-    assert (n, parts) == (n_ref, parts_ref) == (1, [3, 0])                       # only C's 3 downloads
+    assert (n, parts) == (n_ref, parts_ref) == (1, [3 * L, 0])                   # only C's 3 downloads (x L, per element)
     assert_bits_equal(agg.read(0, ipls.TGT_REP), rep[0], "REP[0] after drop + collect")
     # without the drop B's downloads would have been folded as well
     twice = partial_b + O.reduce([O.synth_bucket(L, 0, k) for k in (70, 71)], L, ipls.START_FIRST) \
@@ -1199,7 +1199,7 @@ def test_collect_replicas_in_java_hashmap_order(ipls, O):
         asc[p] = asc[p] + arrays[(p, a)]
     n_ref = O.collect_replicas(rep, store, [0] * P)
     n, parts = agg.Collect_Replicas()
-    assert n == n_ref == 5 and parts == [3, 2]
+    assert n == n_ref == 5 and parts == [3 * L, 2 * L]
     for p in range(P):
         assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}] (HashMap order)")
     assert any(not np.array_equal(asc[p].view(np.uint64), rep[p].view(np.uint64)) for p in range(P))

@@ -355,7 +355,7 @@ def test_jni_replica_store_drop_and_hashmap_order(jvm, gpu, O):
     n_ref = O.collect_replicas(rep, store, exp)
     parts = jvm.ints([0, 0])
     n, exc = jvm.call("collectReplicas", h, parts, res=ctypes.c_int32)
-    assert exc is None and n == n_ref == 2 and list(jvm.data(parts, np.int32)) == exp == [3, 0]
+    assert exc is None and n == n_ref == 2 and list(jvm.data(parts, np.int32)) == exp == [3 * L, 0]
     out = jvm.bytes_(b"\0" * (8 * L))
     _, exc = jvm.call("finalizePartition", h, 0, out)              # W = AGG (+0.0) + REP
     assert exc is None and jvm.data(out, np.uint8).tobytes() == O.be_encode(0.0 + rep[0])

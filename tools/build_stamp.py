@@ -52,6 +52,32 @@ def lib_src_sha256(root: Path = ROOT) -> str:
     return h.hexdigest()
 
 
+def device_code_sha256(lib: Path):
+    """sha256 of the .hip_fatbin section of the .so: the gfx950 code objects of
+    every kernel, nothing of the host code.  Two builds with the same value
+    run the same kernel ISA, so a PMC count taken on one applies to the other
+    (for the same launch).  Pure-Python ELF64 section walk (no binutils
+    needed on the GPU box); None if the section is missing."""
+    import struct
+    data = Path(lib).read_bytes()
+    if data[:4] != b"\x7fELF" or data[4] != 2:
+        return None
+    e_shoff, = struct.unpack_from("<Q", data, 0x28)
+    e_shentsize, e_shnum, e_shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def sh(i):
+        o = e_shoff + i * e_shentsize
+        name, _typ, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", data, o)
+        return name, off, size
+    _, str_off, _ = sh(e_shstrndx)
+    for i in range(e_shnum):
+        name, off, size = sh(i)
+        end = data.index(b"\0", str_off + name)
+        if data[str_off + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()
+    return None
+
+
 def _git(*args):
     try:
         r = subprocess.run(["git", "-C", str(ROOT), *args], capture_output=True, text=True, timeout=30)
@@ -69,6 +95,7 @@ def main():
         "so_sha256": sha256_file(lib),
         "kernel_src_sha256": kernel_src_sha256(),
         "lib_src_sha256": lib_src_sha256(),
+        "device_code_sha256": device_code_sha256(lib),
         "git_rev": rev,
         "sources_dirty": None if dirty is None else bool(dirty),
         "built_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),

@@ -74,7 +74,8 @@ def main():
              "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                        "KiB*1024, FETCH_SIZE doubled (gfx950 half-count of wide streaming reads)"}
     if builds:
-        d[wl]["build"] = {k: builds[0].get(k) for k in ("so_sha256", "kernel_src_sha256", "git_rev", "sources_dirty")}
+        d[wl]["build"] = {k: builds[0].get(k) for k in ("so_sha256", "kernel_src_sha256", "device_code_sha256",
+                                                         "git_rev", "sources_dirty")}
     if source:
         d[wl]["source"] = source
     out.write_text(json.dumps(d, indent=1) + "\n")
