@@ -227,6 +227,46 @@ int main(int argc, char** argv) {
       CHECK(file == ref, "update_file bytes of AGG + REP");
     });
 
+    run("Other_Replica_Gradients: downloads, a remove, Collect_Replicas in HashMap order", [&] {
+      // three other aggregators of partition 0 whose Pair(0, id) hashes fall
+      // in bins 13, 7 and 2 of the 16-bin HashMap (found with oracle.JavaHashMap;
+      // hashCodes 1951003300, 1951003326, 1951003387): keySet() walks them in
+      // reverse insertion order.  The fourth is dropped: its partial arrived
+      // (Download_Scheduler.java:329-332).
+      PeerData pd;
+      pd._MODEL_SIZE = 60001;
+      pd._PARTITIONS = 1;
+      IPLS ipls(pd, {0});
+      const int64_t L = ipls_oracle_partition_len(60001, 1, 0);
+      const char* ids[4] = {"QmPeer0006", "QmPeer0011", "QmPeer0030", "QmPeerGone"};
+      const double scale[4] = {1e16, 1.0, -1e16, 3.0};
+      std::vector<std::vector<double>> g;
+      for (int a = 0; a < 4; ++a) {
+        g.push_back(synth(L, 0, 20 + a));
+        for (auto& x : g.back()) x *= scale[a];
+        ipls.Other_Replica_Gradients(0, a, ids[a], g.back());
+      }
+      int32_t h0 = 0;
+      check(ipls_java_pair_hash(0, (const uint8_t*)ids[0], 10, &h0), nullptr);
+      CHECK(h0 == 1951003300, "Pair(0, \"QmPeer0006\").hashCode()");
+      CHECK(ipls.Other_Replica_Gradients_remove(0, 3) && !ipls.Other_Replica_Gradients_remove(0, 3), "remove once");
+      auto parts = ipls.Collect_Replicas();
+      CHECK(parts.size() == 1 && parts[0] == (int32_t)(3 * L), "Participants: received x length per key");
+      auto file = ipls.AggregatePartition(0);
+      std::vector<double> rep((size_t)L, 0.0);
+      for (int a : {2, 1, 0})   // keySet() order
+        for (int64_t j = 0; j < L; ++j) rep[j] = rep[j] + g[a][j];
+      std::vector<double> w((size_t)L);
+      for (int64_t j = 0; j < L; ++j) w[j] = 0.0 + rep[j];   // W = AGG (+0.0) + REP
+      std::vector<uint8_t> ref(8 * (size_t)L);
+      ipls_oracle_be_encode(w.data(), L, ref.data());
+      CHECK(file == ref, "W = AGG + REP with REP folded in the HashMap's key order");
+      std::vector<double> asc((size_t)L, 0.0);
+      for (int a : {0, 1, 2})
+        for (int64_t j = 0; j < L; ++j) asc[j] = asc[j] + g[a][j];
+      CHECK(!bits_equal(asc.data(), rep.data(), (size_t)L), "(the ascending order gives other bits)");
+    });
+
     run("gradients from the future -> Update_Client_WaitAck_List", [&] {
       PeerData pd;
       pd._MODEL_SIZE = 50001;

@@ -76,13 +76,14 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_finalize<true, false, BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_fd, arena, tpp);                                                    \
                   }})
-#define DIV(BS, V)                                                                                          \
-  vars.push_back({"divide   BS=" #BS " V=" #V, div_bytes, [=](hipStream_t s) {                              \
+#define DIVX(BS, V, AL, TAG)                                                                                \
+  vars.push_back({"divide   BS=" #BS " V=" #V TAG, div_bytes, [=](hipStream_t s) {                          \
                     const int64_t tile = (int64_t)BS * 2 * V;                                                \
                     const int tpp = (int)((L - 1 + tile - 1) / tile);                                        \
-                    hipLaunchKernelGGL((k_divide<false, false, BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
+                    hipLaunchKernelGGL((k_divide<false, false, BS, V, AL>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_dd, (const double*)arena, model, tpp);                              \
                   }})
+#define DIV(BS, V) DIVX(BS, V, true, "")
   FIN(256, 4);   // shipped
   FIN(256, 8);
   FIN(256, 16);
@@ -91,7 +92,9 @@ int main(int argc, char** argv) {
   FIN(1024, 4);
   FIN(1024, 8);
   FIN(1024, 16);
-  DIV(256, 4);   // shipped
+  DIV(256, 4);   // shipped (16-B loads whatever the alignment, round 4)
+  DIVX(256, 4, false, " 8B");   // round 3: two 8-B loads per lane
+  DIVX(512, 4, true, "");
   DIV(256, 8);
   DIV(256, 16);
   DIV(512, 8);
@@ -100,6 +103,7 @@ int main(int argc, char** argv) {
   DIV(1024, 16);
 #undef FIN
 #undef DIV
+#undef DIVX
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t a, b;

@@ -3,7 +3,7 @@
 # command and the two PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, no
 # trace domains) for every workload whose traffic the bench line reports:
 # C (k_reduce, and the round leg's k_finalize / k_divide / k_round), B, D-be, F.
-# Usage (repo root on the box): tools/gpu_pmc_all.sh TAG
+# Usage (repo root on the box): [CFGS="C B"] [SKIP_TRACE=1] tools/gpu_pmc_all.sh TAG
 set -o pipefail
 TAG=${1:-r04}
 R=$(pwd)
@@ -12,10 +12,12 @@ mkdir -p $O
 export TMPDIR=/tmp
 LEAN="--no-cpu-baseline --no-e2e --no-other-configs --no-per-arrival"
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/trace_C -o run -- \
-  python3 $R/bench.py $LEAN > $O/bench_trace_C.json 2> $O/bench_trace_C.err || exit 13
-echo "trace done" 
-for cfg in C B D F; do
+if [ -z "$SKIP_TRACE" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/trace_C -o run -- \
+    python3 $R/bench.py $LEAN > $O/bench_trace_C.json 2> $O/bench_trace_C.err || exit 13
+  echo "trace done"
+fi
+for cfg in ${CFGS:-C B D F}; do
   extra=""
   [ $cfg = D ] && extra="--be"
   for ctr in FETCH_SIZE WRITE_SIZE; do
