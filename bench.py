@@ -1313,11 +1313,20 @@ def spawn_ranks(n: int) -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
+    def die_with_parent():
+        # a rank must not outlive a parent that was killed outright (SIGKILL
+        # at a driver's time limit): Linux sends it SIGTERM then
+        try:
+            import ctypes
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
+        except Exception:   # noqa: BLE001 -- best effort
+            pass
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IPLS_BENCH_SPAWNED="1")
-        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env,
+                                      preexec_fn=die_with_parent))
 
     def stop_all(*_):
         for p in procs:

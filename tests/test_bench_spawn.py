@@ -68,3 +68,33 @@ def test_watchdog_through_the_spawner():
     assert r.returncode == 3, (r.returncode, r.stderr)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and json.loads(lines[0])["watchdog"]["expired"] is True
+
+
+def test_ranks_die_with_a_killed_parent():
+    """A parent killed outright (SIGKILL at a driver's time limit) leaves no
+    rank behind: each child asked for SIGTERM on its parent's death."""
+    import signal
+    import time
+
+    import psutil
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--watchdog-selftest",
+                          "--replica-timeout", "120"], env=env, cwd=str(ROOT),
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        kids = []
+        for _ in range(100):                       # both ranks started
+            kids = psutil.Process(p.pid).children()
+            if len(kids) == 2:
+                break
+            time.sleep(0.1)
+        assert len(kids) == 2
+        time.sleep(2.0)                            # let them reach the stuck exchange
+        os.kill(p.pid, signal.SIGKILL)
+        p.wait(timeout=30)
+        gone, alive = psutil.wait_procs(kids, timeout=30)
+        assert not alive, [k.pid for k in alive]
+    finally:
+        if p.poll() is None:
+            p.kill()
