@@ -211,7 +211,8 @@ def test_sharded_ingest_indirect_async_and_replicas(ipls, O):
             agg.OtherReplicaGradients(p, a, O.synth_bucket(Ls[p], p, a))
             agg.OtherReplicaGradients(p, a, O.synth_bucket(Ls[p] - 3, p, a + 1))
     c1, c2 = one.Collect_Replicas(), two.Collect_Replicas()
-    assert c1 == c2 and c1[0] == 4 and c1[1] == [2, 2, 0, 4]
+    # Participants increments: received x stored length per key (IPLS.java:1229-1234)
+    assert c1 == c2 and c1[0] == 4 and c1[1] == [2 * Ls[0], 2 * Ls[1], 0, 4 * Ls[3]]
     for p in range(P):
         assert_bits_equal(two.read(p), one.read(p), f"AGG[{p}]")
         assert_bits_equal(two.read(p, ipls.TGT_REP), one.read(p, ipls.TGT_REP), f"REP[{p}]")
