@@ -627,10 +627,7 @@ struct DivDesc {
   int64_t out_off;
 };
 
-#ifndef IPLS_DIV_ALIGNED
-#define IPLS_DIV_ALIGNED 1
-#endif
-template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV, bool ALIGNED = IPLS_DIV_ALIGNED>
+template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV>
 __global__ __launch_bounds__(BS) void k_divide(const DivDesc* __restrict__ parts,
                                                const double* __restrict__ arena,
                                                unsigned long long* __restrict__ out,
@@ -641,12 +638,6 @@ __global__ __launch_bounds__(BS) void k_divide(const DivDesc* __restrict__ parts
   // lines (64 lanes x 16 B = 8 lines), and each lane reads its two W values
   // with 8-B loads (W's alignment relative to the output is arbitrary; reads
   // of partial lines cost little, partial-line writes do).
-  // ALIGNED (round 4): W is read with 16-B loads whatever its alignment to
-  // the output.  When the output's line boundary falls on an odd W index,
-  // each lane loads the aligned pair [i-1, i], keeps its high half and takes
-  // w[i+1] as the low half of the next lane's pair (__shfl_down); the wave's
-  // last lane loads that one double itself.  Two 8-B non-temporal loads of
-  // the same 16 B (the round-3 form) fetched 1.5 % of W twice (PMC).
   constexpr int kBlock = BS;
   constexpr int kV = V;
   constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
@@ -675,40 +666,11 @@ __global__ __launch_bounds__(BS) void k_divide(const DivDesc* __restrict__ parts
   if (base >= n) return;
   if (base + kTile <= n) {
     double x[kV][2];
-    if constexpr (ALIGNED) {
-      if ((((uintptr_t)(w + base)) & 15) == 0) {   // uniform per block
 #pragma unroll
-        for (int v = 0; v < kV; ++v) {
-          const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
-          const d2 a = __builtin_bit_cast(d2, __builtin_nontemporal_load((gcu2)(w + i)));
-          x[v][0] = a.x;
-          x[v][1] = a.y;
-        }
-      } else {
-        u2 a[kV];
-#pragma unroll
-        for (int v = 0; v < kV; ++v) {
-          const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
-          a[v] = __builtin_nontemporal_load((gcu2)(w + i - 1));   // [i-1, i]
-        }
-        const bool last = (threadIdx.x & 63) == 63;
-#pragma unroll
-        for (int v = 0; v < kV; ++v) {
-          const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
-          const unsigned long long lo = a[v].x;
-          unsigned long long nx = __shfl_down(lo, 1, 64);          // w[i+1] = next lane's low half
-          if (last) nx = *(const __attribute__((address_space(1))) unsigned long long*)(w + i + 1);
-          x[v][0] = __builtin_bit_cast(double, (unsigned long long)a[v].y);
-          x[v][1] = __builtin_bit_cast(double, nx);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int v = 0; v < kV; ++v) {
-        const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
-        x[v][0] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i));
-        x[v][1] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i + 1));
-      }
+    for (int v = 0; v < kV; ++v) {
+      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      x[v][0] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i));
+      x[v][1] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i + 1));
     }
 #pragma unroll
     for (int v = 0; v < kV; ++v) {

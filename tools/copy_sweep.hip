@@ -31,6 +31,106 @@
 
 using namespace ipls;
 
+namespace ipls {
+// The round-4 A/B form of k_divide (not shipped): ALIGNED = true reads W with
+// 16-B loads whatever its alignment to the output; false is the shipped form.
+template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV, bool ALIGNED = false>
+__global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ parts,
+                                               const double* __restrict__ arena,
+                                               unsigned long long* __restrict__ out,
+                                               int tiles_per_part) {
+  // The flat output offset p*chunk is arbitrary, so the tiles are laid over
+  // the OUTPUT: block 0 first writes the `head` elements up to the first 128-B
+  // line boundary of this partition's output, then every wave stores whole
+  // lines (64 lanes x 16 B = 8 lines), and each lane reads its two W values
+  // with 8-B loads (W's alignment relative to the output is arbitrary; reads
+  // of partial lines cost little, partial-line writes do).
+  // ALIGNED (the round-4 A/B): W read with 16-B loads whatever
+  // its alignment to the output -- with the output's line boundary on an odd
+  // W index, each lane loads the aligned pair [i-1, i], keeps its high half
+  // and takes w[i+1] from the next lane's pair (__shfl_down; the wave's last
+  // lane loads it itself).  The shipped two 8-B loads show 1.5 % more read
+  // traffic than W's bytes (PMC), but the 16-B form reads 3.9 % more and
+  // runs 6-8 % slower (tools/copy_sweep.hip, profiles/r04/d/).
+  constexpr int kBlock = BS;
+  constexpr int kV = V;
+  constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
+  const int q = blockIdx.x / tiles_per_part;
+  const int t = blockIdx.x - q * tiles_per_part;
+  const DivDesc d = parts[q];
+  const int64_t n = d.len - 1;
+  const double* w = arena + d.w_off;
+  const double cnt = w[d.len - 1];
+  // Math.pow(10,12) * W[last] (IPLS.java:1167): 1e12 is exact, product rounded once.
+  const double den = SECURE ? 1e12 * cnt : cnt;
+  auto f = [&](double x) -> unsigned long long {
+    const double y = (cnt == 0.0) ? x : x / den;
+    unsigned long long bits = __builtin_bit_cast(unsigned long long, y);
+    if constexpr (OUT_BE) {
+      if (y != y) bits = 0x7ff8000000000000ULL;
+      bits = __builtin_bswap64(bits);
+    }
+    return bits;
+  };
+  unsigned long long* o = out + d.out_off;
+  const int64_t to_line = (16 - (int64_t)(((uintptr_t)o >> 3) & 15)) & 15;   // elements to a 128-B boundary
+  const int64_t head = to_line < n ? to_line : n;
+  if (t == 0 && threadIdx.x < head) o[threadIdx.x] = f(w[threadIdx.x]);
+  const int64_t base = (int64_t)t * kTile + head;
+  if (base >= n) return;
+  if (base + kTile <= n) {
+    double x[kV][2];
+    if constexpr (ALIGNED) {
+      if ((((uintptr_t)(w + base)) & 15) == 0) {   // uniform per block
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+          const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+          const d2 a = __builtin_bit_cast(d2, __builtin_nontemporal_load((gcu2)(w + i)));
+          x[v][0] = a.x;
+          x[v][1] = a.y;
+        }
+      } else {
+        u2 a[kV];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+          const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+          a[v] = __builtin_nontemporal_load((gcu2)(w + i - 1));   // [i-1, i]
+        }
+        const bool last = (threadIdx.x & 63) == 63;
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+          const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+          const unsigned long long lo = a[v].x;
+          unsigned long long nx = __shfl_down(lo, 1, 64);          // w[i+1] = next lane's low half
+          if (last) nx = *(const __attribute__((address_space(1))) unsigned long long*)(w + i + 1);
+          x[v][0] = __builtin_bit_cast(double, (unsigned long long)a[v].y);
+          x[v][1] = __builtin_bit_cast(double, nx);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < kV; ++v) {
+        const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+        x[v][0] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i));
+        x[v][1] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i + 1));
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < kV; ++v) {
+      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      u2 v2;
+      v2.x = f(x[v][0]);
+      v2.y = f(x[v][1]);
+      __builtin_nontemporal_store(v2, (gu2)(o + i));
+    }
+    return;
+  }
+  for (int64_t i = base + threadIdx.x; i < n; i += kBlock) o[i] = f(w[i]);
+}
+
+// ---------------------------------------------------------------------------
+}  // namespace ipls
+
 struct Var {
   std::string name;
   double bytes;
@@ -80,10 +180,10 @@ int main(int argc, char** argv) {
   vars.push_back({"divide   BS=" #BS " V=" #V TAG, div_bytes, [=](hipStream_t s) {                          \
                     const int64_t tile = (int64_t)BS * 2 * V;                                                \
                     const int tpp = (int)((L - 1 + tile - 1) / tile);                                        \
-                    hipLaunchKernelGGL((k_divide<false, false, BS, V, AL>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
+                    hipLaunchKernelGGL((k_divide_ab<false, false, BS, V, AL>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_dd, (const double*)arena, model, tpp);                              \
                   }})
-#define DIV(BS, V) DIVX(BS, V, true, "")
+#define DIV(BS, V) DIVX(BS, V, false, "")
   FIN(256, 4);   // shipped
   FIN(256, 8);
   FIN(256, 16);
@@ -92,9 +192,9 @@ int main(int argc, char** argv) {
   FIN(1024, 4);
   FIN(1024, 8);
   FIN(1024, 16);
-  DIV(256, 4);   // shipped (16-B loads whatever the alignment, round 4)
-  DIVX(256, 4, false, " 8B");   // round 3: two 8-B loads per lane
-  DIVX(512, 4, true, "");
+  DIVX(256, 4, false, " 8B");   // shipped: two 8-B loads per lane
+  DIVX(256, 4, true, " 16B");   // round-4 A/B: 16-B loads whatever the alignment
+  DIVX(512, 4, true, " 16B");
   DIV(256, 8);
   DIV(256, 16);
   DIV(512, 8);
