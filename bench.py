@@ -1297,6 +1297,16 @@ def watchdog_selftest(args) -> None:
         print(json.dumps(out), flush=True)
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One stderr line per finished leg (rank-tagged, seconds since start): a
+    long run keeps showing that it is alive, and a stuck leg is named."""
+    print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - _T0:.1f}s] {msg}", file=sys.stderr,
+          flush=True)
+
+
 def spawn_ranks(n: int) -> int:
     """`python3 bench.py --gpus N` with N > 1 and no launcher (WORLD_SIZE
     unset): start the N rank processes here, one per GPU, the way torchrun
@@ -1473,6 +1483,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = float(t.item())
 
+    progress(f"headline: {args.steps} steps in {dt:.3f} s")
     bytes_step = P * (K + 1) * L * 8
     total_bytes = bytes_step * args.steps * world
     value = total_bytes / dt_max / 1e9
@@ -1558,6 +1569,8 @@ def main():
                 return fn(*a, **kw)
             except Exception as e:   # noqa: BLE001
                 return {"error": f"{type(e).__name__}: {e}"}
+            finally:
+                progress(f"{fn.__name__} done")
         if world == 1 and not args.be:
             out["publish"] = side(publish_leg, ipls, torch, agg, stream, L, verify=not args.no_verify)
         if world == 1 and not args.be and not args.no_per_arrival:
@@ -1599,6 +1612,7 @@ def main():
         dog.start()
         stage = dog.stage
         if not args.no_replica_leg:
+            progress(f"{stage[0]} done; starting replica_exchange" if stage[0] != "replica_exchange" else "starting replica_exchange")
             stage[0] = "replica_exchange"
             try:
                 leg = replica_exchange(ipls, agg, rows, P, L, K, rank, world, local, args.replica_reps,
@@ -1608,6 +1622,7 @@ def main():
             if out is not None:
                 out["replica_exchange"] = leg
         if not args.no_ulp_leg:
+            progress(f"{stage[0]} done; starting rccl_reduce_ulp" if stage[0] != "rccl_reduce_ulp" else "starting rccl_reduce_ulp")
             stage[0] = "rccl_reduce_ulp"
             try:
                 ul = rccl_reduce_leg(ipls, torch, dist, rank, world, local, L, args.replica_reps,
@@ -1617,6 +1632,7 @@ def main():
             if out is not None:
                 out["rccl_reduce_ulp"] = ul
         if not args.no_strong_leg and not args.strong:
+            progress(f"{stage[0]} done; starting strong_scaling_D" if stage[0] != "strong_scaling_D" else "starting strong_scaling_D")
             stage[0] = "strong_scaling_D"
             del arena, rows
             torch.cuda.empty_cache()
@@ -1627,6 +1643,7 @@ def main():
             if out is not None:
                 out["strong_scaling_D"] = sl
         if not args.no_e2e:
+            progress(f"{stage[0]} done; starting host_inclusive_multi" if stage[0] != "host_inclusive_multi" else "starting host_inclusive_multi")
             stage[0] = "host_inclusive_multi"
             if "arena" in locals():
                 del arena, rows
@@ -1643,6 +1660,7 @@ def main():
             # rank 0 drives every GPU through ONE C-ABI handle (what a JVM would
             # do); the other ranks wait on a host-side (gloo) barrier, so no
             # spinning collective kernel shares their GPUs with the leg
+            progress(f"{stage[0]} done; starting c_abi_multi_gpu" if stage[0] != "c_abi_multi_gpu" else "starting c_abi_multi_gpu")
             stage[0] = "c_abi_multi_gpu"
             if "arena" in locals():
                 del arena, rows
