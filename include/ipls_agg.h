@@ -267,6 +267,14 @@ int ipls_agg_other_replica_drop(ipls_agg *h, int p, int32_t aggregator);
  * IPLS_E_RANGE (nothing folded) if one is longer than its partition. */
 int ipls_agg_collect_replicas(ipls_agg *h, int32_t *participants);
 
+/* The order Collect_Replicas would fold the stored keys in right now, as
+ * (partition, aggregator) pairs: pairs[2i], pairs[2i+1] for i < the returned
+ * count (at most max_pairs written; pairs may be NULL to ask for the count).
+ * A diagnostic for a Java caller to check the library's HashMap model against
+ * its own `new ArrayList<>(Other_Replica_Gradients.keySet())`.  *capacity
+ * (nullable) receives the model's table capacity (0 after new HashMap<>()). */
+int ipls_agg_replica_order(ipls_agg *h, int32_t *pairs, int max_pairs, int32_t *capacity);
+
 /* Batched fixed-order fold, ONE kernel launch for n_parts partitions:
  *   for q in [0,n_parts): target[p_first+q] = fold(start_mode; bufs[q*k + 0..k-1])
  * bufs are device pointers (DEV_F64 or DEV_BE), each at least L_p long.

@@ -747,6 +747,19 @@ int ipls_agg_collect_replicas(ipls_agg* H, int32_t* participants) {
   return total;
 }
 
+int ipls_agg_replica_order(ipls_agg* H, int32_t* pairs, int max_pairs, int32_t* capacity) {
+  if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
+  if (max_pairs < 0 || (max_pairs > 0 && !pairs)) return ferr(H, IPLS_E_INVAL, "bad pairs buffer");
+  std::lock_guard<std::mutex> lk(H->rep_mu);
+  const auto ord = H->rep_order.order();
+  for (size_t i = 0; i < ord.size() && (int)i < max_pairs; ++i) {
+    pairs[2 * i] = ord[i].first;
+    pairs[2 * i + 1] = ord[i].second;
+  }
+  if (capacity) *capacity = (int32_t)H->rep_order.capacity();
+  return (int)ord.size();
+}
+
 int ipls_agg_reduce_batch(ipls_agg* H, int p_first, int n_parts, const void* const* bufs, int k, int src_kind,
                           int start_mode, int target) {
   KeepDevice keep_device;

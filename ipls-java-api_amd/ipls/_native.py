@@ -103,6 +103,7 @@ SIGNATURES = {
     "ipls_agg_other_replica_keyed": (_i, [_vp, _i, _i32, _i32, _vp, _i64, _i]),
     "ipls_agg_other_replica_drop": (_i, [_vp, _i, _i32]),
     "ipls_java_pair_hash": (_i, [_i32, _vp, _i64, _P(_i32)]),
+    "ipls_agg_replica_order": (_i, [_vp, _P(_i32), _i, _P(_i32)]),
     "ipls_agg_collect_replicas": (_i, [_vp, _P(_i32)]),
     "ipls_agg_ingest_pubsub": (_i, [_vp, _i, _P(_vp), _P(_i64), _i, _i, _P(_i32), _P(_i32)]),
     "ipls_agg_blend": (_i, [_vp, _i, _i, _vp, _i64, _i, ctypes.c_double, ctypes.c_double]),

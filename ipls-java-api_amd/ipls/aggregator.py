@@ -375,6 +375,16 @@ class Aggregator:
         collected.  True if the key was stored."""
         return self._chk(self._lib.ipls_agg_other_replica_drop(self._h, partition, aggregator)) == 1
 
+    def replica_order(self):
+        """(keys, capacity): the (partition, aggregator) order Collect_Replicas
+        would fold in now -- the library's model of the JDK HashMap's keySet()
+        order -- and the model's table capacity."""
+        n = self._chk(self._lib.ipls_agg_replica_order(self._h, None, 0, None))
+        buf = (ctypes.c_int32 * max(2, 2 * n))()
+        cap = ctypes.c_int32()
+        n = self._chk(self._lib.ipls_agg_replica_order(self._h, buf, n, ctypes.byref(cap)))
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)], cap.value
+
     def Collect_Replicas(self):
         """IPLS.java:1217-1241: fold every stored Other_Replica_Gradients array
         into REP in the JDK HashMap's key-set order and clear the store.

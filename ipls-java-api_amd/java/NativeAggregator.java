@@ -122,6 +122,14 @@ public final class NativeAggregator implements AutoCloseable {
         return otherReplicaDrop(handle, p, aggregator);
     }
 
+    /** The (partition, aggregator) order collectReplicas() would fold in now,
+     *  {p0, a0, p1, a1, ...}: compare it with the keys of
+     *  new ArrayList<>(PeerData.Other_Replica_Gradients.keySet()) mapped to
+     *  aggregator indices to check the native HashMap model in a real JVM. */
+    public int[] replicaKeyOrder() {
+        return replicaKeyOrder(handle);
+    }
+
     /** IPLS.Collect_Replicas (IPLS.java:1217-1241); returns, per partition, what the
      *  reference adds to PeerData.Participants (received x length per key: its
      *  put/replace runs once per element, :1229-1234).  The caller applies a
@@ -301,6 +309,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void otherReplicaDirect(long h, int p, int aggregator, int keyHash, ByteBuffer buf, int pos,
                                                   long n);
     private static native boolean otherReplicaDrop(long h, int p, int aggregator);
+    private static native int[] replicaKeyOrder(long h);
     private static native int collectReplicas(long h, int[] participants);
     private static native void getPartitionsWire(long h, ByteBuffer direct, int pos, long nBytes);
     private static native ByteBuffer hostAllocDirect(int bytes);

@@ -479,6 +479,26 @@ JNIEXPORT jboolean JNICALL Java_NativeAggregator_otherReplicaDrop(JNIEnv *env, j
     return rc == 1 ? JNI_TRUE : JNI_FALSE;
 }
 
+/* The library's Collect_Replicas order as {p0, a0, p1, a1, ...} (a check of
+ * its HashMap model against the JVM's own keySet() order). */
+JNIEXPORT jintArray JNICALL Java_NativeAggregator_replicaKeyOrder(JNIEnv *env, jclass c, jlong h) {
+    (void)c;
+    int n = LIB(ipls_agg_replica_order(H(h), NULL, 0, NULL));
+    if (n < 0) { throw_for(env, n, H(h)); return NULL; }
+    int32_t *pairs = (int32_t *)malloc((size_t)(n > 0 ? 2 * n : 2) * sizeof(int32_t));
+    if (!pairs) { throw_msg(env, "java/lang/OutOfMemoryError", "replicaKeyOrder"); return NULL; }
+    n = LIB(ipls_agg_replica_order(H(h), pairs, n, NULL));
+    jintArray res = NULL;
+    if (n < 0) {
+        throw_for(env, n, H(h));
+    } else {
+        res = (*env)->NewIntArray(env, 2 * n);
+        if (res) (*env)->SetIntArrayRegion(env, res, 0, 2 * n, (const jint *)pairs);
+    }
+    free(pairs);
+    return res;
+}
+
 JNIEXPORT jint JNICALL Java_NativeAggregator_collectReplicas(JNIEnv *env, jclass c, jlong h, jintArray out) {
     (void)c;
     /* the library writes one count per partition: out.length >= P, i.e.

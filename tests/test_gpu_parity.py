@@ -1226,6 +1226,8 @@ def test_collect_replicas_order_after_resize_and_drops(ipls, O):
             kh = O.java_pair_hash(p, f"12D3KooW{a}{'x' * a}")
             agg.OtherReplicaGradients(p, a, g, key_hash=kh)
             O.other_replica_add(store, p, a, g, key_hash=kh)
+            if i % 10 == 9:                       # the library's model vs the simulated JDK table
+                assert agg.replica_order() == (store.map.keys(), len(store.map.table) if store.map.table else 0)
         assert len(store.map.table) >= 32 and not store.map.tree_bin
         exp_parts = [0] * P
         n_ref = O.collect_replicas(rep, store, exp_parts)

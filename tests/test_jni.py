@@ -344,6 +344,8 @@ def test_jni_replica_store_drop_and_hashmap_order(jvm, gpu, O):
         _, exc = jvm.call("otherReplicaDirect", h, 0, a, kh, buf, 0, L64(L))
         assert exc is None
         O.other_replica_add(store, 0, a, g, key_hash=kh)
+    r, exc = jvm.call("replicaKeyOrder", h, res=ctypes.c_void_p)
+    assert exc is None and [tuple(x) for x in jvm.data(r, np.int32).reshape(-1, 2)] == store.map.keys()
     r, exc = jvm.call("otherReplicaDrop", h, 0, 2, res=ctypes.c_bool)
     assert exc is None and r is True and O.other_replica_drop(store, 0, 2)
     r, exc = jvm.call("otherReplicaDrop", h, 1, 2, res=ctypes.c_bool)
