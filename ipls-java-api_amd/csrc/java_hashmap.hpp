@@ -39,6 +39,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <map>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -110,21 +111,27 @@ class JavaHashOrder {
 
   // Other_Replica_Gradients.put(key, array) of an absent key (HashMap.putVal).
   void put_new(const Key& k, int32_t hash) {
-    if (cap_ == 0) cap_ = 16;                       // resize() of the empty table
+    if (cap_ == 0) set_capacity(16);                // resize() of the empty table
     const uint32_t b = bin(hash, cap_);
-    int64_t chain = 0;                              // keys already in that bin
-    for (const auto& e : keys_)
-      if (bin(e.second.hash, cap_) == b) ++chain;
+    const int64_t chain = bins_[b];                 // keys already in that bin
     keys_[k] = E{hash, seq_++};
+    ++bins_[b];
     if (chain >= 8) {                               // binCount >= TREEIFY_THRESHOLD - 1
-      if (cap_ < 64) cap_ *= 2;                     // treeifyBin: resize instead
+      if (cap_ < 64) set_capacity(cap_ * 2);        // treeifyBin: resize instead
       else tree_bin_ = true;
     }
-    if ((int64_t)keys_.size() > cap_ / 4 * 3) cap_ *= 2;   // ++size > threshold
+    if ((int64_t)keys_.size() > cap_ / 4 * 3) set_capacity(cap_ * 2);   // ++size > threshold
   }
 
   // Other_Replica_Gradients.remove(key) (removeNode): the capacity stays.
-  bool remove(const Key& k) { return keys_.erase(k) != 0; }
+  bool remove(const Key& k) {
+    auto it = keys_.find(k);
+    if (it == keys_.end()) return false;
+    auto b = bins_.find(bin(it->second.hash, cap_));
+    if (b != bins_.end() && --b->second == 0) bins_.erase(b);
+    keys_.erase(it);
+    return true;
+  }
 
   // new ArrayList<>(keySet()): ascending bin, insertion order within a bin.
   std::vector<Key> order() const {
@@ -141,6 +148,7 @@ class JavaHashOrder {
   // Other_Replica_Gradients = new HashMap<>() (IPLS.java:1238)
   void clear() {
     keys_.clear();
+    bins_.clear();
     cap_ = 0;
     tree_bin_ = false;
   }
@@ -154,11 +162,18 @@ class JavaHashOrder {
     int32_t hash;
     uint64_t seq;
   };
+  // a resize: the per-bin key counts under the new capacity (amortised O(1) per put)
+  void set_capacity(int64_t cap) {
+    cap_ = cap;
+    bins_.clear();
+    for (const auto& e : keys_) ++bins_[bin(e.second.hash, cap_)];
+  }
   static uint32_t bin(int32_t h, int64_t cap) {
     const uint32_t u = (uint32_t)h;
     return (u ^ (u >> 16)) & (uint32_t)(cap - 1);
   }
   std::map<Key, E> keys_;
+  std::unordered_map<uint32_t, int64_t> bins_;   // keys per bin under cap_
   int64_t cap_ = 0;
   uint64_t seq_ = 0;
   bool tree_bin_ = false;
