@@ -4,9 +4,10 @@
 // in INTEGRATION.md.  Not compiled in this image (no JDK); the C half is
 // ipls-java-api_amd/jni/ipls_jni.c.
 //
-// Arrays are passed as primitive arrays (pinned with GetPrimitiveArrayCritical)
-// or as direct ByteBuffers (zero copy; allocate them with hostAlloc() so the
-// library DMA's straight from them).
+// Arrays are passed as primitive arrays (the shim copies them with
+// Get/Set<T>ArrayRegion: never pinned across a library call, so the GC keeps
+// running) or as direct ByteBuffers (zero copy; allocate them with hostAlloc()
+// so the library DMA's straight from them).
 
 import java.nio.ByteBuffer;
 
