@@ -1500,6 +1500,61 @@ def test_concurrent_callers_one_handle(ipls, O, devices):
     agg.close()
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_concurrent_replica_store(ipls, O, devices):
+    """Download_Scheduler threads store and drop other aggregators' downloads
+    concurrently (Download_Scheduler.java:215-268, 329-332 under com_mtx).
+    Four threads, each on its own partitions: the store never loses or
+    mixes an array, the reported key order (the HashMap model) is ascending
+    in bin under its capacity, and Collect_Replicas folds exactly that order,
+    bit-exact."""
+    import threading
+    P, L, T = 8, 20011, 4
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
+    ids = [f"12D3KooWConc{a}" for a in range(6)]
+    live = [dict() for _ in range(T)]          # per thread: (p, a) -> stored array
+    errors = []
+
+    def worker(w):
+        rng = np.random.default_rng(700 + w)
+        mine = [p for p in range(P) if p % T == w]
+        try:
+            for j in range(50):
+                p, a = mine[j % len(mine)], int(rng.integers(0, len(ids)))
+                if rng.integers(0, 4) == 0:
+                    assert agg.OtherReplicaDrop(p, a) == ((p, a) in live[w])
+                    live[w].pop((p, a), None)
+                    continue
+                g = O.synth_bucket(L, p, 100 * w + j) * float(10.0 ** rng.integers(-6, 7))
+                agg.OtherReplicaGradients(p, a, g, key_hash=O.java_pair_hash(p, ids[a]))
+                if (p, a) in live[w]:
+                    live[w][(p, a)] = live[w][(p, a)] + g
+                else:
+                    live[w][(p, a)] = g.copy()
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    ths = [threading.Thread(target=worker, args=(w,)) for w in range(T)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    stored = {k: v for d in live for k, v in d.items()}
+    order, cap = agg.replica_order()
+    assert sorted(order) == sorted(stored)
+    bins = [O.JavaHashMap.spread(O.java_pair_hash(p, ids[a])) & (cap - 1) for p, a in order]
+    assert bins == sorted(bins)
+    rep = [np.zeros(L) for _ in range(P)]
+    for p, a in order:
+        rep[p] = rep[p] + stored[(p, a)]
+    n, _ = agg.Collect_Replicas()
+    assert n == len(stored)
+    for p in range(P):
+        assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}]")
+    agg.close()
+
+
 def test_partial_update_pair_files(ipls, O):
     """-i 1 partial updates: commit_partial_update's Pair<Integer,double[]>
     bytes (IPLS_Comm.java:51-61) from AGG on the device; a replica's Pair
