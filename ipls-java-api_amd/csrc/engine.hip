@@ -1605,23 +1605,26 @@ int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, i
   const unsigned long long* d;
   bool be;
   if (int rc = flat_to_device(h, src, n, src_kind, &d, &be)) return rc;
-  unsigned long long* dst;
-  if (first) {   // Other.put(key, GetParameters(Hash)): a new array of the file's length (:263)
-    HIP_TRY(h, hipMalloc(&dst, (size_t)std::max<int64_t>(n, 1) * 8));
-    h->other[key] = ipls_dev::OtherRep{dst, n, 1};
-  } else {
-    dst = it->second.d;
-    it->second.received += 1;   // Other_Replica_Gradients_Received + 1 (:260)
-  }
+  unsigned long long* dst = first ? nullptr : it->second.d;
+  // Other.put(key, GetParameters(Hash)): a new array of the file's length (:263)
+  if (first) HIP_TRY(h, hipMalloc(&dst, (size_t)std::max<int64_t>(n, 1) * 8));
+  hipError_t e = hipSuccess;
   if (n > 0) {
     const dim3 g(std::min<unsigned>(blocks_for(n, kBlock), 4096));
 #define FN(B, F) hipLaunchKernelGGL((k_fold_n<B, F>), g, dim3(kBlock), 0, h->stream, dst, d, n)
     if (be) { if (first) FN(true, true); else FN(true, false); }
     else { if (first) FN(false, true); else FN(false, false); }
 #undef FN
-    HIP_TRY(h, hipGetLastError());
+    e = hipGetLastError();
   }
-  if (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE) HIP_TRY(h, hipStreamSynchronize(h->stream));
+  if (e == hipSuccess && (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE)) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) {   // the store is left as it was (the front's key model relies on it)
+    (void)hipGetLastError();
+    if (first) hipFree(dst);
+    return fail(h, IPLS_E_DEVICE, "replica fold failed: %s", hipGetErrorString(e));
+  }
+  if (first) h->other[key] = ipls_dev::OtherRep{dst, n, 1};
+  else it->second.received += 1;   // Other_Replica_Gradients_Received + 1 (:260)
   return IPLS_OK;
 }
 

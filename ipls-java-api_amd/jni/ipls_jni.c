@@ -362,6 +362,7 @@ JNIEXPORT jint JNICALL Java_NativeAggregator_ingestTexts(JNIEnv *env, jclass c, 
         jbyteArray t = (jbyteArray)(*env)->GetObjectArrayElement(env, msgs, i);
         if (len[i] > 0) (*env)->GetByteArrayRegion(env, t, 0, (jsize)len[i], (jbyte *)(arena + off[i]));
         (*env)->DeleteLocalRef(env, t);
+        if ((*env)->ExceptionCheck(env)) goto out;   /* the array changed under us (AIOOBE pending) */
         ptr[i] = arena + off[i];
     }
     if (parts) {
@@ -576,6 +577,7 @@ JNIEXPORT jbyteArray JNICALL Java_NativeAggregator_mergeFiles(JNIEnv *env, jclas
         jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, files, i);
         if (lens[i] > 0) (*env)->GetByteArrayRegion(env, a, 0, (jsize)lens[i], (jbyte *)(arena + offs[i]));
         (*env)->DeleteLocalRef(env, a);
+        if ((*env)->ExceptionCheck(env)) goto done;   /* the array changed under us (AIOOBE pending) */
         ptrs[i] = arena + offs[i];
     }
     int64_t cap = 8 * (lens[0] / 8);
