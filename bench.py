@@ -257,6 +257,14 @@ def f_stream_leg(ipls, torch, device: int, P: int = 16, L: int = 8388608, K: int
     from concurrent.futures import ThreadPoolExecutor
     nb = 8 * L
     N = P * K
+    try:   # the pool is faulted in page by page: never let it run the host out of memory
+        import psutil
+        avail = psutil.virtual_memory().available
+        if avail < 1.25 * (N + ring + P) * nb:
+            return {"error": f"skipped: {avail / 2**30:.0f} GiB of host memory available, "
+                             f"{1.25 * (N + ring + P) * nb / 2**30:.0f} GiB needed"}
+    except ImportError:
+        pass
     t_prep = time.perf_counter()
     pool = torch.empty(N * nb, dtype=torch.uint8)           # pageable host bytes: every bucket's `ipfs cat`
     tmp = torch.empty(nb, dtype=torch.uint8, device=torch.device("cuda", device))
