@@ -137,3 +137,39 @@ def test_front_model_matches_jdk_table_simulation(O, seed, nbits):
         assert got == keys
         compared += 1
     assert compared > 50
+
+
+def test_golden_java_order_cases(O):
+    """tests/golden/java_order_expected.txt is the oracle's answer to
+    java_order_cases.txt (tests/golden/make_java_order.py); the same text is
+    what tests/java/PinJavaOrder.java prints from a real JVM, so on a host
+    with a JDK a diff pins the restatement.  Here: the oracle still gives the
+    committed answer, and so does the library's own model (the C++ driver fed
+    the same keys and hashes)."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_java_order as G
+    cases = (ROOT / "tests" / "golden" / "java_order_cases.txt").read_text(encoding="utf-8").splitlines()
+    want = (ROOT / "tests" / "golden" / "java_order_expected.txt").read_text(encoding="utf-8").splitlines()
+    assert G.expected(cases) == want
+    # the library's model: keys as (p, int index of the ID), hashes from the library itself
+    import ipls
+    _build_driver()
+    ids, cmds, present = {}, [], set()
+    for ln in cases:
+        f = ln.split(" ")
+        if f[0] == "put":
+            k = (int(f[1]), ids.setdefault(f[2], len(ids)))
+            cmds.append(f"p {k[0]} {k[1]} {ipls.java_pair_hash(int(f[1]), f[2])}")
+        elif f[0] == "remove":
+            cmds.append(f"r {f[1]} {ids.setdefault(f[2], len(ids))}")
+        elif f[0] == "order":
+            cmds.append("o")
+        elif f[0] == "clear":
+            cmds.append("c")
+    out = subprocess.run([str(DRIVER)], input="\n".join(cmds) + "\n", capture_output=True, text=True,
+                         timeout=60, check=True).stdout.splitlines()
+    name = {v: k for k, v in ids.items()}
+    got = [" ".join(["order"] + [f"{p}:{name[int(a)]}" for p, a in (kv.split(":") for kv in ln.split()[2:])])
+           for ln in out]
+    assert got == [w for w in want if w.startswith("order")]
