@@ -1,0 +1,61 @@
+"""Dev probe: what a heap-array native costs against the direct-buffer one,
+through the JNI shim and the fake JVM (tests/jni/fake_jvm.c) on the GPU box.
+One partition of L doubles (one bucket per call, as the Updater folds):
+  accumulate(double[])         -- Get<T>ArrayRegion into the shim's per-thread
+                                  staging (pinned), then the library's fold
+  accumulateDirect(ByteBuffer) -- a hostAlloc direct buffer, zero copy
+  finalizePartition(byte[])    -- the BE sum into staging, Set<T>ArrayRegion
+  finalizePartitionDirect      -- the BE sum straight into a direct buffer
+GB/s = bytes of the Java-side array / wall time per call (median of reps).
+Usage: jni_heap_probe.py [L] [reps]"""
+import ctypes
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "ipls-java-api_amd"), str(ROOT / "tests")]
+import test_jni as TJ  # noqa: E402
+
+L = int(sys.argv[1]) if len(sys.argv) > 1 else 4194304
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+jvm = TJ.JVM()
+L64 = ctypes.c_int64
+h, exc = jvm.call("open", L64(0), 1, 3, 0, 0, 0, res=ctypes.c_int64)
+assert exc is None and h
+h = L64(h)
+# a synthetic-geometry handle is opened through the C-ABI cfg (bucket_len): use model_size = L - 1 instead
+jvm.call("close", h)
+h, exc = jvm.call("open", L64(L - 1), 1, 3, 0, 0, 0, res=ctypes.c_int64)
+assert exc is None and h
+h = L64(h)
+g = np.random.default_rng(1).standard_normal(L)
+arr = jvm.doubles(g)
+buf, mem = jvm.direct(8 * L)
+mem[:] = np.frombuffer(g.astype(">f8").tobytes(), dtype=np.uint8)
+out_heap = jvm.bytes_(b"\0" * (8 * L))
+pin_obj, _ = jvm.call("hostAllocDirect", 8 * L, res=ctypes.c_void_p)
+pin_obj = ctypes.c_void_p(pin_obj)
+
+
+def timed(fn):
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+res = {}
+res["accumulate_heap_double[]"] = timed(lambda: jvm.call("accumulate", h, 0, 0, arr))
+res["accumulateDirect_pinned_BE"] = timed(lambda: jvm.call("accumulateDirect", h, 0, 0, pin_obj, 0, L64(L), 1))
+res["finalize_heap_byte[]"] = timed(lambda: jvm.call("finalizePartition", h, 0, out_heap))
+res["finalizeDirect_pinned"] = timed(lambda: jvm.call("finalizePartitionDirect", h, 0, pin_obj, 0))
+jvm.call("close", h)
+print(json.dumps({"L": L, "bytes_per_call": 8 * L, "reps": reps,
+                  **{k: {"ms": round(v * 1e3, 3), "GBps": round(8 * L / v / 1e9, 2)} for k, v in res.items()}}))
