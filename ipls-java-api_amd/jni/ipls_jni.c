@@ -73,25 +73,18 @@ void IPLS_JNI_CALL_HOOK(const char *call);
 /* ---- per-thread staging for heap arrays ----
  * Two slots per thread, each grown to the largest array that thread has
  * passed so far and kept for reuse (no allocation and no page faults per
- * call); freed when the thread ends.  The slots are pinned host memory
- * (ipls_host_alloc): the library then DMAs from / to them directly, so a
- * heap array costs one host copy (Get/Set<T>ArrayRegion) and no staging
- * copy inside HIP.  Where pinning fails (no GPU, pinned memory exhausted)
- * a slot falls back to malloc'd memory, which the library also accepts. */
-struct stage { void *p[2]; size_t cap[2]; int pinned[2]; };
+ * call); freed when the thread ends.  Plain malloc'd memory: pinned slots
+ * (ipls_host_alloc) measured no faster -- the Get/Set<T>ArrayRegion copy
+ * bounds a heap-array call either way (tools/jni_heap_probe.py,
+ * profiles/r04/i/: accumulate(double[]) 21.8 GB/s pinned vs 21.4 pageable,
+ * finalize 15.0 vs 19.0; direct buffers 52-55 GB/s). */
+struct stage { void *p[2]; size_t cap[2]; };
 static pthread_key_t g_stage_key;
 static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
-static void stage_release(struct stage *st, int slot) {
-    if (!st->p[slot]) return;
-    if (st->pinned[slot]) (void)ipls_host_free(st->p[slot]);
-    else free(st->p[slot]);
-    st->p[slot] = NULL;
-    st->cap[slot] = 0;
-}
 static void stage_free(void *v) {
     struct stage *st = (struct stage *)v;
-    stage_release(st, 0);
-    stage_release(st, 1);
+    free(st->p[0]);
+    free(st->p[1]);
     free(st);
 }
 static void stage_init(void) { (void)pthread_key_create(&g_stage_key, stage_free); }
@@ -111,19 +104,10 @@ static void *stage(JNIEnv *env, int slot, size_t bytes) {
     }
     if (bytes == 0) bytes = 1;
     if (st->cap[slot] < bytes) {
-        const size_t cap = (bytes + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);   /* 2 MiB steps */
-        stage_release(st, slot);
-        void *q = NULL;
-        const char *mode = getenv("IPLS_JNI_STAGING");   /* "pageable": malloc'd slots (an A/B switch) */
-        if (!(mode && !strcmp(mode, "pageable")) && LIB(ipls_host_alloc(cap, &q)) == IPLS_OK && q) {
-            st->pinned[slot] = 1;
-        } else {
-            q = malloc(cap);
-            st->pinned[slot] = 0;
-        }
+        void *q = realloc(st->p[slot], bytes);
         if (!q) { throw_msg(env, "java/lang/OutOfMemoryError", "JNI staging buffer"); return NULL; }
         st->p[slot] = q;
-        st->cap[slot] = cap;
+        st->cap[slot] = bytes;
     }
     return st->p[slot];
 }

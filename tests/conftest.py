@@ -12,6 +12,15 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+# torch first: its bundled HIP runtime must be the one in the process before
+# anything loads libipls_agg.so (which links /opt/rocm's).  The other order --
+# the library loaded, then torch imported and initialised -- leaves the
+# library with "no HIP device available" (tools/jni_open_probe.py late_torch,
+# profiles/r04/i/); a test module that loads the library without importing
+# torch itself (test_jni.py) must not depend on an earlier module having
+# imported it.
+import torch  # noqa: F401,E402
+
 ROOT = Path(__file__).resolve().parent.parent
 PKG = ROOT / "ipls-java-api_amd"
 GOLDEN = ROOT / "tests" / "golden"

@@ -24,11 +24,7 @@ L = int(sys.argv[1]) if len(sys.argv) > 1 else 4194304
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 jvm = TJ.JVM()
 L64 = ctypes.c_int64
-h, exc = jvm.call("open", L64(0), 1, 3, 0, 0, 0, res=ctypes.c_int64)
-assert exc is None and h
-h = L64(h)
-# a synthetic-geometry handle is opened through the C-ABI cfg (bucket_len): use model_size = L - 1 instead
-jvm.call("close", h)
+# one partition of L doubles: model_size = L - 1 (the chunk rule gives L_0 = M + 1)
 h, exc = jvm.call("open", L64(L - 1), 1, 3, 0, 0, 0, res=ctypes.c_int64)
 assert exc is None and h
 h = L64(h)
