@@ -159,6 +159,15 @@ def lib() -> ctypes.CDLL:
     there is deliberately no CPU path behind this package."""
     global _lib
     if _lib is None:
+        # torch (when installed) first: its bundled HIP runtime must be the
+        # process's runtime before the library's own link to /opt/rocm's is
+        # resolved.  In the other order -- this library loaded, then torch
+        # initialised -- the library finds "no HIP device available"
+        # (tools/jni_open_probe.py, profiles/r04/i/).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = load(LIB_PATH)
     return _lib
 
