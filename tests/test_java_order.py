@@ -173,3 +173,45 @@ def test_golden_java_order_cases(O):
     got = [" ".join(["order"] + [f"{p}:{name[int(a)]}" for p, a in (kv.split(":") for kv in ln.split()[2:])])
            for ln in out]
     assert got == [w for w in want if w.startswith("order")]
+
+
+def test_golden_java_pin_cases():
+    """tests/golden/java_pin_expected.txt is this repository's restatement's
+    answer (tests/golden/make_java_pins.py) to java_pin_cases.txt: folds,
+    divides, putDouble / writeDouble, Base64 URL encode / decode (with the
+    decoder's exceptions), Marshall_Packet frames and the ObjectOutputStream
+    bytes of a Pair<Integer,double[]>.  tests/java/PinJavaCodecs.java prints
+    the same text from a real JVM, so on a host with a JDK a diff pins them."""
+    import sys
+    import warnings
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_java_pins as G
+    cases = (ROOT / "tests" / "golden" / "java_pin_cases.txt").read_text().splitlines()
+    want = (ROOT / "tests" / "golden" / "java_pin_expected.txt").read_text().splitlines()
+    assert G.cases() == cases
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)   # inf - inf in the fold cases
+        assert [G.answer(c) for c in cases] == want
+
+
+def test_library_codecs_match_java_pins():
+    """The library's own host codecs (ipls_frame_encode, ipls_pair_encode;
+    no GPU involved) give the pinned bytes of java_pin_expected.txt."""
+    import sys
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_java_pins as G
+    import ipls
+    cases = (ROOT / "tests" / "golden" / "java_pin_cases.txt").read_text().splitlines()
+    want = dict(zip(cases, (ROOT / "tests" / "golden" / "java_pin_expected.txt").read_text().splitlines()))
+    n = 0
+    for c in cases:
+        f = c.split(" ")
+        if f[0] == "frame":
+            got = ipls.frame_encode(G.parse_dl(f[5]), int(f[2]), int(f[3]), int(f[1]), f[4].encode())
+        elif f[0] == "pair":
+            got = ipls.pair_encode(int(f[1]), G.parse_dl(f[2]))
+        else:
+            continue
+        assert f"{f[0]} {bytes(got).hex()}" == want[c], c
+        n += 1
+    assert n == 6
