@@ -1153,6 +1153,34 @@ def test_replica_drop_when_its_partial_arrives(ipls, O):
     agg.close()
 
 
+def test_replica_store_argument_errors(ipls, O):
+    """The keyed store refuses what would desynchronise it from Java's map:
+    a second key hash for a stored key (IPLS_E_INVAL, nothing folded), an
+    out-of-range partition (ArrayIndexOutOfBounds); a failed call leaves the
+    store and its order as they were."""
+    from ipls import _native as N
+    L, P = 1001, 2
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    g = O.synth_bucket(L, 0, 1)
+    kh = O.java_pair_hash(0, "12D3KooWA")
+    agg.OtherReplicaGradients(0, 4, g, key_hash=kh)
+    before = agg.replica_order()
+    with pytest.raises(ipls.IplsError) as e:
+        agg.OtherReplicaGradients(0, 4, g, key_hash=kh + 1)
+    assert e.value.code == N.IPLS_E_INVAL
+    with pytest.raises(ipls.IplsError) as e:
+        agg.OtherReplicaGradients(P, 4, g, key_hash=kh)
+    assert e.value.code == N.IPLS_E_RANGE
+    with pytest.raises(ipls.IplsError):
+        agg.OtherReplicaDrop(-1, 4)
+    assert agg.replica_order() == before
+    n, parts = agg.Collect_Replicas()
+    assert (n, parts) == (1, [L, 0])
+    assert_bits_equal(agg.read(0, ipls.TGT_REP), 0.0 + g, "REP[0]")    # folded once, not twice
+    assert agg.replica_order() == ([], 0)                             # new HashMap<>()
+    agg.close()
+
+
 def _ids_with_non_ascending_order(O, p, n):
     """n peer IDs whose Pair(p, id) hashes fall in bins 13, 7, 2 of a 16-bin
     HashMap: stored in that order, they iterate in reverse -- neither
