@@ -152,95 +152,565 @@ def java_pair_hash(p: int, peer_id: str) -> int:
     return _i32(31 * 1 + lst)
 
 
-class JavaHashMap:
-    """java.util.HashMap's table as JDK 8 keeps it (the pom compiles for 1.8,
-    pom.xml:118-122), restated from the published source: an array of bins,
-    each a chain in link order; hash = h ^ (h >>> 16), bin = hash & (n - 1);
-    the table is made with 16 bins at the first put after construction and
-    doubled (resize) when ++size > 0.75 n, or when a put makes a chain 9 long
-    while n < 64 (treeifyBin); a resize splits every chain into its lo
-    (hash & oldCap == 0) and hi halves, each in chain order, at j and
-    j + oldCap; a new key is appended at its chain's tail; remove unlinks;
-    iteration walks the bins in index order and each chain in link order.
-    A chain that reaches 9 at n >= 64 becomes a red-black tree (TreeNode
-    order); that case is flagged (``tree_bin``), not restated.
+class _Node:
+    """HashMap.Node: hash (the spread hash, a Java int), key, value, next."""
+    __slots__ = ("hash", "key", "value", "next", "parent", "left", "right", "prev", "red", "tree")
 
-    This simulates the table itself, independently of the library's model
-    (java_hashmap.hpp orders keys by (bin, insertion)), so the two check each
-    other."""
+    def __init__(self, h, key, value, nxt, tree=False):
+        self.hash, self.key, self.value, self.next = h, key, value, nxt
+        self.parent = self.left = self.right = self.prev = None
+        self.red = False
+        self.tree = tree                 # a HashMap.TreeNode
+
+
+class JavaHashMap:
+    """java.util.HashMap as JDK 8 keeps it (the pom compiles for 1.8,
+    pom.xml:118-122), restated from the published source, node for node:
+    the table of bins (each a chain linked by `next`), hash = h ^ (h >>> 16)
+    (a Java int), bin = hash & (n - 1); the table is made with 16 bins at the
+    first put after construction and doubled (resize) when ++size > 0.75 n,
+    or when a put makes a chain 9 long while n < 64 (treeifyBin); a resize
+    splits every chain into its lo (hash & oldCap == 0) and hi halves, each
+    in chain order, at j and j + oldCap; a new key is appended at its chain's
+    tail; remove unlinks.  A chain that reaches 9 at n >= 64 becomes a
+    red-black tree of TreeNodes (treeify, putTreeVal, removeTreeNode,
+    balanceInsertion / balanceDeletion, rotations, moveRootToFront, split
+    and untreeify below): its iteration order is still the `next` chain,
+    which those methods rearrange.  Keys whose spread hashes are equal are
+    ordered in a tree by System.identityHashCode (javatuples' Pair is not
+    Comparable<Pair>, so HashMap.comparableClassFor is null and tieBreakOrder
+    decides) -- not reproducible even by Java; ``nondeterministic`` flags it.
+    Iteration walks the bins in index order and each chain in link order.
+
+    This simulates the table itself; the library's model (java_hashmap.hpp)
+    is a second transliteration of the same JDK source, and the two are
+    checked against each other (tests/test_java_order.py)."""
+    TREEIFY, UNTREEIFY, MIN_TREEIFY = 8, 6, 64
 
     def __init__(self):
-        self.table = None          # list of chains: [[key, hash, value], ...]
+        self.table = None            # list of bin heads (_Node or None)
         self.size = 0
         self.threshold = 0
-        self.tree_bin = False
+        self.nondeterministic = False
+        self._nodes = {}             # key -> node (lookup only; never decides an order)
 
     @staticmethod
     def spread(h: int) -> int:
         h &= 0xFFFFFFFF
         return h ^ (h >> 16)
 
+    @staticmethod
+    def _jint(h: int) -> int:
+        h = JavaHashMap.spread(h)
+        return h - (1 << 32) if h & 0x80000000 else h
+
+    @property
+    def tree_bin(self) -> bool:
+        return self.table is not None and any(e is not None and e.tree for e in self.table)
+
+    # ---- HashMap ----
     def _resize(self):
         old = self.table
-        if old is None:
-            self.table = [[] for _ in range(16)]
-            self.threshold = 12
-            return
-        n = len(old)
-        new = [[] for _ in range(2 * n)]
-        for j, chain in enumerate(old):
-            new[j] = [e for e in chain if self.spread(e[1]) & n == 0]
-            new[j + n] = [e for e in chain if self.spread(e[1]) & n != 0]
-        self.table = new
-        self.threshold *= 2
-
-    def _find(self, key, h):
-        if self.table is None:
-            return None
-        for e in self.table[self.spread(h) & (len(self.table) - 1)]:
-            if e[1] == h and e[0] == key:
-                return e
-        return None
+        old_cap = len(old) if old else 0
+        if old_cap > 0:
+            new_cap, self.threshold = old_cap << 1, self.threshold << 1
+        else:
+            new_cap, self.threshold = 16, 12
+        tab = [None] * new_cap
+        self.table = tab
+        for j in range(old_cap):
+            e = old[j]
+            if e is None:
+                continue
+            old[j] = None
+            if e.next is None:
+                tab[e.hash & (new_cap - 1)] = e
+            elif e.tree:
+                self._split(e, tab, j, old_cap)
+            else:
+                lo_h = lo_t = hi_h = hi_t = None
+                while e is not None:
+                    nxt = e.next
+                    if e.hash & old_cap == 0:
+                        if lo_t is None:
+                            lo_h = e
+                        else:
+                            lo_t.next = e
+                        lo_t = e
+                    else:
+                        if hi_t is None:
+                            hi_h = e
+                        else:
+                            hi_t.next = e
+                        hi_t = e
+                    e = nxt
+                if lo_t is not None:
+                    lo_t.next = None
+                    tab[j] = lo_h
+                if hi_t is not None:
+                    hi_t.next = None
+                    tab[j + old_cap] = hi_h
+        return tab
 
     def put(self, key, h: int, value) -> None:
-        if self.table is None:
-            self._resize()
-        e = self._find(key, h)
-        if e is not None:
-            e[2] = value
+        if key in self._nodes:                       # an existing mapping: value replaced, nothing moves
+            self._nodes[key].value = value
             return
-        chain = self.table[self.spread(h) & (len(self.table) - 1)]
-        before = len(chain)
-        chain.append([key, h, value])
-        if before >= 8:                                   # binCount >= TREEIFY_THRESHOLD - 1
-            if len(self.table) < 64:
-                self._resize()
-            else:
-                self.tree_bin = True
+        hh = self._jint(h)
+        tab = self.table
+        if tab is None:
+            tab = self._resize()
+        n = len(tab)
+        i = hh & (n - 1)
+        p = tab[i]
+        if p is None:
+            tab[i] = self._nodes[key] = _Node(hh, key, value, None)
+        elif p.tree:
+            self._nodes[key] = self._put_tree_val(p, tab, hh, key, value)
+        else:
+            bin_count = 0
+            while True:
+                if p.next is None:
+                    p.next = self._nodes[key] = _Node(hh, key, value, None)
+                    if bin_count >= self.TREEIFY - 1:
+                        self._treeify_bin(tab, hh)       # replaces the chain's nodes (and their index)
+                    break
+                p = p.next
+                bin_count += 1
         self.size += 1
         if self.size > self.threshold:
             self._resize()
 
     def get(self, key, h: int):
-        e = self._find(key, h)
-        return None if e is None else e[2]
+        e = self._nodes.get(key)
+        return None if e is None else e.value
 
     def remove(self, key, h: int) -> bool:
-        if self.table is None:
+        node = self._nodes.pop(key, None)
+        if node is None:
             return False
-        chain = self.table[self.spread(h) & (len(self.table) - 1)]
-        for i, e in enumerate(chain):
-            if e[1] == h and e[0] == key:
-                del chain[i]
-                self.size -= 1
-                return True
-        return False
+        tab = self.table
+        i = node.hash & (len(tab) - 1)
+        if node.tree:
+            self._remove_tree_node(node, tab, True)
+        elif tab[i] is node:
+            tab[i] = node.next
+        else:
+            p = tab[i]
+            while p.next is not node:
+                p = p.next
+            p.next = node.next
+        self.size -= 1
+        return True
 
     def keys(self) -> list:
-        return [] if self.table is None else [e[0] for chain in self.table for e in chain]
+        out = []
+        for e in (self.table or []):
+            while e is not None:
+                out.append(e.key)
+                e = e.next
+        return out
 
     def __len__(self):
         return self.size
+
+    def _treeify_bin(self, tab, hh):
+        n = len(tab)
+        if n < self.MIN_TREEIFY:
+            self._resize()
+            return
+        index = (n - 1) & hh
+        e = tab[index]
+        hd = tl = None
+        while e is not None:                         # replacementTreeNode, in chain order
+            p = _Node(e.hash, e.key, e.value, None, tree=True)
+            self._nodes[p.key] = p
+            if tl is None:
+                hd = p
+            else:
+                p.prev = tl
+                tl.next = p
+            tl = p
+            e = e.next
+        tab[index] = hd
+        if hd is not None:
+            self._treeify(hd, tab)
+
+    # ---- TreeNode ----
+    @staticmethod
+    def _root(x):
+        while x.parent is not None:
+            x = x.parent
+        return x
+
+    @staticmethod
+    def _move_root_to_front(tab, root):
+        if root is None or not tab:
+            return
+        index = (len(tab) - 1) & root.hash
+        first = tab[index]
+        if root is not first:
+            tab[index] = root
+            rp, rn = root.prev, root.next
+            if rn is not None:
+                rn.prev = rp
+            if rp is not None:
+                rp.next = rn
+            if first is not None:
+                first.prev = root
+            root.next = first
+            root.prev = None
+
+    def _dir(self, h, ph):
+        if ph > h:
+            return -1
+        if ph < h:
+            return 1
+        self.nondeterministic = True                 # tieBreakOrder: System.identityHashCode
+        return -1
+
+    def _treeify(self, head, tab):
+        root = None
+        x = head
+        while x is not None:
+            nxt = x.next
+            x.left = x.right = None
+            if root is None:
+                x.parent = None
+                x.red = False
+                root = x
+            else:
+                p = root
+                while True:
+                    d = self._dir(x.hash, p.hash)
+                    xp = p
+                    p = p.left if d <= 0 else p.right
+                    if p is None:
+                        x.parent = xp
+                        if d <= 0:
+                            xp.left = x
+                        else:
+                            xp.right = x
+                        root = self._balance_insertion(root, x)
+                        break
+            x = nxt
+        self._move_root_to_front(tab, root)
+
+    def _untreeify(self, first):
+        hd = tl = None
+        q = first
+        while q is not None:                         # replacementNode, in chain order
+            p = _Node(q.hash, q.key, q.value, None)
+            self._nodes[p.key] = p
+            if tl is None:
+                hd = p
+            else:
+                tl.next = p
+            tl = p
+            q = q.next
+        return hd
+
+    def _put_tree_val(self, first, tab, hh, key, value):
+        root = self._root(first) if first.parent is not None else first
+        p = root
+        while True:
+            d = self._dir(hh, p.hash)
+            xp = p
+            p = p.left if d <= 0 else p.right
+            if p is None:
+                xpn = xp.next
+                x = _Node(hh, key, value, xpn, tree=True)
+                if d <= 0:
+                    xp.left = x
+                else:
+                    xp.right = x
+                xp.next = x
+                x.parent = x.prev = xp
+                if xpn is not None:
+                    xpn.prev = x
+                self._move_root_to_front(tab, self._balance_insertion(root, x))
+                return x
+
+    def _remove_tree_node(self, node, tab, movable):
+        n = len(tab)
+        index = (n - 1) & node.hash
+        first = root = tab[index]
+        succ, pred = node.next, node.prev
+        if pred is None:
+            tab[index] = first = succ
+        else:
+            pred.next = succ
+        if succ is not None:
+            succ.prev = pred
+        if first is None:
+            return
+        if root.parent is not None:
+            root = self._root(root)
+        if root is None or (movable and (root.right is None or root.left is None or root.left.left is None)):
+            tab[index] = self._untreeify(first)      # too small
+            return
+        p, pl, pr = node, node.left, node.right
+        if pl is not None and pr is not None:
+            s = pr
+            while s.left is not None:                # successor
+                s = s.left
+            s.red, p.red = p.red, s.red              # swap colours
+            sr, pp = s.right, p.parent
+            if s is pr:
+                p.parent = s
+                s.right = p
+            else:
+                sp = s.parent
+                p.parent = sp
+                if sp is not None:
+                    if s is sp.left:
+                        sp.left = p
+                    else:
+                        sp.right = p
+                s.right = pr
+                if pr is not None:
+                    pr.parent = s
+            p.left = None
+            p.right = sr
+            if sr is not None:
+                sr.parent = p
+            s.left = pl
+            if pl is not None:
+                pl.parent = s
+            s.parent = pp
+            if pp is None:
+                root = s
+            elif p is pp.left:
+                pp.left = s
+            else:
+                pp.right = s
+            replacement = sr if sr is not None else p
+        elif pl is not None:
+            replacement = pl
+        elif pr is not None:
+            replacement = pr
+        else:
+            replacement = p
+        if replacement is not p:
+            pp = replacement.parent = p.parent
+            if pp is None:
+                root = replacement
+            elif p is pp.left:
+                pp.left = replacement
+            else:
+                pp.right = replacement
+            p.left = p.right = p.parent = None
+        r = root if p.red else self._balance_deletion(root, replacement)
+        if replacement is p:                         # detach
+            pp = p.parent
+            p.parent = None
+            if pp is not None:
+                if p is pp.left:
+                    pp.left = None
+                elif p is pp.right:
+                    pp.right = None
+        if movable:
+            self._move_root_to_front(tab, r)
+
+    def _split(self, b, tab, index, bit):
+        lo_h = lo_t = hi_h = hi_t = None
+        lc = hc = 0
+        e = b
+        while e is not None:
+            nxt = e.next
+            e.next = None
+            if e.hash & bit == 0:
+                e.prev = lo_t
+                if lo_t is None:
+                    lo_h = e
+                else:
+                    lo_t.next = e
+                lo_t = e
+                lc += 1
+            else:
+                e.prev = hi_t
+                if hi_t is None:
+                    hi_h = e
+                else:
+                    hi_t.next = e
+                hi_t = e
+                hc += 1
+            e = nxt
+        if lo_h is not None:
+            if lc <= self.UNTREEIFY:
+                tab[index] = self._untreeify(lo_h)
+            else:
+                tab[index] = lo_h
+                if hi_h is not None:
+                    self._treeify(lo_h, tab)
+        if hi_h is not None:
+            if hc <= self.UNTREEIFY:
+                tab[index + bit] = self._untreeify(hi_h)
+            else:
+                tab[index + bit] = hi_h
+                if lo_h is not None:
+                    self._treeify(hi_h, tab)
+
+    @staticmethod
+    def _rotate_left(root, p):
+        if p is not None and p.right is not None:
+            r = p.right
+            rl = p.right = r.left
+            if rl is not None:
+                rl.parent = p
+            pp = r.parent = p.parent
+            if pp is None:
+                root = r
+                r.red = False
+            elif pp.left is p:
+                pp.left = r
+            else:
+                pp.right = r
+            r.left = p
+            p.parent = r
+        return root
+
+    @staticmethod
+    def _rotate_right(root, p):
+        if p is not None and p.left is not None:
+            l = p.left
+            lr = p.left = l.right
+            if lr is not None:
+                lr.parent = p
+            pp = l.parent = p.parent
+            if pp is None:
+                root = l
+                l.red = False
+            elif pp.right is p:
+                pp.right = l
+            else:
+                pp.left = l
+            l.right = p
+            p.parent = l
+        return root
+
+    def _balance_insertion(self, root, x):
+        x.red = True
+        while True:
+            xp = x.parent
+            if xp is None:
+                x.red = False
+                return x
+            xpp = xp.parent
+            if not xp.red or xpp is None:
+                return root
+            xppl = xpp.left
+            if xp is xppl:
+                xppr = xpp.right
+                if xppr is not None and xppr.red:
+                    xppr.red = False
+                    xp.red = False
+                    xpp.red = True
+                    x = xpp
+                else:
+                    if x is xp.right:
+                        x = xp
+                        root = self._rotate_left(root, x)
+                        xp = x.parent
+                        xpp = None if xp is None else xp.parent
+                    if xp is not None:
+                        xp.red = False
+                        if xpp is not None:
+                            xpp.red = True
+                            root = self._rotate_right(root, xpp)
+            else:
+                if xppl is not None and xppl.red:
+                    xppl.red = False
+                    xp.red = False
+                    xpp.red = True
+                    x = xpp
+                else:
+                    if x is xp.left:
+                        x = xp
+                        root = self._rotate_right(root, x)
+                        xp = x.parent
+                        xpp = None if xp is None else xp.parent
+                    if xp is not None:
+                        xp.red = False
+                        if xpp is not None:
+                            xpp.red = True
+                            root = self._rotate_left(root, xpp)
+
+    def _balance_deletion(self, root, x):
+        while True:
+            if x is None or x is root:
+                return root
+            xp = x.parent
+            if xp is None:
+                x.red = False
+                return x
+            if x.red:
+                x.red = False
+                return root
+            xpl = xp.left
+            if xpl is x:
+                xpr = xp.right
+                if xpr is not None and xpr.red:
+                    xpr.red = False
+                    xp.red = True
+                    root = self._rotate_left(root, xp)
+                    xp = x.parent
+                    xpr = None if xp is None else xp.right
+                if xpr is None:
+                    x = xp
+                else:
+                    sl, sr = xpr.left, xpr.right
+                    if (sr is None or not sr.red) and (sl is None or not sl.red):
+                        xpr.red = True
+                        x = xp
+                    else:
+                        if sr is None or not sr.red:
+                            if sl is not None:
+                                sl.red = False
+                            xpr.red = True
+                            root = self._rotate_right(root, xpr)
+                            xp = x.parent
+                            xpr = None if xp is None else xp.right
+                        if xpr is not None:
+                            xpr.red = False if xp is None else xp.red
+                            sr = xpr.right
+                            if sr is not None:
+                                sr.red = False
+                        if xp is not None:
+                            xp.red = False
+                            root = self._rotate_left(root, xp)
+                        x = root
+            else:
+                if xpl is not None and xpl.red:
+                    xpl.red = False
+                    xp.red = True
+                    root = self._rotate_right(root, xp)
+                    xp = x.parent
+                    xpl = None if xp is None else xp.left
+                if xpl is None:
+                    x = xp
+                else:
+                    sl, sr = xpl.left, xpl.right
+                    if (sl is None or not sl.red) and (sr is None or not sr.red):
+                        xpl.red = True
+                        x = xp
+                    else:
+                        if sl is None or not sl.red:
+                            if sr is not None:
+                                sr.red = False
+                            xpl.red = True
+                            root = self._rotate_left(root, xpl)
+                            xp = x.parent
+                            xpl = None if xp is None else xp.left
+                        if xpl is not None:
+                            xpl.red = False if xp is None else xp.red
+                            sl = xpl.left
+                            if sl is not None:
+                                sl.red = False
+                        if xp is not None:
+                            xp.red = False
+                            root = self._rotate_right(root, xp)
+                        x = root
 
 
 class ReplicaStore:

@@ -4,7 +4,7 @@
 // the JDK table.  Commands, one per line:
 //   p <partition> <aggregator> <hash>   put (if absent)
 //   r <partition> <aggregator>          remove
-//   o                                   print "<capacity> <tree_bin> p:a p:a ..."
+//   o                                   print "<capacity> <tree_bin> <nondeterministic> p:a p:a ..."
 //   c                                   clear (new HashMap<>())
 #include <cstdio>
 #include <cstring>
@@ -24,7 +24,7 @@ int main() {
       if (std::scanf("%d %d", &p, &a) != 2) return 2;
       m.remove({p, a});
     } else if (!std::strcmp(cmd, "o")) {
-      std::printf("%lld %d", (long long)m.capacity(), (int)m.tree_bin());
+      std::printf("%lld %d %d", (long long)m.capacity(), (int)m.tree_bin(), (int)m.nondeterministic());
       for (const auto& k : m.order()) std::printf(" %d:%d", k.first, k.second);
       std::printf("\n");
     } else if (!std::strcmp(cmd, "c")) {

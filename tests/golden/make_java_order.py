@@ -66,7 +66,35 @@ def cases() -> list[str]:
         out.append(f"put 5 {pid}")
     out.append("order")
     out.append("clear")
-    # 5: many keys of one aggregator over many partitions (the hashes 992 + 31p + h)
+    # 5: a red-black tree bin: 14 IDs whose Pair(0, id) hashes agree in the low 8
+    # bits after h ^ (h >>> 16) (found by search) share one bin up to 256 bins,
+    # so the 9th of them turns the bin into a TreeNode tree at 64 bins; then
+    # removals (removeTreeNode), more keys (resizes: split / untreeify)
+    out.append("case tree_bin")
+    coll, i, want = [], 0, None
+    while len(coll) < 14:
+        pid = f"QmTree{i}"
+        i += 1
+        b = O.JavaHashMap.spread(O.java_pair_hash(0, pid)) & 255
+        if want is None:
+            want = b
+        if b == want and O.java_pair_hash(0, pid) not in {O.java_pair_hash(0, c) for c in coll}:
+            coll.append(pid)
+    for pid in coll:
+        out.append(f"put 0 {pid}")
+    out.append("order")
+    for pid in (coll[3], coll[0], coll[9]):
+        out.append(f"remove 0 {pid}")
+    out.append("order")
+    for j in range(60):
+        out.append(f"put {1 + j % 7} 12D3KooWFill{j}")
+        if j % 20 == 19:
+            out.append("order")
+    for pid in coll[4:9]:
+        out.append(f"remove 0 {pid}")
+    out.append("order")
+    out.append("clear")
+    # 6: many keys of one aggregator over many partitions (the hashes 992 + 31p + h)
     out.append("case one_aggregator_many_partitions")
     for p in range(0, 200, 3):
         out.append(f"put {p} 12D3KooWSame")
@@ -94,7 +122,7 @@ def expected(lines: list[str]) -> list[str]:
             if (p, pid) in hashes:
                 m.remove((p, pid), hashes.pop((p, pid)))
         elif f[0] == "order":
-            assert not m.tree_bin
+            assert not m.nondeterministic
             out.append("order " + " ".join(f"{p}:{pid}" for p, pid in m.keys()))
         elif f[0] == "clear":
             m, hashes = O.JavaHashMap(), {}

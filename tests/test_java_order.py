@@ -91,23 +91,44 @@ def _build_driver():
                    check=True)
 
 
-@pytest.mark.parametrize("seed,nbits", [(1, 32), (2, 6), (3, 5), (4, 9), (5, 32)])
-def test_front_model_matches_jdk_table_simulation(O, seed, nbits):
-    """Random streams of put / remove / collect over (p, aggregator) keys; with
-    few hash bits (nbits) many keys collide, chains reach 9 below 64 bins
-    (treeifyBin resizes) and removes leave holes.  After every 'o' the model's
-    order must equal the simulated table's iteration order (skipped only once
-    a tree bin appears, which neither side restates)."""
+@pytest.mark.parametrize("seed,mode", [(1, "java"), (2, "bits6"), (3, "bits5"), (4, "bits9"), (5, "java"),
+                                       (6, "collide"), (7, "collide"), (8, "collide"), (9, "collide_big"),
+                                       (10, "collide_big")])
+def test_front_model_matches_jdk_table_simulation(O, seed, mode):
+    """Random streams of put / remove / collect over (p, aggregator) keys,
+    replayed on the library's model (csrc/java_hashmap.hpp, through
+    tests/cpp/java_order_driver.cpp) and on the oracle's JavaHashMap -- two
+    independent transliterations of JDK 8's HashMap / TreeNode.  After every
+    'o' the capacities, tree flags and key orders must agree.  "java": real
+    Pair hashCodes; "bitsN": N-bit hashes (many equal full hashes: chains,
+    treeifyBin resizes below 64 bins, and trees whose equal-hash ties Java
+    breaks by identity -- compared until that flag is raised); "collide":
+    distinct full hashes with equal low 10 bits, so bins of >= 64-bin tables
+    turn into red-black trees (treeify, putTreeVal, removeTreeNode with its
+    rebalancing, split and untreeify on resize) whose chain order is exact."""
     _build_driver()
     rng = np.random.default_rng(seed)
     cmds, expect = [], []
-    m, hashes = O.JavaHashMap(), {}
+    m, hashes, used = O.JavaHashMap(), {}, set()
+
+    def draw_hash(p, a):
+        if mode == "java":
+            return O.java_pair_hash(p, f"12D3KooW{a}")
+        if mode.startswith("bits"):
+            return int(rng.integers(0, 1 << int(mode[4:])))
+        base = int(rng.choice([7, 300, 1000]))
+        while True:   # distinct full hashes whose spread h ^ (h >>> 16) keeps the low 10 bits = base
+            h = base + (1 << 10) * int(rng.integers(0, 64)) + (1 << 26) * int(rng.integers(0, 32))
+            if h not in used:
+                used.add(h)
+                return h
+
+    n_keys = 25 if mode != "collide_big" else 60
     for step in range(3000):
         r = rng.integers(0, 20)
-        p, a = int(rng.integers(0, 40)), int(rng.integers(0, 25))
+        p, a = int(rng.integers(0, 40)), int(rng.integers(0, n_keys))
         if r < 12:
-            h = int(rng.integers(0, 1 << nbits)) if nbits < 32 else O.java_pair_hash(p, f"12D3KooW{a}")
-            h = hashes.get((p, a), h)
+            h = hashes[(p, a)] if (p, a) in hashes else draw_hash(p, a)
             cmds.append(f"p {p} {a} {h}")
             if (p, a) not in hashes:
                 hashes[(p, a)] = h
@@ -116,27 +137,29 @@ def test_front_model_matches_jdk_table_simulation(O, seed, nbits):
             cmds.append(f"r {p} {a}")
             if (p, a) in hashes:
                 m.remove((p, a), hashes.pop((p, a)))
-        elif r < 19:
-            cmds.append("o")
-            expect.append((len(m.table) if m.table else 0, int(m.tree_bin), m.keys()))
         else:
             cmds.append("o")
-            expect.append((len(m.table) if m.table else 0, int(m.tree_bin), m.keys()))
-            cmds.append("c")
-            m, hashes = O.JavaHashMap(), {}
+            expect.append((len(m.table) if m.table else 0, int(m.tree_bin), int(m.nondeterministic), m.keys()))
+            if r == 19 and rng.random() < 0.15:
+                cmds.append("c")
+                m, hashes = O.JavaHashMap(), {}
     out = subprocess.run([str(DRIVER)], input="\n".join(cmds) + "\n", capture_output=True, text=True, timeout=120,
                          check=True).stdout.splitlines()
     assert len(out) == len(expect)
-    compared = 0
-    for line, (cap, tree, keys) in zip(out, expect):
+    compared = trees = 0
+    for line, (cap, tree, nondet, keys) in zip(out, expect):
         f = line.split()
-        assert int(f[0]) == cap and int(f[1]) == tree, (line[:80], cap, tree)
-        if tree:
+        assert int(f[2]) == nondet, (line[:80], nondet)
+        if nondet:                                   # Java's own order is not reproducible from here on
             continue
-        got = [tuple(int(x) for x in kv.split(":")) for kv in f[2:]]
+        assert (int(f[0]), int(f[1])) == (cap, tree), (line[:80], cap, tree)
+        got = [tuple(int(x) for x in kv.split(":")) for kv in f[3:]]
         assert got == keys
         compared += 1
-    assert compared > 50
+        trees += tree
+    assert compared > 30
+    if mode.startswith("collide"):
+        assert trees > 5, trees                      # the tree code really ran
 
 
 def test_golden_java_order_cases(O):
@@ -170,7 +193,7 @@ def test_golden_java_order_cases(O):
     out = subprocess.run([str(DRIVER)], input="\n".join(cmds) + "\n", capture_output=True, text=True,
                          timeout=60, check=True).stdout.splitlines()
     name = {v: k for k, v in ids.items()}
-    got = [" ".join(["order"] + [f"{p}:{name[int(a)]}" for p, a in (kv.split(":") for kv in ln.split()[2:])])
+    got = [" ".join(["order"] + [f"{p}:{name[int(a)]}" for p, a in (kv.split(":") for kv in ln.split()[3:])])
            for ln in out]
     assert got == [w for w in want if w.startswith("order")]
 
