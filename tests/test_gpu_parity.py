@@ -1265,6 +1265,50 @@ def test_collect_replicas_order_after_resize_and_drops(ipls, O):
     agg.close()
 
 
+def test_collect_replicas_order_through_a_tree_bin(ipls, O):
+    """A HashMap bin that becomes a red-black tree (HashMap.treeifyBin at 9
+    keys and >= 64 bins): 14 keys whose hashes share the low 8 bits go to one
+    bin, drops unlink tree nodes (removeTreeNode), and more keys resize the
+    table so TreeNode.split cuts the tree into a half that stays a tree and
+    a half of at most 6 keys that becomes a chain again (untreeify).  The library's order model and the oracle's
+    JDK simulation agree on the key order at every step, and the collect
+    folds in that order bit for bit, with cancelling magnitudes so a
+    different order changes the bits."""
+    L, P = 2053, 3
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    store = O.ReplicaStore()
+    rep = [np.zeros(L) for _ in range(P)]
+    scale = [1e16, 1.0, -1e16, 3.0, -1.0, 1e-3]
+    coll = [(j % P, j) for j in range(14)]              # hashes 0x1A + 64 j: spread(h) = h
+    for i, (p, a) in enumerate(coll):
+        g = O.synth_bucket(L, p, 300 + i) * scale[i % len(scale)]
+        kh = 0x1A + 64 * i
+        agg.OtherReplicaGradients(p, a, g, key_hash=kh)
+        O.other_replica_add(store, p, a, g, key_hash=kh)
+    assert store.map.tree_bin and len(store.map.table) == 64
+    assert agg.replica_order() == (store.map.keys(), 64)
+    for p, a in (coll[1], coll[7], coll[11]):
+        assert agg.OtherReplicaDrop(p, a) == O.other_replica_drop(store, p, a) == 1
+    assert agg.replica_order() == (store.map.keys(), 64)
+    for j in range(60):                                  # 71 keys > 0.75 x 64: 128 bins
+        p, a = j % P, 100 + j
+        g = O.synth_bucket(L, p, 400 + j) * scale[j % len(scale)]
+        kh = O.java_pair_hash(p, f"12D3KooWFill{j}")
+        agg.OtherReplicaGradients(p, a, g, key_hash=kh)
+        O.other_replica_add(store, p, a, g, key_hash=kh)
+    tab = store.map.table
+    assert len(tab) == 128 and not store.map.nondeterministic
+    assert tab[0x1A] is not None and tab[0x1A].tree                # even j (and fill keys): still a tree
+    assert tab[0x1A + 64] is not None and not tab[0x1A + 64].tree  # odd j: a chain again
+    assert agg.replica_order() == (store.map.keys(), 128)
+    exp_parts = [0] * P
+    n_ref = O.collect_replicas(rep, store, exp_parts)
+    assert agg.Collect_Replicas() == (n_ref, exp_parts)
+    for p in range(P):
+        assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}] (tree bin)")
+    agg.close()
+
+
 def test_ack_frame_sets_weight_address(ipls, O):
     """ThreadReceiver pid 4 (IPLS.java:491-498): the ACK frame's payload becomes
     Weight_Address[p]; GetPartitions then divides it."""
