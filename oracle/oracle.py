@@ -314,6 +314,53 @@ class JavaHashMap:
     def __len__(self):
         return self.size
 
+    def check_invariants(self) -> None:
+        """Structural checks, independent of how the table got here: every
+        node sits in its hash's bin, the lookup index and size agree with the
+        chains, and every tree bin is a valid red-black tree over exactly its
+        chain's nodes, rooted at the bin's first node, ordered by hash --
+        TreeNode.checkInvariants (which moveRootToFront asserts) plus the
+        red-black rules (black root, no red node with a red child, one black
+        height).  Raises AssertionError."""
+        seen = 0
+        for j, e in enumerate(self.table or []):
+            if e is None:
+                continue
+            chain, prev = [], None
+            while e is not None:
+                assert e.hash & (len(self.table) - 1) == j, "node outside its hash's bin"
+                assert self._nodes.get(e.key) is e, "lookup index is stale"
+                assert e.tree == self.table[j].tree, "tree and plain nodes mixed in one bin"
+                if e.tree:
+                    assert e.prev is prev, "prev link broken"
+                chain.append(e)
+                prev, e = e, e.next
+            seen += len(chain)
+            root = chain[0]
+            if not root.tree:
+                continue
+            assert root.parent is None and not root.red, "bin head is not a black root"
+            members = set()
+
+            def walk(t, lo, hi):                     # -> black height; lo/hi bound the hashes
+                if t is None:
+                    return 1
+                assert id(t) not in members, "cycle in tree"
+                members.add(id(t))
+                assert (lo is None or t.hash >= lo) and (hi is None or t.hash <= hi), "tree not ordered by hash"
+                for c in (t.left, t.right):
+                    if c is not None:
+                        assert c.parent is t, "parent link broken"
+                        assert not (t.red and c.red), "red node with a red child"
+                bl = walk(t.left, lo, t.hash)
+                br = walk(t.right, t.hash, hi)
+                assert bl == br, "unequal black heights"
+                return bl + (0 if t.red else 1)
+
+            walk(root, None, None)
+            assert members == {id(x) for x in chain}, "tree and chain hold different nodes"
+        assert seen == self.size == len(self._nodes), "size / index / chains disagree"
+
     def _treeify_bin(self, tab, hh):
         n = len(tab)
         if n < self.MIN_TREEIFY:

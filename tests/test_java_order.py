@@ -5,11 +5,13 @@ HashMap<Pair<Integer,String>, double[]> Other_Replica_Gradients
 - String / javatuples Pair hash codes: the oracle's restatement against
   published Java values, and the library's ipls_java_pair_hash against the
   oracle (UTF-8 including supplementary characters; malformed bytes refused).
-- The library front's order model (csrc/java_hashmap.hpp: bin under the
-  current capacity, then insertion order) against the oracle's simulation of
-  the JDK table itself (oracle.JavaHashMap: chains, resize splits, removes),
-  over random put/remove/clear streams built to collide, resize and trigger
-  treeifyBin's resize below 64 bins.
+- The library front's order model (csrc/java_hashmap.hpp) against the
+  oracle's simulation (oracle.JavaHashMap), two separate transliterations of
+  JDK 8's HashMap and TreeNode code, over random put/remove/clear streams
+  built to collide, resize, trigger treeifyBin's resize below 64 bins and
+  build, split and shrink red-black tree bins; the oracle's own structure is
+  checked after every step (TreeNode.checkInvariants plus the red-black
+  rules).
 Parity unpinned: no JDK here; the restatements follow the published JDK 8 and
 javatuples 1.2 sources."""
 import ctypes
@@ -139,6 +141,7 @@ def test_front_model_matches_jdk_table_simulation(O, seed, mode):
                 m.remove((p, a), hashes.pop((p, a)))
         else:
             cmds.append("o")
+            m.check_invariants()                     # the oracle's own structure, JDK's checkInvariants and more
             expect.append((len(m.table) if m.table else 0, int(m.tree_bin), int(m.nondeterministic), m.keys()))
             if r == 19 and rng.random() < 0.15:
                 cmds.append("c")
@@ -238,3 +241,42 @@ def test_library_codecs_match_java_pins():
         assert f"{f[0]} {bytes(got).hex()}" == want[c], c
         n += 1
     assert n == 6
+
+
+def test_oracle_tree_invariants_hold_and_catch_damage(O):
+    """The oracle's JavaHashMap after every operation of a colliding-hash
+    stream (trees built, grown, split, shrunk, untreeified) passes
+    check_invariants; and the checker is not vacuous: a recoloured node, a
+    swapped child and a stale prev link are each reported."""
+    rng = np.random.default_rng(11)
+    m, hs, trees = O.JavaHashMap(), {}, 0
+    for step in range(4000):
+        k = (int(rng.integers(0, 8)), int(rng.integers(0, 40)))
+        if rng.integers(0, 3) and k not in hs:
+            while True:   # distinct hashes with spread low 10 bits = 7: one bin up to 1024 bins
+                h = 7 + (1 << 10) * int(rng.integers(0, 64)) + (1 << 26) * int(rng.integers(0, 32))
+                if h not in hs.values():
+                    break
+            hs[k] = h
+            m.put(k, h, None)
+        elif k in hs:
+            m.remove(k, hs.pop(k))
+        m.check_invariants()
+        trees += m.tree_bin
+    assert trees > 1000 and not m.nondeterministic
+
+    def tree_head(mm):
+        return next(e for e in mm.table if e is not None and e.tree)
+
+    def damaged(hurt):
+        mm = O.JavaHashMap()
+        for j in range(20):
+            mm.put((0, j), 7 + (1 << 10) * (j + 1), None)
+        mm.check_invariants()
+        hurt(tree_head(mm))
+        with pytest.raises(AssertionError):
+            mm.check_invariants()
+
+    damaged(lambda r: setattr(r, "red", True))                                     # red root
+    damaged(lambda r: (setattr(r, "left", r.right), setattr(r, "right", r.left)))  # order broken
+    damaged(lambda r: setattr(r.next, "prev", None))                               # chain link broken
