@@ -268,8 +268,11 @@ int ipls_agg_other_replica_drop(ipls_agg *h, int p, int32_t aggregator);
 int ipls_agg_collect_replicas(ipls_agg *h, int32_t *participants);
 
 /* The order Collect_Replicas would fold the stored keys in right now, as
- * (partition, aggregator) pairs: pairs[2i], pairs[2i+1] for i < the returned
- * count (at most max_pairs written; pairs may be NULL to ask for the count).
+ * (partition, aggregator) pairs: pairs[2i], pairs[2i+1].  Returns the number
+ * of stored keys and writes the first min(that, max_pairs) of them (pairs may
+ * be NULL with max_pairs 0 to ask for the count); a return above max_pairs
+ * means the list was cut -- another thread may have stored keys since the
+ * count was asked for -- and the caller asks again with more room.
  * A diagnostic for a Java caller to check the library's HashMap model against
  * its own `new ArrayList<>(Other_Replica_Gradients.keySet())`.  *capacity
  * (nullable) receives the model's table capacity (0 after new HashMap<>()). */

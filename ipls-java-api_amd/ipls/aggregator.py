@@ -379,11 +379,14 @@ class Aggregator:
         """(keys, capacity): the (partition, aggregator) order Collect_Replicas
         would fold in now -- the library's model of the JDK HashMap's keySet()
         order -- and the model's table capacity."""
-        n = self._chk(self._lib.ipls_agg_replica_order(self._h, None, 0, None))
-        buf = (ctypes.c_int32 * max(2, 2 * n))()
+        room = self._chk(self._lib.ipls_agg_replica_order(self._h, None, 0, None))
         cap = ctypes.c_int32()
-        n = self._chk(self._lib.ipls_agg_replica_order(self._h, buf, n, ctypes.byref(cap)))
-        return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)], cap.value
+        while True:   # keys stored by another thread in between: ask again with more room
+            buf = (ctypes.c_int32 * max(2, 2 * room))()
+            n = self._chk(self._lib.ipls_agg_replica_order(self._h, buf, room, ctypes.byref(cap)))
+            if n <= room:
+                return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)], cap.value
+            room = n
 
     def Collect_Replicas(self):
         """IPLS.java:1217-1241: fold every stored Other_Replica_Gradients array

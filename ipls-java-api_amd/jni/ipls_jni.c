@@ -491,11 +491,17 @@ JNIEXPORT jboolean JNICALL Java_NativeAggregator_otherReplicaDrop(JNIEnv *env, j
  * its HashMap model against the JVM's own keySet() order). */
 JNIEXPORT jintArray JNICALL Java_NativeAggregator_replicaKeyOrder(JNIEnv *env, jclass c, jlong h) {
     (void)c;
-    int n = LIB(ipls_agg_replica_order(H(h), NULL, 0, NULL));
-    if (n < 0) { throw_for(env, n, H(h)); return NULL; }
-    int32_t *pairs = (int32_t *)malloc((size_t)(n > 0 ? 2 * n : 2) * sizeof(int32_t));
-    if (!pairs) { throw_msg(env, "java/lang/OutOfMemoryError", "replicaKeyOrder"); return NULL; }
-    n = LIB(ipls_agg_replica_order(H(h), pairs, n, NULL));
+    int room = LIB(ipls_agg_replica_order(H(h), NULL, 0, NULL)), n;
+    if (room < 0) { throw_for(env, room, H(h)); return NULL; }
+    int32_t *pairs = NULL;
+    for (;;) {   /* keys stored by another thread in between: ask again with more room */
+        free(pairs);
+        pairs = (int32_t *)malloc((size_t)(room > 0 ? 2 * (size_t)room : 2) * sizeof(int32_t));
+        if (!pairs) { throw_msg(env, "java/lang/OutOfMemoryError", "replicaKeyOrder"); return NULL; }
+        n = LIB(ipls_agg_replica_order(H(h), pairs, room, NULL));
+        if (n <= room) break;
+        room = n;
+    }
     jintArray res = NULL;
     if (n < 0) {
         throw_for(env, n, H(h));

@@ -3,6 +3,7 @@ committed golden fixtures.  Bit-exact for every element (NaN == NaN; payloads
 unspecified by Java).  Parity status of the oracle itself: unpinned
  -- see oracle/__init__.py.
 """
+import ctypes
 import hashlib
 
 import numpy as np
@@ -1174,6 +1175,14 @@ def test_replica_store_argument_errors(ipls, O):
     with pytest.raises(ipls.IplsError):
         agg.OtherReplicaDrop(-1, 4)
     assert agg.replica_order() == before
+    # a buffer with less room than there are keys: the full count comes back,
+    # only max_pairs pairs are written (the callers ask again with more room)
+    agg.OtherReplicaGradients(1, 5, O.synth_bucket(L, 1, 2), key_hash=O.java_pair_hash(1, "12D3KooWB"))
+    keys, _ = agg.replica_order()
+    buf = (ctypes.c_int32 * 4)(*([-7] * 4))
+    assert agg._lib.ipls_agg_replica_order(agg._h, buf, 1, None) == 2
+    assert list(buf) == [keys[0][0], keys[0][1], -7, -7]
+    assert agg.OtherReplicaDrop(1, 5) is True
     n, parts = agg.Collect_Replicas()
     assert (n, parts) == (1, [L, 0])
     assert_bits_equal(agg.read(0, ipls.TGT_REP), 0.0 + g, "REP[0]")    # folded once, not twice
