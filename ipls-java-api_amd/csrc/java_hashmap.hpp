@@ -196,6 +196,54 @@ class JavaHashOrder {
   }
   bool nondeterministic() const { return nondet_; }
 
+  // Structural checks (for tests; nullptr = sound): every node in its hash's
+  // bin, index / size / chains agree, and every tree bin is a red-black tree
+  // over exactly its chain's nodes, rooted at the bin's first node, ordered
+  // by hash -- TreeNode.checkInvariants plus the red-black rules.
+  const char* check_invariants() const {
+    size_t seen = 0;
+    const int n = (int)tab_.size();
+    for (int j = 0; j < n; ++j) {
+      const int head = tab_[(size_t)j];
+      if (head < 0) continue;
+      std::vector<int> chain;
+      for (int e = head, prev = -1; e >= 0; prev = e, e = nd(e).next) {
+        if ((nd(e).hash & (n - 1)) != j) return "node outside its hash's bin";
+        auto it = index_.find(nd(e).key);
+        if (it == index_.end() || it->second.second != e) return "lookup index is stale";
+        if (nd(e).tree != nd(head).tree) return "tree and plain nodes mixed in one bin";
+        if (nd(e).tree && nd(e).prev != prev) return "prev link broken";
+        if (chain.size() > index_.size()) return "cycle in chain";
+        chain.push_back(e);
+      }
+      seen += chain.size();
+      if (!nd(head).tree) continue;
+      if (nd(head).parent >= 0 || nd(head).red) return "bin head is not a black root";
+      std::vector<int> members;
+      const char* bad = nullptr;
+      // -> black height; lo/hi bound the hashes (inclusive: ties may sit either side after rotations)
+      auto walk = [&](auto&& self, int t, int64_t lo, int64_t hi) -> int {
+        if (t < 0 || bad) return 1;
+        if (members.size() > chain.size()) { bad = "cycle in tree"; return 1; }
+        members.push_back(t);
+        const Node& x = nd(t);
+        if (x.hash < lo || x.hash > hi) { bad = "tree not ordered by hash"; return 1; }
+        for (int c : {x.left, x.right})
+          if (c >= 0 && (nd(c).parent != t || (x.red && nd(c).red))) { bad = "parent link or red-red"; return 1; }
+        const int bl = self(self, x.left, lo, x.hash), br = self(self, x.right, x.hash, hi);
+        if (bl != br) bad = "unequal black heights";
+        return bl + (x.red ? 0 : 1);
+      };
+      walk(walk, head, INT64_MIN, INT64_MAX);
+      if (bad) return bad;
+      std::sort(members.begin(), members.end());
+      std::sort(chain.begin(), chain.end());
+      if (members != chain) return "tree and chain hold different nodes";
+    }
+    if (seen != index_.size() || (int64_t)seen != (int64_t)size_) return "size / index / chains disagree";
+    return nullptr;
+  }
+
  private:
   static constexpr int kTreeify = 8, kUntreeify = 6, kMinTreeify = 64;
   struct Node {

@@ -6,6 +6,8 @@
 //   r <partition> <aggregator>          remove
 //   o                                   print "<capacity> <tree_bin> <nondeterministic> p:a p:a ..."
 //   c                                   clear (new HashMap<>())
+// After every command the model's structure is checked (check_invariants);
+// a failure is printed to stderr and ends the run with status 3.
 #include <cstdio>
 #include <cstring>
 
@@ -31,6 +33,10 @@ int main() {
       m.clear();
     } else {
       return 2;
+    }
+    if (const char* bad = m.check_invariants()) {
+      std::fprintf(stderr, "invariant: %s\n", bad);
+      return 3;
     }
   }
   return 0;
