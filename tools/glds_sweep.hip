@@ -125,7 +125,9 @@ int main(int argc, char** argv) {
   const int64_t L = argc > 2 ? atoll(argv[2]) : 4194304;
   const int K = argc > 3 ? atoi(argv[3]) : 32;
   const int REPS = argc > 4 ? atoi(argv[4]) : 10;
-  const bool be_out = getenv("GLDS_NATIVE_OUT") == nullptr;
+  // GLDS_NATIVE=1: native doubles in and out (against the shipped native fold)
+  const bool native = getenv("GLDS_NATIVE") != nullptr;
+  const bool be_out = !native && getenv("GLDS_NATIVE_OUT") == nullptr;
   if (L % (1024 * 2 * 16) != 0) {
     fprintf(stderr, "L must be a multiple of 32768\n");
     return 2;
@@ -140,7 +142,8 @@ int main(int argc, char** argv) {
       unsigned long long* b = base + (int64_t)(p * K + k) * stride;
       ptrs[p * K + k] = b;
       const unsigned long long key = 0x1B52026ULL ^ ((unsigned long long)p << 40) ^ ((unsigned long long)k << 32);
-      hipLaunchKernelGGL(k_synth<true>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
+      if (native) hipLaunchKernelGGL(k_synth<false>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
+      else hipLaunchKernelGGL(k_synth<true>, dim3(4096), dim3(kBlock), 0, 0, b, L, key);
     }
   const unsigned long long** d_ptrs;
   CK(hipMalloc(&d_ptrs, ptrs.size() * 8));
@@ -161,9 +164,12 @@ int main(int argc, char** argv) {
   auto bp = (const unsigned long long* const*)d_ptrs;
 
   std::vector<Var> vars;
-  vars.push_back(Var{"shipped BE R=16 BS=1024 SEQF=3", [=](hipStream_t s) {
+  vars.push_back(Var{"shipped R=16 BS=1024 (BE: SEQF=3)", [=](hipStream_t s) {
                        const int tpp = (int)(L / (1024 * 2 * 16));
-                       if (be_out)
+                       if (native)
+                         hipLaunchKernelGGL((k_reduce<false, false, kZero, 1, 16, true, 0, 1024>), dim3(tpp * P),
+                                            dim3(1024), 0, s, bp, d_pd, K, tpp, P);
+                       else if (be_out)
                          hipLaunchKernelGGL((k_reduce<true, true, kZero, 1, 16, true, 0, 1024, 3>), dim3(tpp * P),
                                             dim3(1024), 0, s, bp, d_pd, K, tpp, P);
                        else
@@ -179,7 +185,10 @@ int main(int argc, char** argv) {
 #define GL(R, BS, G, D)                                                                                  \
   vars.push_back(Var{"glds R=" #R " BS=" #BS " G=" #G " D=" #D, [=](hipStream_t s) {                     \
                        const int tpp = (int)(L / ((int64_t)BS * 2 * R));                                 \
-                       if (be_out)                                                                       \
+                       if (native)                                                                       \
+                         hipLaunchKernelGGL((k_glds<false, false, R, BS, G, D>), dim3(tpp * P), dim3(BS), 0, s, \
+                                            bp, d_pd, K, tpp);                                           \
+                       else if (be_out)                                                                  \
                          hipLaunchKernelGGL((k_glds<true, true, R, BS, G, D>), dim3(tpp * P), dim3(BS), 0, s, \
                                             bp, d_pd, K, tpp);                                           \
                        else                                                                              \
@@ -232,8 +241,8 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       v.ms.push_back(ms);
     }
-  printf("# P=%d L=%lld K=%d REPS=%d BE in%s; algorithmic bytes/launch=%.0f\n", P, (long long)L, K, REPS,
-         be_out ? " + out" : ", native out", alg);
+  printf("# P=%d L=%lld K=%d REPS=%d %s; algorithmic bytes/launch=%.0f\n", P, (long long)L, K, REPS,
+         native ? "native doubles in and out" : be_out ? "BE in + out" : "BE in, native out", alg);
   for (auto& v : vars) {
     std::sort(v.ms.begin(), v.ms.end());
     const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
