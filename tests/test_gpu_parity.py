@@ -1791,6 +1791,10 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     # aggregator peer IDs: odd seeds pass the Pair hash of a real-looking ID
     # (ipls_agg_other_replica_keyed), even seeds the index-as-ID default
     peer_ids = [f"12D3KooW{seed}x{i}{'Q' * (i % 3)}" for i in range(5)]
+    # seeds 2 mod 3: keyed hashes that share their low 6 bits (one HashMap bin
+    # up to 64 bins), more store traffic and rare collects, so the store's
+    # map resizes through treeifyBin and grows red-black tree bins
+    collide = seed % 3 == 2
     msgs = [O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmS")) for g in pool]
     script = list(prefix)
     for step in range(len(script) + steps):
@@ -1799,6 +1803,8 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
         def draw(key, fn):
             return fixed[key] if key in fixed else fn()
         op = draw("op", lambda: int(rng.integers(0, 17)))
+        if collide and op in (8, 16) and "op" not in fixed:
+            op = 14
         p = draw("p", lambda: int(rng.integers(0, P)))
         k = int(rng.integers(0, len(pool)))
         g = pool[k]
@@ -1886,13 +1892,22 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
             gbuf[:n] = g[:n]
             M["agg"][p] = M["agg"][p] + gbuf
         elif op == 14:                                      # Download_Scheduler: another aggregator's bucket
-            a = int(rng.integers(0, 5))
+            a = int(rng.integers(0, 12 if collide else 5))
             if rng.integers(0, 4) == 0:                     # its partial arrived: Other_Replica_Gradients.remove
                 assert agg.OtherReplicaDrop(p, a) == O.other_replica_drop(store, p, a)
             else:
-                kh = O.java_pair_hash(p, peer_ids[a]) if seed % 2 else None
+                if collide:
+                    kh = 0x1A + 64 * (p * 12 + a)
+                else:
+                    kh = O.java_pair_hash(p, peer_ids[a]) if seed % 2 else None
                 agg.OtherReplicaGradients(p, a, g, key_hash=kh)
                 O.other_replica_add(store, p, a, g, key_hash=kh)
+            if collide:                                     # the library's model vs the JDK simulation
+                assert agg.replica_order()[0] == store.map.keys(), f"step {step}: replica order"
+                if shapes is not None and store.map.tree_bin:
+                    shapes.add(("replica store", "tree bin", 0, False, -1))
+        elif op == 15 and collide and rng.integers(0, 6):  # (collide: most collects skipped)
+            pass
         elif op == 15:                                      # Collect_Replicas
             n, part = agg.Collect_Replicas()
             exp_part = [0] * P

@@ -18,6 +18,7 @@ import test_gpu_parity as T  # noqa: E402
 
 def main(first=100, n=200, mode="small"):
     t0 = time.time()
+    collide_seeds = tree_seeds = 0
     big = mode == "big"
     for seed in range(first, first + n):
         group = [1, 2, 3, 5, 8, 16, 32, 64][seed % 8]
@@ -32,10 +33,15 @@ def main(first=100, n=200, mode="small"):
             continue
         P = 1 + seed % 5
         L = [2, 3, 17, 1024, 5003, 65537, 262147][seed % 7]
-        T.test_stateful_random_sequence(ipls, O, seed, group, devices, P=P, L=L)
+        shapes = set()
+        T.test_stateful_random_sequence(ipls, O, seed, group, devices, P=P, L=L, shapes=shapes)
+        if seed % 3 == 2:   # the colliding-hash seeds: did the replica store grow a tree bin?
+            collide_seeds += 1
+            tree_seeds += any(sh[0] == "replica store" for sh in shapes)
         if (seed - first) % 20 == 19:
             print(f"seeds {first}..{seed} ok ({time.time() - t0:.0f} s)", flush=True)
-    print(f"fuzz ok: {n} seeds x 300 steps", flush=True)
+    print(f"fuzz ok: {n} seeds x 300 steps; replica-store tree bins in {tree_seeds} of {collide_seeds} "
+          f"colliding-hash seeds", flush=True)
 
 
 if __name__ == "__main__":
