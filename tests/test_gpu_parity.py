@@ -1905,7 +1905,7 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
             if collide:                                     # the library's model vs the JDK simulation
                 assert agg.replica_order()[0] == store.map.keys(), f"step {step}: replica order"
                 if shapes is not None and store.map.tree_bin:
-                    shapes.add(("replica store", "tree bin", 0, False, -1))
+                    shapes.add(("replica store", "tree bin", "", False, -1))
         elif op == 15 and collide and rng.integers(0, 6):  # (collide: most collects skipped)
             pass
         elif op == 15:                                      # Collect_Replicas

@@ -29,7 +29,7 @@ def main(first=100, n=200, mode="small"):
             shapes = set()
             T.test_stateful_random_sequence(ipls, O, seed, group, devices, P=P, L=L, shapes=shapes)
             print(f"seed {seed} ok: P={P} L={L} group={group} devices={devices} "
-                  f"(kernel, shape, map, be, start) reached {sorted(shapes)} ({time.time() - t0:.0f} s)", flush=True)
+                  f"(kernel, shape, map, be, start) reached {sorted(shapes, key=repr)} ({time.time() - t0:.0f} s)", flush=True)
             continue
         P = 1 + seed % 5
         L = [2, 3, 17, 1024, 5003, 65537, 262147][seed % 7]
