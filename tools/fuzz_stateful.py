@@ -28,6 +28,9 @@ def main(first=100, n=200, mode="small"):
             L = [4 * 1048576 + 5, 2 * 1048576 + 3, 4 * 1048576, 1048576 + 7][(seed // 4) % 4]
             shapes = set()
             T.test_stateful_random_sequence(ipls, O, seed, group, devices, P=P, L=L, shapes=shapes)
+            if seed % 3 == 2:
+                collide_seeds += 1
+                tree_seeds += any(sh[0] == "replica store" for sh in shapes)
             print(f"seed {seed} ok: P={P} L={L} group={group} devices={devices} "
                   f"(kernel, shape, map, be, start) reached {sorted(shapes, key=repr)} ({time.time() - t0:.0f} s)", flush=True)
             continue
