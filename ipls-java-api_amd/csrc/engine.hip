@@ -24,6 +24,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1656,9 +1657,11 @@ int dev_collect_replicas(ipls_dev* h, int32_t* participants, const int32_t* orde
     return fail(h, IPLS_E_INVAL, "collect order lists %d keys, the store holds %zu", n_order, h->other.size());
   std::vector<std::map<std::pair<int, int32_t>, ipls_dev::OtherRep>::iterator> seq;
   seq.reserve(n_order);
+  std::set<std::pair<int, int32_t>> seen;   // each key once (O(n log n) for large stores)
   for (int i = 0; i < n_order; ++i) {
-    auto it = h->other.find(std::make_pair((int)order[2 * i], order[2 * i + 1]));
-    if (it == h->other.end() || std::find(seq.begin(), seq.end(), it) != seq.end())
+    const std::pair<int, int32_t> key((int)order[2 * i], order[2 * i + 1]);
+    auto it = h->other.find(key);
+    if (it == h->other.end() || !seen.insert(key).second)
       return fail(h, IPLS_E_INVAL, "collect order key (%d, %d) is not a stored key", order[2 * i] + h->p_lo,
                   order[2 * i + 1]);
     seq.push_back(it);

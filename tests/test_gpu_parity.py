@@ -1318,6 +1318,36 @@ def test_collect_replicas_order_through_a_tree_bin(ipls, O):
     agg.close()
 
 
+def test_collect_replicas_many_keys(ipls, O):
+    """A store of ~1,500 keys (64 partitions x up to 40 aggregators, real
+    Pair hashes of peer-ID strings; the map grows to 2,048 bins), with drops:
+    the library's order equals the JDK simulation's, and the collect folds
+    every key into REP bit for bit with the reference's Participants."""
+    L, P, A = 33, 64, 40
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
+    store = O.ReplicaStore()
+    rep = [np.zeros(L) for _ in range(P)]
+    rng = np.random.default_rng(17)
+    for i in range(2600):
+        p, a = int(rng.integers(0, P)), int(rng.integers(0, A))
+        if rng.integers(0, 10) == 0:
+            assert agg.OtherReplicaDrop(p, a) == O.other_replica_drop(store, p, a)
+            continue
+        g = O.synth_bucket(L, p, i) * float(10.0 ** rng.integers(-6, 7))
+        kh = O.java_pair_hash(p, f"QmPeer{a:03d}")
+        agg.OtherReplicaGradients(p, a, g, key_hash=kh)
+        O.other_replica_add(store, p, a, g, key_hash=kh)
+    assert len(store.map) > 1200 and len(store.map.table) >= 2048
+    assert agg.replica_order() == (store.map.keys(), len(store.map.table))
+    exp_parts = [0] * P
+    n_ref = O.collect_replicas(rep, store, exp_parts)
+    assert agg.Collect_Replicas() == (n_ref, exp_parts)
+    for p in range(P):
+        assert_bits_equal(agg.read(p, ipls.TGT_REP), rep[p], f"REP[{p}] (many keys)")
+    assert agg.replica_order() == ([], 0)
+    agg.close()
+
+
 def test_ack_frame_sets_weight_address(ipls, O):
     """ThreadReceiver pid 4 (IPLS.java:491-498): the ACK frame's payload becomes
     Weight_Address[p]; GetPartitions then divides it."""
