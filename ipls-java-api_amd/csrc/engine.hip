@@ -381,6 +381,14 @@ int d2h(ipls_dev* h, void* dst, const void* src, size_t bytes) {
 
 unsigned blocks_for(int64_t n, int64_t per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 
+// The elementwise kernels (k_fold_n, k_blend, k_scale, k_encode_secure) take
+// their 16-B tile shape when every operand is 16-B aligned: one block per
+// kEwTile elements; otherwise the 8-B grid-stride loop on a capped grid.
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static dim3 ew_grid(int64_t n, bool vec, unsigned cap) {
+  return dim3(std::max(1u, vec ? blocks_for(n, kEwTile) : std::min<unsigned>(blocks_for(n, kBlock), cap)));
+}
+
 // ---- kernel dispatch: k_reduce ----
 // Three shapes (tools/reduce_sweep.hip, profiles/r01/sweep*.txt), the first
 // whose tiles fill the 256 CUs (fill()):
@@ -1611,8 +1619,13 @@ int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, i
   if (first) HIP_TRY(h, hipMalloc(&dst, (size_t)std::max<int64_t>(n, 1) * 8));
   hipError_t e = hipSuccess;
   if (n > 0) {
-    const dim3 g(std::min<unsigned>(blocks_for(n, kBlock), 4096));
-#define FN(B, F) hipLaunchKernelGGL((k_fold_n<B, F>), g, dim3(kBlock), 0, h->stream, dst, d, n)
+    const bool vec = al16(dst) && al16(d);
+    const dim3 g = ew_grid(n, vec, 4096);
+#define FN(B, F)                                                                                         \
+  do {                                                                                                   \
+    if (vec) hipLaunchKernelGGL((k_fold_n<B, F, true>), g, dim3(kBlock), 0, h->stream, dst, d, n);      \
+    else hipLaunchKernelGGL((k_fold_n<B, F, false>), g, dim3(kBlock), 0, h->stream, dst, d, n);         \
+  } while (0)
     if (be) { if (first) FN(true, true); else FN(true, false); }
     else { if (first) FN(false, true); else FN(false, false); }
 #undef FN
@@ -1685,9 +1698,14 @@ int dev_collect_replicas(ipls_dev* h, int32_t* participants, const int32_t* orde
       participants[p] = (int32_t)((uint32_t)participants[p] + (uint32_t)it->second.received * (uint32_t)n);
     if (n > 0) {
       if (int rc = materialize(h, p, IPLS_TGT_REP)) return rc;
-      hipLaunchKernelGGL((k_fold_n<false, false>), dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)),
-                         dim3(kBlock), 0, h->stream, (unsigned long long*)(h->arena + h->rep_off[p]),
-                         it->second.d, n);
+      auto rdst = (unsigned long long*)(h->arena + h->rep_off[p]);
+      const bool vec = al16(rdst) && al16(it->second.d);
+      if (vec)
+        hipLaunchKernelGGL((k_fold_n<false, false, true>), ew_grid(n, true, 4096), dim3(kBlock), 0, h->stream, rdst,
+                           it->second.d, n);
+      else
+        hipLaunchKernelGGL((k_fold_n<false, false, false>), ew_grid(n, false, 4096), dim3(kBlock), 0, h->stream,
+                           rdst, it->second.d, n);
       HIP_TRY(h, hipGetLastError());
     }
     ++folded;
@@ -2122,9 +2140,16 @@ int dev_blend(ipls_dev* h, int p, int target, const void* src, int64_t n, int sr
   }
   if (int rc = materialize(h, p, target)) return rc;
   double* t = h->arena + target_off(h, p, target);
-  const dim3 g(std::min<unsigned>(blocks_for(L, kBlock), 8192));
-  if (be) hipLaunchKernelGGL(k_blend<true>, g, dim3(kBlock), 0, h->stream, t, (const unsigned long long*)d, L, a, b);
-  else hipLaunchKernelGGL(k_blend<false>, g, dim3(kBlock), 0, h->stream, t, (const unsigned long long*)d, L, a, b);
+  const bool vec = al16(t) && al16(d);
+  const dim3 g = ew_grid(L, vec, 8192);
+  auto gs = (const unsigned long long*)d;
+  if (be) {
+    if (vec) hipLaunchKernelGGL((k_blend<true, true>), g, dim3(kBlock), 0, h->stream, t, gs, L, a, b);
+    else hipLaunchKernelGGL((k_blend<true, false>), g, dim3(kBlock), 0, h->stream, t, gs, L, a, b);
+  } else {
+    if (vec) hipLaunchKernelGGL((k_blend<false, true>), g, dim3(kBlock), 0, h->stream, t, gs, L, a, b);
+    else hipLaunchKernelGGL((k_blend<false, false>), g, dim3(kBlock), 0, h->stream, t, gs, L, a, b);
+  }
   HIP_TRY(h, hipGetLastError());
   return IPLS_OK;
 }
@@ -2138,8 +2163,12 @@ int dev_scale(ipls_dev* h, int p, int dst_target, int src_target, double c) {
   if (int rc = materialize(h, p, src_target)) return rc;
   if (uint8_t* f = zero_flag(h, p, dst_target)) *f = 0;
   const int64_t L = h->len[p];
-  hipLaunchKernelGGL(k_scale, dim3(std::min<unsigned>(blocks_for(L, kBlock), 8192)), dim3(kBlock), 0, h->stream,
-                     h->arena + target_off(h, p, dst_target), (const double*)(h->arena + target_off(h, p, src_target)), L, c);
+  double* sd = h->arena + target_off(h, p, dst_target);
+  auto ss = (const double*)(h->arena + target_off(h, p, src_target));
+  if (al16(sd) && al16(ss))
+    hipLaunchKernelGGL(k_scale<true>, ew_grid(L, true, 8192), dim3(kBlock), 0, h->stream, sd, ss, L, c);
+  else
+    hipLaunchKernelGGL(k_scale<false>, ew_grid(L, false, 8192), dim3(kBlock), 0, h->stream, sd, ss, L, c);
   HIP_TRY(h, hipGetLastError());
   return IPLS_OK;
 }
@@ -2149,15 +2178,22 @@ int ipls_encode_secure(const void* src, void* dst, int64_t n, int src_kind, int 
   if ((src_kind != IPLS_DEV_F64 && src_kind != IPLS_DEV_BE) || (dst_kind != IPLS_DEV_F64 && dst_kind != IPLS_DEV_BE))
     return fail(nullptr, IPLS_E_INVAL, "device operands only (DEV_F64 / DEV_BE)");
   if (n == 0) return IPLS_OK;
-  const dim3 g(std::min<unsigned>(blocks_for(n, kBlock), 8192));
   hipStream_t st = (hipStream_t)stream;
   auto s = (const unsigned long long*)src;
   auto d = (unsigned long long*)dst;
   const bool bi = src_kind == IPLS_DEV_BE, bo = dst_kind == IPLS_DEV_BE;
-  if (bi && bo) hipLaunchKernelGGL((k_encode_secure<true, true>), g, dim3(kBlock), 0, st, s, d, n);
-  else if (bi) hipLaunchKernelGGL((k_encode_secure<true, false>), g, dim3(kBlock), 0, st, s, d, n);
-  else if (bo) hipLaunchKernelGGL((k_encode_secure<false, true>), g, dim3(kBlock), 0, st, s, d, n);
-  else hipLaunchKernelGGL((k_encode_secure<false, false>), g, dim3(kBlock), 0, st, s, d, n);
+  const bool vec = al16(s) && al16(d);
+  const dim3 g = ew_grid(n, vec, 8192);
+#define ENC(BI, BO)                                                                                     \
+  do {                                                                                                  \
+    if (vec) hipLaunchKernelGGL((k_encode_secure<BI, BO, true>), g, dim3(kBlock), 0, st, s, d, n);      \
+    else hipLaunchKernelGGL((k_encode_secure<BI, BO, false>), g, dim3(kBlock), 0, st, s, d, n);         \
+  } while (0)
+  if (bi && bo) ENC(true, true);
+  else if (bi) ENC(true, false);
+  else if (bo) ENC(false, true);
+  else ENC(false, false);
+#undef ENC
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(nullptr, IPLS_E_DEVICE, "k_encode_secure: %s", hipGetErrorString(e));
   return IPLS_OK;
@@ -2300,13 +2336,17 @@ int64_t dev_merge_files(ipls_dev* h, const uint8_t* const* files, const int64_t*
     if (nd[i] == 0) continue;
     if (int rc = ensure_scratch(h, (size_t)nd[i] * 8)) return rc;
     if (int rc = stage_h2d(h, h->d_scratch, files[i] + off[i], (size_t)nd[i] * 8)) return rc;
-    const dim3 g(std::min<unsigned>(blocks_for(nd[i], kBlock), 4096));
-    if (i == 0)   // Aggregation = GetParameters(Hashes.get(0)): the first file as is
-      hipLaunchKernelGGL((k_fold_n<true, true>), g, dim3(kBlock), 0, h->stream, h->d_merge,
-                         (const unsigned long long*)h->d_scratch, nd[i]);
-    else
-      hipLaunchKernelGGL((k_fold_n<true, false>), g, dim3(kBlock), 0, h->stream, h->d_merge,
-                         (const unsigned long long*)h->d_scratch, nd[i]);
+    // (both device buffers come from hipMalloc: the tile shape)
+    const bool vec = al16(h->d_merge) && al16(h->d_scratch);
+    const dim3 g = ew_grid(nd[i], vec, 4096);
+    auto msrc = (const unsigned long long*)h->d_scratch;
+    if (i == 0) {   // Aggregation = GetParameters(Hashes.get(0)): the first file as is
+      if (vec) hipLaunchKernelGGL((k_fold_n<true, true, true>), g, dim3(kBlock), 0, h->stream, h->d_merge, msrc, nd[i]);
+      else hipLaunchKernelGGL((k_fold_n<true, true, false>), g, dim3(kBlock), 0, h->stream, h->d_merge, msrc, nd[i]);
+    } else {
+      if (vec) hipLaunchKernelGGL((k_fold_n<true, false, true>), g, dim3(kBlock), 0, h->stream, h->d_merge, msrc, nd[i]);
+      else hipLaunchKernelGGL((k_fold_n<true, false, false>), g, dim3(kBlock), 0, h->stream, h->d_merge, msrc, nd[i]);
+    }
     HIP_TRY(h, hipGetLastError());
   }
   // update_file(..., Aggregation): putDouble per element (MyIPFSClass.java:105-116)

@@ -818,6 +818,65 @@ def test_async_variants(ipls, O):
     agg.close()
 
 
+@pytest.mark.parametrize("L", [1, 2047, 2048, 2049, 6149, 20011])
+def test_elementwise_kernels_both_shapes(ipls, O, L):
+    """k_blend, k_scale, k_encode_secure and k_fold_n take a 16-B tile shape
+    (2,048 elements per block) when every operand is 16-B aligned and an 8-B
+    grid-stride loop otherwise.  Device operands at a 16-B boundary and at
+    8 mod 16, at lengths around the tile (one element, one short of a tile,
+    a tile, one over, three tiles and a tail): the bits equal the oracle's
+    either way, native and big-endian."""
+    pool = torch.empty(4 * L + 8, dtype=torch.float64, device="cuda")
+    pool_be = torch.empty(8 * (4 * L + 8), dtype=torch.uint8, device="cuda")
+    assert pool.data_ptr() % 16 == 0 and pool_be.data_ptr() % 16 == 0
+
+    def dev_at(x, shift, be=False):       # x placed at a 16-B boundary (shift 0) or 8 mod 16 (shift 1)
+        if be:
+            b = np.frombuffer(O.be_encode(x), dtype=np.uint8)
+            pool_be[8 * shift:8 * shift + b.size].copy_(torch.from_numpy(b.copy()))
+            return ipls.DeviceBuffer(int(pool_be.data_ptr()) + 8 * shift, len(x), big_endian=True)
+        pool[shift:shift + len(x)].copy_(torch.from_numpy(x))
+        return ipls.DeviceBuffer(int(pool.data_ptr()) + 8 * shift, len(x))
+
+    for shift in (0, 1):
+        agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+        w0 = O.synth_bucket(L, 4, shift) * 37.0
+        agg.cache_partition(0, w0)
+        g1, g2 = O.synth_bucket(L, 4, 10 + shift), O.synth_bucket(L, 4, 20 + shift)
+        agg.UpdateAsyncReplica(dev_at(g1, shift), 0)                  # k_blend, native
+        torch.cuda.synchronize()
+        agg.UpdateLeavingPeer(dev_at(g2, shift, be=True), 0)          # k_blend, big-endian
+        w = O.blend(O.blend(w0, g1, 0.75, 1.0), g2, 0.6, 1 - 0.6)
+        assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), w, f"blends L={L} shift={shift}")
+        agg.AsyncPublishScale(0)                                        # k_scale (arena: aligned)
+        assert_bits_equal(agg.read(0, ipls.TGT_AGG), O.scale(w, 0.25), f"scale L={L}")
+        # k_fold_n: stored download (FIRST), a second one folded in, then the collect into REP
+        store = O.ReplicaStore()
+        for k, be in ((30, False), (31, True)):
+            gk = O.synth_bucket(L, 4, k + shift) * 1e3
+            agg.OtherReplicaGradients(0, 7, dev_at(gk, shift, be=be))
+            torch.cuda.synchronize()
+            O.other_replica_add(store, 0, 7, gk)
+        rep = [np.zeros(L)]
+        O.collect_replicas(rep, store, [0])
+        agg.Collect_Replicas()
+        assert_bits_equal(agg.read(0, ipls.TGT_REP), rep[0], f"replica fold L={L} shift={shift}")
+        agg.close()
+        # k_encode_secure between device buffers, every byte-order pairing
+        x = O.synth_bucket(L, 5, shift) * 3000.0
+        x[::7] = 11.0
+        x[1::7] = -11.0
+        want = O.encode_secure(x)
+        src = dev_at(x, shift)
+        for bo in (False, True):
+            out = torch.zeros(8 * (L + 2), dtype=torch.uint8, device="cuda")
+            dst = ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, L, big_endian=bo)
+            ipls.encode_secure(src, dst)
+            torch.cuda.synchronize()
+            got = bytes(out[8 * shift:8 * (shift + L)].cpu().numpy())
+            assert got == (O.be_encode(want) if bo else want.tobytes()), f"encode_secure L={L} shift={shift} be={bo}"
+
+
 def test_encode_secure_device(ipls, O, golden):
     x = golden["enc_in"]
     t, d = dev(x)
