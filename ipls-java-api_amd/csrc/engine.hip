@@ -388,6 +388,10 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static dim3 ew_grid(int64_t n, bool vec, unsigned cap) {
   return dim3(std::max(1u, vec ? blocks_for(n, kEwTile) : std::min<unsigned>(blocks_for(n, kBlock), cap)));
 }
+static void launch_bswap(hipStream_t st, const unsigned long long* in, unsigned long long* out, int64_t n) {
+  if (al16(in) && al16(out)) hipLaunchKernelGGL(k_bswap64<true>, ew_grid(n, true, 4096), dim3(kBlock), 0, st, in, out, n);
+  else hipLaunchKernelGGL(k_bswap64<false>, ew_grid(n, false, 4096), dim3(kBlock), 0, st, in, out, n);
+}
 
 // ---- kernel dispatch: k_reduce ----
 // Three shapes (tools/reduce_sweep.hip, profiles/r01/sweep*.txt), the first
@@ -1272,8 +1276,7 @@ static int gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, bool* zero
       // double-buffered like the per-arrival buckets (stage_bucket)
       if (int rc = stage_bucket(h, bytes, (size_t)nw * 8, &dsrc)) return rc;
     }
-    hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(nw, kBlock), 4096)), dim3(kBlock), 0,
-                       h->stream, (const unsigned long long*)dsrc, h->d_gbuf, nw);
+    launch_bswap(h->stream, (const unsigned long long*)dsrc, h->d_gbuf, nw);
     HIP_TRY(h, hipGetLastError());
     if (!*zero_copy)
       if (int rc = release_stage(h)) return rc;
@@ -1379,14 +1382,12 @@ int dev_read(ipls_dev* h, int p, int target, void* dst, int64_t n, int dst_kind)
       HIP_TRY(h, hipMemcpyAsync(dst, srcd, (size_t)L * 8, hipMemcpyDeviceToDevice, h->stream));
       return IPLS_OK;
     case IPLS_DEV_BE:
-      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
-                         h->stream, (const unsigned long long*)srcd, (unsigned long long*)dst, L);
+      launch_bswap(h->stream, (const unsigned long long*)srcd, (unsigned long long*)dst, L);
       HIP_TRY(h, hipGetLastError());
       return IPLS_OK;
     case IPLS_HOST_BE: {
       if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
-      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
-                         h->stream, (const unsigned long long*)srcd, (unsigned long long*)h->d_scratch, L);
+      launch_bswap(h->stream, (const unsigned long long*)srcd, (unsigned long long*)h->d_scratch, L);
       HIP_TRY(h, hipGetLastError());
       return d2h(h, dst, h->d_scratch, (size_t)L * 8);
     }
@@ -1498,8 +1499,7 @@ int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_ou
         if (int rc = d2h(h, sum_out, w, (size_t)L * 8)) return rc;
       } else if (sum_kind == IPLS_HOST_BE) {
         if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
-        hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
-                           h->stream, (const unsigned long long*)w, (unsigned long long*)h->d_scratch, L);
+        launch_bswap(h->stream, (const unsigned long long*)w, (unsigned long long*)h->d_scratch, L);
         HIP_TRY(h, hipGetLastError());
         if (int rc = d2h(h, sum_out, h->d_scratch, (size_t)L * 8)) return rc;
       } else {
@@ -1535,9 +1535,7 @@ int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind
     HIP_TRY(h, dev_use(h->device));
     if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
     if (int rc = stage_h2d(h, h->d_scratch, (const char*)src + poff, (size_t)L * 8)) return rc;
-    hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0,
-                       h->stream, (const unsigned long long*)h->d_scratch,
-                       (unsigned long long*)(h->arena + h->w_off[p]), L);
+    launch_bswap(h->stream, (const unsigned long long*)h->d_scratch, (unsigned long long*)(h->arena + h->w_off[p]), L);
     HIP_TRY(h, hipGetLastError());
     return IPLS_OK;
   }
@@ -1553,8 +1551,7 @@ int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind
     case IPLS_HOST_BE: {
       if (int rc = ensure_scratch(h, (size_t)n * 8)) return rc;
       if (int rc = stage_h2d(h, h->d_scratch, src, (size_t)n * 8)) return rc;
-      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)), dim3(kBlock), 0,
-                         h->stream, (const unsigned long long*)h->d_scratch, (unsigned long long*)w, n);
+      launch_bswap(h->stream, (const unsigned long long*)h->d_scratch, (unsigned long long*)w, n);
       HIP_TRY(h, hipGetLastError());
       return IPLS_OK;
     }
@@ -1562,8 +1559,7 @@ int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind
       HIP_TRY(h, hipMemcpyAsync(w, src, (size_t)n * 8, hipMemcpyDeviceToDevice, h->stream));
       return IPLS_OK;
     case IPLS_DEV_BE:
-      hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(n, kBlock), 4096)), dim3(kBlock), 0,
-                         h->stream, (const unsigned long long*)src, (unsigned long long*)w, n);
+      launch_bswap(h->stream, (const unsigned long long*)src, (unsigned long long*)w, n);
       HIP_TRY(h, hipGetLastError());
       return IPLS_OK;
     default:
@@ -2285,8 +2281,7 @@ int64_t dev_commit_partial(ipls_dev* h, int p, int32_t workers, uint8_t* out, in
     std::memset(out + hl, 0, (size_t)L * 8);   // +0.0 in any byte order
   } else {
     if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
-    hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(L, kBlock), 4096)), dim3(kBlock), 0, h->stream,
-                       (const unsigned long long*)(h->arena + h->agg_off[p]), (unsigned long long*)h->d_scratch, L);
+    launch_bswap(h->stream, (const unsigned long long*)(h->arena + h->agg_off[p]), (unsigned long long*)h->d_scratch, L);
     HIP_TRY(h, hipGetLastError());
     if (int rc = d2h(h, out + hl, h->d_scratch, (size_t)L * 8)) return rc;
   }
@@ -2351,8 +2346,7 @@ int64_t dev_merge_files(ipls_dev* h, const uint8_t* const* files, const int64_t*
   }
   // update_file(..., Aggregation): putDouble per element (MyIPFSClass.java:105-116)
   if (int rc = ensure_scratch(h, (size_t)n0 * 8)) return rc;
-  hipLaunchKernelGGL(k_bswap64, dim3(std::min<unsigned>(blocks_for(n0, kBlock), 4096)), dim3(kBlock), 0, h->stream,
-                     (const unsigned long long*)h->d_merge, (unsigned long long*)h->d_scratch, n0);
+  launch_bswap(h->stream, (const unsigned long long*)h->d_merge, (unsigned long long*)h->d_scratch, n0);
   HIP_TRY(h, hipGetLastError());
   if (int rc = d2h(h, out, h->d_scratch, (size_t)n0 * 8)) return rc;
   return 8 * n0;

@@ -750,11 +750,30 @@ __global__ __launch_bounds__(kBlock) void k_split(const unsigned long long* __re
 }
 
 // Layout conversion between native and big-endian doubles (pack / unpack).
+//   VEC: the 16-B tile shape of the elementwise kernels (kEwTile elements per
+//   block, see k_fold_n) when both operands are 16-B aligned
+template <bool VEC = false>
 __global__ __launch_bounds__(kBlock) void k_bswap64(const unsigned long long* __restrict__ in,
                                                     unsigned long long* __restrict__ out, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock)
-    out[i] = __builtin_bswap64(in[i]);
+  if constexpr (VEC) {
+    const int64_t base = (int64_t)blockIdx.x * kEwTile;
+    if (base + kEwTile <= n) {
+      u2 v[kEwV];
+#pragma unroll
+      for (int k = 0; k < kEwV; ++k) v[k] = __builtin_nontemporal_load((gcu2)(in + base + 2 * ((int64_t)k * kBlock + threadIdx.x)));
+#pragma unroll
+      for (int k = 0; k < kEwV; ++k) {
+        const unsigned long long a = v[k].x, b = v[k].y;
+        __builtin_nontemporal_store(u2{__builtin_bswap64(a), __builtin_bswap64(b)},
+                                    (gu2)(out + base + 2 * ((int64_t)k * kBlock + threadIdx.x)));
+      }
+      return;
+    }
+    for (int64_t i = base + threadIdx.x; i < n; i += kBlock) out[i] = __builtin_bswap64(in[i]);
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+      out[i] = __builtin_bswap64(in[i]);
+  }
 }
 
 // Strided model load (InitializeWeights(List<Double>), IPLS.java:1880-1901):

@@ -861,6 +861,16 @@ def test_elementwise_kernels_both_shapes(ipls, O, L):
         O.collect_replicas(rep, store, [0])
         agg.Collect_Replicas()
         assert_bits_equal(agg.read(0, ipls.TGT_REP), rep[0], f"replica fold L={L} shift={shift}")
+        # k_bswap64: REP read out as big-endian bytes into a device buffer, and
+        # Weights set from big-endian device bytes (cache_partition)
+        from ipls import _native as N
+        out = torch.zeros(8 * (L + 2), dtype=torch.uint8, device="cuda")
+        agg._chk(agg._lib.ipls_agg_read(agg._h, 0, ipls.TGT_REP, int(out.data_ptr()) + 8 * shift, L, N.DEV_BE))
+        torch.cuda.synchronize()
+        assert bytes(out[8 * shift:8 * (shift + L)].cpu().numpy()) == O.be_encode(rep[0]), f"BE read L={L}"
+        w3 = O.synth_bucket(L, 4, 40 + shift)
+        agg.cache_partition(0, dev_at(w3, shift, be=True))
+        assert_bits_equal(agg.read(0, ipls.TGT_WEIGHTS), w3, f"BE weights L={L} shift={shift}")
         agg.close()
         # k_encode_secure between device buffers, every byte-order pairing
         x = O.synth_bucket(L, 5, shift) * 3000.0

@@ -179,6 +179,11 @@ int main(int argc, char** argv) {
                   [=]() { hipLaunchKernelGGL(k_scale<true>, dim3(tiles(kEwV)), dim3(kBlock), 0, 0, (double*)d, (const double*)s, N, c); }, nullptr, {}});
   vars.push_back({"scale tiles V=4", 16.0 * N, none,
                   [=]() { hipLaunchKernelGGL((k_scale_v<4>), dim3(tiles(4)), dim3(kBlock), 0, 0, (double*)d, (const double*)s, N, c); }, nullptr, {}});
+  // bswap (the codec copy: target reads/writes in big-endian, GetParameters into Gradient_Buff)
+  vars.push_back({"bswap grid-stride 8 B (unaligned)", 16.0 * N, none,
+                  [=]() { hipLaunchKernelGGL(k_bswap64<false>, dim3(gf), dim3(kBlock), 0, 0, s, d, N); }, nullptr, {}});
+  vars.push_back({"bswap product k_bswap64<VEC>", 16.0 * N, none,
+                  [=]() { hipLaunchKernelGGL(k_bswap64<true>, dim3(tiles(kEwV)), dim3(kBlock), 0, 0, s, d, N); }, nullptr, {}});
   // fold_n
   vars.push_back({"fold_n grid-stride 8 B (unaligned)", 24.0 * N, reset_t,
                   [=]() { hipLaunchKernelGGL((k_fold_n<false, false>), dim3(gf), dim3(kBlock), 0, 0, t, g, N); }, nullptr, {}});
@@ -196,9 +201,9 @@ int main(int argc, char** argv) {
   };
   std::vector<unsigned long long> want(N), got(N);
   bool ok = true;
-  const int groups[][2] = {{0, 5}, {5, 8}, {8, 11}};
+  const int groups[][2] = {{0, 5}, {5, 8}, {8, 10}, {10, 13}};
   for (auto& gr : groups) {
-    unsigned long long* out = (gr[0] == 5) ? d : t;
+    unsigned long long* out = (gr[0] == 5 || gr[0] == 8) ? d : t;
     result(vars[gr[0]], out, want);
     for (int i = gr[0] + 1; i < gr[1]; ++i) {
       result(vars[i], out, got);
