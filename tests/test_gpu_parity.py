@@ -865,6 +865,7 @@ def test_elementwise_kernels_both_shapes(ipls, O, L):
         # Weights set from big-endian device bytes (cache_partition)
         from ipls import _native as N
         out = torch.zeros(8 * (L + 2), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()              # torch's fill runs on its own stream, not the handle's
         agg._chk(agg._lib.ipls_agg_read(agg._h, 0, ipls.TGT_REP, int(out.data_ptr()) + 8 * shift, L, N.DEV_BE))
         torch.cuda.synchronize()
         assert bytes(out[8 * shift:8 * (shift + L)].cpu().numpy()) == O.be_encode(rep[0]), f"BE read L={L}"
@@ -880,6 +881,7 @@ def test_elementwise_kernels_both_shapes(ipls, O, L):
         src = dev_at(x, shift)
         for bo in (False, True):
             out = torch.zeros(8 * (L + 2), dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
             dst = ipls.DeviceBuffer(int(out.data_ptr()) + 8 * shift, L, big_endian=bo)
             ipls.encode_secure(src, dst)
             torch.cuda.synchronize()
