@@ -1786,8 +1786,13 @@ int dev_split(ipls_dev* h, const void* flat, int64_t n, int src_kind, int p, voi
                                      : (unsigned long long*)dst;
   if (host_out && src_kind != IPLS_HOST_F64 && src_kind != IPLS_HOST_BE)
     out = (unsigned long long*)h->d_scratch;
-  const dim3 g(blocks_for(L, kBlock));
-#define SPL(BI, BO) hipLaunchKernelGGL((k_split<BI, BO, 0>), g, dim3(kBlock), 0, h->stream, d, (int64_t)0, ncopy, L, out)
+  const bool vec = al16(d) && al16(out);
+  const dim3 g = vec ? dim3(std::max(1u, blocks_for(L, kEwTile))) : dim3(blocks_for(L, kBlock));
+#define SPL(BI, BO)                                                                                              \
+  do {                                                                                                           \
+    if (vec) hipLaunchKernelGGL((k_split<BI, BO, 0, true>), g, dim3(kBlock), 0, h->stream, d, (int64_t)0, ncopy, L, out); \
+    else hipLaunchKernelGGL((k_split<BI, BO, 0, false>), g, dim3(kBlock), 0, h->stream, d, (int64_t)0, ncopy, L, out); \
+  } while (0)
   if (be_in) { if (be_out) SPL(true, true); else SPL(true, false); }
   else { if (be_out) SPL(false, true); else SPL(false, false); }
 #undef SPL
@@ -1821,15 +1826,21 @@ int dev_update_gradient(ipls_dev* h, const void* flat, int64_t n, int src_kind, 
     const int64_t L = h->len[p];
     unsigned long long* acc = (unsigned long long*)(h->arena + h->agg_off[p]);
     const bool zero = h->agg_zero[p];
-    const dim3 g(blocks_for(L, kBlock));
-    // Logically-zero accumulator: write +0.0 + v (== fold into zeros).
-    if (zero) HIP_TRY(h, hipMemsetAsync(acc, 0, (size_t)L * 8, h->stream));
-    if (be)
-      hipLaunchKernelGGL((k_split<true, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p] - h->flat_base,
-                         nc[p], L, acc);
-    else
-      hipLaunchKernelGGL((k_split<false, false, 1>), g, dim3(kBlock), 0, h->stream, d, h->flat_off[p] - h->flat_base,
-                         nc[p], L, acc);
+    const int64_t lo = h->flat_off[p] - h->flat_base;
+    // the segment's start decides: partitions whose flat offset is odd read
+    // their values at 8 mod 16 and keep the element-per-lane shape
+    const bool vec = al16(d + lo) && al16(acc);
+    const dim3 g = vec ? dim3(std::max(1u, blocks_for(L, kEwTile))) : dim3(blocks_for(L, kBlock));
+    // Logically-zero accumulator: MODE 2 writes +0.0 + v without reading it
+    // (the bits of a fold into zeros)
+#define UPD(BI, M)                                                                                              \
+  do {                                                                                                          \
+    if (vec) hipLaunchKernelGGL((k_split<BI, false, M, true>), g, dim3(kBlock), 0, h->stream, d, lo, nc[p], L, acc); \
+    else hipLaunchKernelGGL((k_split<BI, false, M, false>), g, dim3(kBlock), 0, h->stream, d, lo, nc[p], L, acc); \
+  } while (0)
+    if (be) { if (zero) UPD(true, 2); else UPD(true, 1); }
+    else { if (zero) UPD(false, 2); else UPD(false, 1); }
+#undef UPD
     HIP_TRY(h, hipGetLastError());
     h->agg_zero[p] = 0;
   }

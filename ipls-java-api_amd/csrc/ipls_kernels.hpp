@@ -731,21 +731,65 @@ __global__ __launch_bounds__(BS) void k_divide(const DivDesc* __restrict__ parts
 //   dst[stop] = 1.0, rest 0.0.  Optional fused fold into an accumulator
 //   (UpdateGradient own-accumulate, IPLS.java:1737-1743).
 // ---------------------------------------------------------------------------
-template <bool BE_IN, bool BE_OUT, bool FOLD>
+//   MODE 0: dst = v (OrganizeGradients' split; BE_OUT packs big-endian)
+//   MODE 1: dst = dst + v (own accumulate into AGG, IPLS.java:1737-1743)
+//   MODE 2: dst = +0.0 + v (the same into a logically-zero AGG: the zeros are
+//           not read, and the bits equal a fold into a zeroed array)
+//   VEC: the elementwise tile shape (see k_fold_n) when flat + lo and dst are
+//   16-B aligned; tiles wholly inside [0, ncopy) go 16 B at a time, the tile
+//   that holds the count slot element by element.
+template <bool BE_IN, bool BE_OUT, int MODE, bool VEC = false>
 __global__ __launch_bounds__(kBlock) void k_split(const unsigned long long* __restrict__ flat,
                                                   int64_t lo, int64_t ncopy, int64_t L,
                                                   unsigned long long* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= L) return;
-  double v;
-  if (i < ncopy) v = decode1<BE_IN>(flat[lo + i]);
-  else if (i == ncopy) v = 1.0;
-  else v = 0.0;
-  if constexpr (FOLD) {
-    const double a = __builtin_bit_cast(double, dst[i]);
-    dst[i] = __builtin_bit_cast(unsigned long long, a + v);
+  static_assert(MODE == 0 || !BE_OUT, "the folds write native doubles");
+  auto one = [&](int64_t i) {
+    double v;
+    if (i < ncopy) v = decode1<BE_IN>(flat[lo + i]);
+    else if (i == ncopy) v = 1.0;
+    else v = 0.0;
+    if constexpr (MODE == 1) {
+      const double a = __builtin_bit_cast(double, dst[i]);
+      dst[i] = __builtin_bit_cast(unsigned long long, a + v);
+    } else if constexpr (MODE == 2) {
+      dst[i] = __builtin_bit_cast(unsigned long long, 0.0 + v);
+    } else {
+      dst[i] = BE_OUT ? f64_to_be(v) : __builtin_bit_cast(unsigned long long, v);
+    }
+  };
+  if constexpr (VEC) {
+    const int64_t base = (int64_t)blockIdx.x * kEwTile;
+    if (base + kEwTile <= ncopy) {
+      const unsigned long long* src = flat + lo;
+      u2 sv[kEwV], dv[kEwV];
+#pragma unroll
+      for (int k = 0; k < kEwV; ++k) {
+        const int64_t i = base + 2 * ((int64_t)k * kBlock + threadIdx.x);
+        sv[k] = __builtin_nontemporal_load((gcu2)(src + i));
+        if constexpr (MODE == 1) dv[k] = *(gcu2)(dst + i);
+      }
+#pragma unroll
+      for (int k = 0; k < kEwV; ++k) {
+        const int64_t i = base + 2 * ((int64_t)k * kBlock + threadIdx.x);
+        const d2 x = decode2<BE_IN>(sv[k]);
+        d2 o;
+        if constexpr (MODE == 1) {
+          const d2 a = __builtin_bit_cast(d2, dv[k]);
+          o = d2{a.x + x.x, a.y + x.y};
+        } else if constexpr (MODE == 2) {
+          o = d2{0.0 + x.x, 0.0 + x.y};
+        } else {
+          o = x;
+        }
+        *(gu2)(dst + i) = encode2<BE_OUT>(o);
+      }
+      return;
+    }
+    const int64_t end = base + kEwTile < L ? base + kEwTile : L;
+    for (int64_t i = base + threadIdx.x; i < end; i += kBlock) one(i);
   } else {
-    dst[i] = BE_OUT ? f64_to_be(v) : __builtin_bit_cast(unsigned long long, v);
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < L) one(i);
   }
 }
 

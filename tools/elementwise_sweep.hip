@@ -184,6 +184,17 @@ int main(int argc, char** argv) {
                   [=]() { hipLaunchKernelGGL(k_bswap64<false>, dim3(gf), dim3(kBlock), 0, 0, s, d, N); }, nullptr, {}});
   vars.push_back({"bswap product k_bswap64<VEC>", 16.0 * N, none,
                   [=]() { hipLaunchKernelGGL(k_bswap64<true>, dim3(tiles(kEwV)), dim3(kBlock), 0, 0, s, d, N); }, nullptr, {}});
+  // own accumulate (UpdateGradient: k_split MODE 1 = AGG += v, MODE 2 = +0.0 + v into a zero AGG)
+  const unsigned gl = blocks_for(N, kBlock);
+  vars.push_back({"own-acc element per lane (unaligned)", 24.0 * N, reset_t,
+                  [=]() { hipLaunchKernelGGL((k_split<false, false, 1, false>), dim3(gl), dim3(kBlock), 0, 0, g, (int64_t)0, N - 1, N, t); }, nullptr, {}});
+  vars.push_back({"own-acc product k_split<1, VEC>", 24.0 * N, reset_t,
+                  [=]() { hipLaunchKernelGGL((k_split<false, false, 1, true>), dim3(tiles(kEwV)), dim3(kBlock), 0, 0, g, (int64_t)0, N - 1, N, t); }, nullptr, {}});
+  vars.push_back({"own-acc zero AGG: memset + fold (old)", 16.0 * N, reset_t,
+                  [=]() { (void)hipMemsetAsync(t, 0, B, 0);
+                          hipLaunchKernelGGL((k_split<false, false, 1, false>), dim3(gl), dim3(kBlock), 0, 0, g, (int64_t)0, N - 1, N, t); }, nullptr, {}});
+  vars.push_back({"own-acc zero AGG: k_split<2, VEC>", 16.0 * N, reset_t,
+                  [=]() { hipLaunchKernelGGL((k_split<false, false, 2, true>), dim3(tiles(kEwV)), dim3(kBlock), 0, 0, g, (int64_t)0, N - 1, N, t); }, nullptr, {}});
   // fold_n
   vars.push_back({"fold_n grid-stride 8 B (unaligned)", 24.0 * N, reset_t,
                   [=]() { hipLaunchKernelGGL((k_fold_n<false, false>), dim3(gf), dim3(kBlock), 0, 0, t, g, N); }, nullptr, {}});
@@ -201,7 +212,7 @@ int main(int argc, char** argv) {
   };
   std::vector<unsigned long long> want(N), got(N);
   bool ok = true;
-  const int groups[][2] = {{0, 5}, {5, 8}, {8, 10}, {10, 13}};
+  const int groups[][2] = {{0, 5}, {5, 8}, {8, 10}, {10, 12}, {12, 14}, {14, 17}};
   for (auto& gr : groups) {
     unsigned long long* out = (gr[0] == 5 || gr[0] == 8) ? d : t;
     result(vars[gr[0]], out, want);
