@@ -889,6 +889,42 @@ def test_elementwise_kernels_both_shapes(ipls, O, L):
             assert got == (O.be_encode(want) if bo else want.tobytes()), f"encode_secure L={L} shift={shift} be={bo}"
 
 
+@pytest.mark.parametrize("M,P", [(20481, 4), (443610, 3), (65536, 5)])
+def test_update_gradient_both_shapes(ipls, O, M, P):
+    """IPLS.UpdateGradient's own accumulate (IPLS.java:1737-1743) through
+    k_split: partitions whose segment of the flat vector starts 16-B aligned
+    take the tile shape, the others one element per lane; a logically-zero
+    AGG is written as +0.0 + v without a memset (MODE 2), later steps fold
+    (MODE 1).  Host input and device input at a 16-B boundary and at 8 mod
+    16; big-endian device input; -0.0 values show the +0.0 start."""
+    owned = list(range(P))
+    for kind in ("host", "dev0", "dev1", "be1"):
+        agg = ipls.Aggregator(M, P)
+        acc = {p: np.zeros(agg.lengths[p]) for p in owned}
+        keep = []
+        for step in range(3):
+            g = O.synth_bucket(M, 7, 10 * step + len(kind))
+            g[::97] = -0.0
+            if kind == "host":
+                src = g
+            else:
+                shift = 0 if kind == "dev0" else 1
+                be = kind == "be1"
+                raw = np.frombuffer(O.be_encode(g) if be else g.tobytes(), dtype=np.uint8)
+                t = torch.zeros(raw.size + 16, dtype=torch.uint8, device="cuda")
+                t[8 * shift:8 * shift + raw.size] = torch.from_numpy(raw.copy()).to("cuda")
+                torch.cuda.synchronize()
+                keep.append(t)
+                src = ipls.DeviceBuffer(int(t.data_ptr()) + 8 * shift, M, big_endian=be)
+            agg.UpdateGradient(src, owned)
+            parts = O.organize_gradients(g, M, P)
+            for p in owned:
+                acc[p] = O.fold(acc[p], parts[p])
+        for p in owned:
+            assert_bits_equal(agg.read(p, ipls.TGT_AGG), acc[p], f"AGG[{p}] M={M} {kind}")
+        agg.close()
+
+
 def test_encode_secure_device(ipls, O, golden):
     x = golden["enc_in"]
     t, d = dev(x)
