@@ -1262,7 +1262,7 @@ class Watchdog:
         if self.out is not None:
             self.out[self.stage[0]] = {"error": msg}
             self.out["watchdog"] = {"expired": True, "stage": self.stage[0], "exit_code": self.EXIT_CODE}
-            print(json.dumps(self.out), flush=True)
+            emit(self.out)
         print(f"bench.py: side leg {self.stage[0]} {msg}", file=sys.stderr, flush=True)
         os._exit(self.EXIT_CODE)
 
@@ -1309,10 +1309,32 @@ def watchdog_selftest(args) -> None:
     buf = torch.zeros(1)
     dist.recv(buf, src=(rank + 1) % world)     # never sent: stuck until the watchdog fires
     if dog.cancel() and out is not None:       # not reached
-        print(json.dumps(out), flush=True)
+        emit(out)
 
 
 _T0 = time.perf_counter()
+_JSON_OUT = None
+
+
+def claim_stdout() -> None:
+    """Keep fd 1 for the one JSON line: a dup of it is kept for emit(), and
+    fd 1 itself is pointed at stderr, so anything else a rank's libraries
+    print there (gloo's "[Gloo] Rank k is connected to ..." when the side
+    group forms, runtime notices) cannot interleave with the line a driver
+    parses.  Called in every rank (and the single process), never in the
+    spawning parent, whose fd 1 the ranks inherit."""
+    global _JSON_OUT
+    if _JSON_OUT is None:
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit(obj) -> None:
+    """Write the JSON line to the real stdout."""
+    out = _JSON_OUT if _JSON_OUT is not None else sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
 
 
 def progress(msg: str) -> None:
@@ -1394,9 +1416,8 @@ def plumbing_selftest(args) -> None:
     ranks = [None] * dist.get_world_size()
     dist.all_gather_object(ranks, me)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "selftest": "plumbing",
-                          "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
-                                   "ranks": ranks}}), flush=True)
+        emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "selftest": "plumbing",
+              "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks}})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -1409,6 +1430,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    claim_stdout()
     if args.watchdog_selftest:
         return watchdog_selftest(args)
     if args.plumbing_selftest:
@@ -1701,7 +1723,7 @@ def main():
         dog.cancel()          # every leg finished: the line is printed once, here
                               # (if the dog fired first, it printed and exits)
     if out is not None:
-        print(json.dumps(out), flush=True)
+        emit(out)
     agg.close()
     if world > 1:
         dist.destroy_process_group()

@@ -24,6 +24,9 @@ def test_gpus_2_spawns_two_ranks():
     assert r.returncode == 0, r.stderr
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout          # rank 0 only
+    # and nothing else on stdout: gloo's connection log and other library
+    # prints go to stderr (bench.claim_stdout), so a driver can take stdout whole
+    assert r.stdout.strip().splitlines() == lines, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2
     assert line["rccl"]["world_size"] == 2 and line["rccl"]["backend"] == "gloo"
