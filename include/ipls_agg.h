@@ -179,6 +179,20 @@ int ipls_agg_accumulate(ipls_agg *h, int p, int target, const void *src, int64_t
 int ipls_agg_accumulate_async(ipls_agg *h, int p, int target, const void *src, int64_t n,
                               int src_kind, uint64_t *ticket);
 
+/* One range of one arrival, asynchronous: src[0..n) is folded into
+ * target[offset .. offset+n) of partition p (Agg[i] = Agg[i] + g[i],
+ * Updater.java:115-117, for those i), reading pinned host memory
+ * (ipls_host_alloc; HOST_F64 or HOST_BE) over PCIe with no staging copy.
+ * offset must be even and src 16-B aligned.  A bucket folded as any set of
+ * ranges that covers [0, L_p) once gets the bits of the whole-bucket fold:
+ * every element is added once, in call order.  This lets a caller that must
+ * first copy the bucket (the JNI shim's double[] natives) overlap that copy
+ * with the fold, chunk by chunk.  Keep src untouched until
+ * ipls_agg_wait(h, *ticket) returns.  IPLS_E_RANGE outside [0, L_p);
+ * IPLS_E_INVAL for other memory or a misaligned range. */
+int ipls_agg_accumulate_range(ipls_agg *h, int p, int target, const void *src, int64_t offset, int64_t n,
+                              int src_kind, uint64_t *ticket);
+
 /* Wait until fold `ticket` (and every fold queued before it) has finished. */
 int ipls_agg_wait(ipls_agg *h, uint64_t ticket);
 

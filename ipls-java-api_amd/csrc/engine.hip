@@ -1251,6 +1251,48 @@ int dev_accumulate_async(ipls_dev* h, int p, int target, const void* src, int64_
   return end_batch(h);
 }
 
+// One range of one arrival: src[0..n) folded into target[off..off+n) of
+// partition p, zero copy from pinned host memory, asynchronous.  The JNI
+// shim's heap-array natives copy a Java double[] into pinned staging chunk by
+// chunk and fold each chunk as soon as it has landed, so the copy of the next
+// chunk overlaps the fold of this one.  Whatever the split, every element of
+// the bucket is added exactly once, in call order: the bits of the
+// whole-bucket fold (Updater.java:115-117).
+int dev_accumulate_range(ipls_dev* h, int p, int target, const void* src, int64_t off, int64_t n, int src_kind,
+                         uint64_t* ticket) {
+  if (!h || !ticket || !src) return fail(h, IPLS_E_INVAL, "null argument");
+  IPLS_LOCK(h);   // earlier queued device buckets fold first
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (src_kind != IPLS_HOST_F64 && src_kind != IPLS_HOST_BE)
+    return fail(h, IPLS_E_INVAL, "a ranged fold reads a pinned host bucket (HOST_F64 / HOST_BE), not kind %d", src_kind);
+  const int64_t L = h->len[p];
+  if (off < 0 || n < 0 || off > L || n > L - off)
+    return fail(h, IPLS_E_RANGE, "range [%lld, %lld) outside partition %d of length %lld", (long long)off,
+                (long long)(off + n), p, (long long)L);
+  if ((off & 1) || ((uintptr_t)src & 15))
+    return fail(h, IPLS_E_INVAL, "a ranged fold needs an even start and 16-B aligned bytes");
+  void* alias = nullptr;
+  if (!is_pinned_host(src, &alias) || !alias)
+    return fail(h, IPLS_E_INVAL, "a ranged fold reads pinned host memory (ipls_host_alloc)");
+  if (n == 0) {
+    *ticket = h->ticket_done;
+    return IPLS_OK;
+  }
+  HIP_TRY(h, dev_use(h->device));
+  if (int rc = materialize(h, p, target)) return rc;   // a logically-zero target becomes real zeros first
+  unsigned long long* d0 = (unsigned long long*)(h->arena + target_off(h, p, target)) + off;
+  const auto* s0 = (const unsigned long long*)alias;
+  const unsigned blocks = std::max(1u, std::min<unsigned>(blocks_for(n >> 1, kBlock * 4), 128u));
+  const bool be = src_kind == IPLS_HOST_BE;
+  if (be) hipLaunchKernelGGL((k_fold1<true, false, kAccum>), dim3(blocks), dim3(kBlock), 0, h->stream, d0, s0, n);
+  else hipLaunchKernelGGL((k_fold1<false, false, kAccum>), dim3(blocks), dim3(kBlock), 0, h->stream, d0, s0, n);
+  HIP_TRY(h, hipGetLastError());
+  h->last_launch = launch_info(IPLS_KERNEL_FOLD1, 0, kBlock, 4, 0, 0, blocks, be, false, kstart(IPLS_START_ACCUM));
+  *ticket = h->ticket_next++;
+  return end_batch(h);
+}
+
 // GetParameters(hash, Gradient_Buff) (MyIPFSClass.java:444-455) into the
 // engine's Gradient_Buff (Updater.java:162, zeroed once, Updater.java:165-167):
 // arr[i] = getDouble() for i < data.length/8; past arr.length it throws after

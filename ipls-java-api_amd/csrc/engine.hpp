@@ -45,6 +45,8 @@ int dev_split(ipls_dev* h, const void* flat, int64_t n, int src_kind, int p, voi
 int dev_update_gradient(ipls_dev* h, const void* flat, int64_t n, int src_kind, const int32_t* owned, int n_owned);
 int dev_accumulate(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind);
 int dev_accumulate_async(ipls_dev* h, int p, int target, const void* src, int64_t n, int src_kind, uint64_t* ticket);
+int dev_accumulate_range(ipls_dev* h, int p, int target, const void* src, int64_t off, int64_t n, int src_kind,
+                         uint64_t* ticket);
 int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64_t n_bytes);
 int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** gbuf, int64_t* glen);
 int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind);

@@ -74,17 +74,22 @@ void IPLS_JNI_CALL_HOOK(const char *call);
  * Two slots per thread, each grown to the largest array that thread has
  * passed so far and kept for reuse (no allocation and no page faults per
  * call); freed when the thread ends.  Plain malloc'd memory: pinned slots
- * (ipls_host_alloc) measured no faster -- the Get/Set<T>ArrayRegion copy
- * bounds a heap-array call either way (tools/jni_heap_probe.py,
- * profiles/r04/i/: accumulate(double[]) 21.8 GB/s pinned vs 21.4 pageable,
- * finalize 15.0 vs 19.0; direct buffers 52-55 GB/s). */
-struct stage { void *p[2]; size_t cap[2]; };
+ * (ipls_host_alloc) measured no faster as whole-array copies -- the
+ * Get/Set<T>ArrayRegion copy bounds a heap-array call either way
+ * (tools/jni_heap_probe.py, profiles/r04/i/: accumulate(double[]) 21.8 GB/s
+ * pinned vs 21.4 pageable, finalize 15.0 vs 19.0; direct buffers 52-55 GB/s).
+ * What does help is overlapping that copy with the fold: large double[]
+ * arrivals go chunk by chunk through a pinned two-slot ring (ring_slot,
+ * accumulate below). */
+struct stage { void *p[2]; size_t cap[2]; void *ring[2]; };
 static pthread_key_t g_stage_key;
 static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
 static void stage_free(void *v) {
     struct stage *st = (struct stage *)v;
     free(st->p[0]);
     free(st->p[1]);
+    for (int i = 0; i < 2; ++i)
+        if (st->ring[i]) (void)LIB(ipls_host_free(st->ring[i]));
     free(st);
 }
 static void stage_init(void) { (void)pthread_key_create(&g_stage_key, stage_free); }
@@ -110,6 +115,25 @@ static void *stage(JNIEnv *env, int slot, size_t bytes) {
         st->cap[slot] = bytes;
     }
     return st->p[slot];
+}
+
+/* The pinned ring of the pipelined double[] fold (accumulate below): two
+ * slots of RING_CHUNK doubles per thread, pinned once (ipls_host_alloc) so
+ * the library folds each chunk straight from them over PCIe.  NULL with an
+ * OutOfMemoryError pending. */
+#define RING_CHUNK ((jsize)1 << 19)   /* doubles per slot: 4 MiB */
+static double *ring_slot(JNIEnv *env, int slot) {
+    if (!stage(env, slot, 1)) return NULL;   /* the per-thread record */
+    struct stage *st = (struct stage *)pthread_getspecific(g_stage_key);
+    if (!st->ring[slot]) {
+        void *q = NULL;
+        if (LIB(ipls_host_alloc((size_t)RING_CHUNK * 8, &q)) < 0 || !q) {
+            throw_msg(env, "java/lang/OutOfMemoryError", "JNI pinned staging ring");
+            return NULL;
+        }
+        st->ring[slot] = q;
+    }
+    return (double *)st->ring[slot];
 }
 
 /* A copy of the whole double[] / byte[] in staging slot `slot`. */
@@ -280,6 +304,34 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
     (void)c;
     if (!g) return;   /* Gradient == null: the Updater loops do nothing (Updater.java:115) */
     jsize n = (*env)->GetArrayLength(env, g);
+    int64_t L = 0;
+    if (n >= 2 * RING_CHUNK && LIB(ipls_agg_partition_len(H(h), p, &L)) == 0 && L >= 2 * RING_CHUNK && L <= n) {
+        /* Pipelined: chunk k is copied out of the heap (GetDoubleArrayRegion)
+         * into ring slot k % 2 while chunk k - 1 folds from the other slot
+         * (ipls_agg_accumulate_range, zero copy).  Each element of the
+         * bucket's first L is added once, in order: the whole-bucket bits. */
+        uint64_t tk[2] = {0, 0};
+        int used[2] = {0, 0}, rc = 0;
+        for (int64_t off = 0, k = 0; off < L; off += RING_CHUNK, ++k) {
+            const int s = (int)(k & 1);
+            const jsize len = (jsize)(L - off < RING_CHUNK ? L - off : RING_CHUNK);
+            if (used[s] && (rc = LIB(ipls_agg_wait(H(h), tk[s]))) < 0) break;
+            used[s] = 0;
+            double *buf = ring_slot(env, s);
+            if (!buf) { rc = 1; break; }                              /* OutOfMemoryError pending */
+            (*env)->GetDoubleArrayRegion(env, g, (jsize)off, len, buf);
+            if ((*env)->ExceptionCheck(env)) { rc = 1; break; }
+            if ((rc = LIB(ipls_agg_accumulate_range(H(h), p, tgt, buf, off, len, IPLS_HOST_F64, &tk[s]))) < 0) break;
+            used[s] = 1;
+        }
+        for (int s = 0; s < 2; ++s)   /* the folds still reading the ring, after an error too */
+            if (used[s]) {
+                const int w = LIB(ipls_agg_wait(H(h), tk[s]));
+                if (rc == 0 && w < 0) rc = w;
+            }
+        if (rc < 0) throw_for(env, rc, H(h));
+        return;
+    }
     void *src = copy_doubles(env, g, n, 0);
     if (!src) return;
     CHECK(LIB(ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_F64)), H(h));

@@ -283,6 +283,39 @@ def test_jni_round_against_oracle(jvm, gpu, O):
 
 
 @pytest.mark.gpu
+def test_jni_heap_accumulate_pipelined(jvm, gpu, O):
+    """accumulate(double[]) for partitions of >= 2 ring chunks (2 x 512 Ki
+    doubles) goes chunk by chunk through the shim's pinned ring, each chunk
+    folded by ipls_agg_accumulate_range while the next is copied: the bits
+    equal the oracle's whole-bucket folds.  An odd partition length (the last
+    chunk short and odd), a logically-zero AGG and then a live one, REP as
+    the target, and an array longer than the partition (Java reads only the
+    first L, Updater.java:115-117); a short array still raises
+    ArrayIndexOutOfBoundsException with nothing folded."""
+    M, P = 2 * 1048576 + 4099, 2                 # L = 1,050,627 / 1,050,626: 2.004 chunks each
+    h = _open(jvm, M, P)
+    lens = [O.partition_len(M, P, p) for p in range(P)]
+    assert min(lens) >= 2 * 524288 and lens[0] % 2 == 1
+    acc = {(p, t): np.zeros(lens[p]) for p in range(P) for t in (0, 1)}
+    for k in range(3):
+        for p in range(P):
+            for t in (0, 1):                         # AGG, REP
+                g = O.synth_bucket(lens[p] + (5 if k == 2 else 0), p, 10 * k + t) * (10.0 ** (k - 1))
+                g[::1009] = -0.0
+                _, exc = jvm.call("accumulate", h, p, t, jvm.doubles(g))
+                assert exc is None
+                acc[(p, t)] = O.fold(acc[(p, t)], g)
+    _, exc = jvm.call("accumulate", h, 0, 0, jvm.doubles(np.ones(lens[0] - 1)))
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    for p in range(P):   # AggregatePartition: W = AGG + REP (IPLS.java:1256), as commit_update bytes
+        out = jvm.bytes_(b"\0" * (8 * lens[p]))
+        _, exc = jvm.call("finalizePartition", h, p, out)
+        assert exc is None
+        assert jvm.data(out, np.uint8).tobytes() == O.be_encode(acc[(p, 0)] + acc[(p, 1)]), f"W[{p}]"
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
 def test_jni_exceptions_leave_state_unchanged(jvm, gpu, O):
     """A short bucket is ArrayIndexOutOfBoundsException with nothing folded
     (Updater.java:115-117 would throw mid-loop; the library rejects it first,
