@@ -925,6 +925,44 @@ def test_update_gradient_both_shapes(ipls, O, M, P):
         agg.close()
 
 
+def test_accumulate_range(ipls, O):
+    """ipls_agg_accumulate_range: one arrival folded as ranges of pinned host
+    memory gets the bits of the whole-bucket fold, into a logically-zero
+    target and a live one, native and big-endian; misuse is refused before
+    anything is folded."""
+    from ipls import _native as N
+    L = 300007
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    lib, h = agg._lib, agg._h
+    pin = ipls.PinnedBuffer(8 * L + 64)
+    view = pin.view()
+    t = ctypes.c_uint64()
+    want = np.zeros(L)
+    for k, (be, cuts) in enumerate(((False, [0, 2048, 150000, L]), (True, [0, 100000, 100002, L]), (False, [0, L]))):
+        g = O.synth_bucket(L, 1, 60 + k) * 10.0 ** k
+        raw = np.frombuffer(O.be_encode(g) if be else g.tobytes(), dtype=np.uint8)
+        view[:raw.size] = raw
+        kind = N.HOST_BE if be else N.HOST_F64
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            assert lib.ipls_agg_accumulate_range(h, 1, ipls.TGT_AGG, pin.ptr + 8 * a, a, b - a, kind, ctypes.byref(t)) == 0
+        assert lib.ipls_agg_wait(h, t.value) == 0
+        want = O.fold(want, g)
+        assert_bits_equal(agg.read(1, ipls.TGT_AGG), want, f"ranges {cuts}")
+    host = np.zeros(L + 2)
+    bad = [(pin.ptr + 8, 1, 10, N.IPLS_E_INVAL),                 # odd start
+           (pin.ptr + 8, 0, 10, N.IPLS_E_INVAL),                 # bytes at 8 mod 16
+           (host.ctypes.data, 0, 10, N.IPLS_E_INVAL),            # not pinned memory
+           (pin.ptr, L - 2, 4, N.IPLS_E_RANGE),                  # past the partition
+           (pin.ptr, -2, 4, N.IPLS_E_RANGE)]
+    for ptr, off, n, code in bad:
+        assert lib.ipls_agg_accumulate_range(h, 1, ipls.TGT_AGG, ptr, off, n, N.HOST_F64, ctypes.byref(t)) == code
+    assert lib.ipls_agg_accumulate_range(h, 1, ipls.TGT_AGG, pin.ptr, 0, 4, N.DEV_F64, ctypes.byref(t)) == N.IPLS_E_INVAL
+    assert_bits_equal(agg.read(1, ipls.TGT_AGG), want, "refused ranges folded nothing")
+    assert_bits_equal(agg.read(0, ipls.TGT_AGG), np.zeros(L), "partition 0 untouched")
+    agg.close()
+    pin.close()
+
+
 def test_encode_secure_device(ipls, O, golden):
     x = golden["enc_in"]
     t, d = dev(x)
