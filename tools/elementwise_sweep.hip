@@ -10,6 +10,7 @@
 //                             Download_Scheduler.java:254-260) 24 B / element
 // "product" rows: the shipped kernels' VEC form; "grid-stride": their
 // unaligned fallback (round 3's only form).
+// Timing: REPS rounds, the variant order rotated by one every round.
 // Usage: elementwise_sweep N REPS     (default 4194304 = one config-C partition;
 // at that size the operands fit the 256 MB Infinity Cache -- 67108864 is HBM)
 #include <hip/hip_runtime.h>
@@ -195,6 +196,22 @@ int main(int argc, char** argv) {
                           hipLaunchKernelGGL((k_split<false, false, 1, false>), dim3(gl), dim3(kBlock), 0, 0, g, (int64_t)0, N - 1, N, t); }, nullptr, {}});
   vars.push_back({"own-acc zero AGG: k_split<2, VEC>", 16.0 * N, reset_t,
                   [=]() { hipLaunchKernelGGL((k_split<false, false, 2, true>), dim3(tiles(kEwV)), dim3(kBlock), 0, 0, g, (int64_t)0, N - 1, N, t); }, nullptr, {}});
+  // AggregatePartition with REP logically zero: W = AGG + 0.0 (k_finalize<REP_ZERO>, 16 B / element,
+  // the shipped kFinV = 8, and 4) against k_scale's tile (the same bytes) -- one arena, offsets 0 / N
+  double* arena = nullptr;
+  CK(hipMalloc(&arena, 2 * B + 256));
+  CK(hipMemcpy(arena, s, B, hipMemcpyDeviceToDevice));
+  FinDesc fd{N, 0, 0, N};
+  FinDesc* d_fd;
+  CK(hipMalloc(&d_fd, sizeof fd));
+  CK(hipMemcpy(d_fd, &fd, sizeof fd, hipMemcpyHostToDevice));
+  auto fin_tpp = [&](int V) { return (int)((N + kBlock * 2 * V - 1) / (kBlock * 2 * V)); };
+  vars.push_back({"finalize REP_ZERO V=8 (shipped)", 16.0 * N, none,
+                  [=]() { hipLaunchKernelGGL((k_finalize<true, false, kBlock, 8>), dim3(fin_tpp(8)), dim3(kBlock), 0, 0, d_fd, arena, fin_tpp(8)); }, nullptr, {}});
+  vars.push_back({"finalize REP_ZERO V=4", 16.0 * N, none,
+                  [=]() { hipLaunchKernelGGL((k_finalize<true, false, kBlock, 4>), dim3(fin_tpp(4)), dim3(kBlock), 0, 0, d_fd, arena, fin_tpp(4)); }, nullptr, {}});
+  vars.push_back({"scale tile on the same arena", 16.0 * N, none,
+                  [=]() { hipLaunchKernelGGL(k_scale<true>, dim3(tiles(kEwV)), dim3(kBlock), 0, 0, arena + N, (const double*)arena, N, 1.0); }, nullptr, {}});
   // fold_n
   vars.push_back({"fold_n grid-stride 8 B (unaligned)", 24.0 * N, reset_t,
                   [=]() { hipLaunchKernelGGL((k_fold_n<false, false>), dim3(gf), dim3(kBlock), 0, 0, t, g, N); }, nullptr, {}});
@@ -212,9 +229,9 @@ int main(int argc, char** argv) {
   };
   std::vector<unsigned long long> want(N), got(N);
   bool ok = true;
-  const int groups[][2] = {{0, 5}, {5, 8}, {8, 10}, {10, 12}, {12, 14}, {14, 17}};
+  const int groups[][2] = {{0, 5}, {5, 8}, {8, 10}, {10, 12}, {12, 14}, {14, 17}, {17, 20}};
   for (auto& gr : groups) {
-    unsigned long long* out = (gr[0] == 5 || gr[0] == 8) ? d : t;
+    unsigned long long* out = (gr[0] == 5 || gr[0] == 8) ? d : gr[0] == 14 ? (unsigned long long*)(arena + N) : t;
     result(vars[gr[0]], out, want);
     for (int i = gr[0] + 1; i < gr[1]; ++i) {
       result(vars[i], out, got);
@@ -227,8 +244,12 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  // the order rotates every rep (variant i runs after a different neighbour
+  // each time): a kernel that directly follows one writing the same output
+  // can read ~8 points fast (caches), which a fixed order would credit to it
   for (int r = 0; r < REPS; ++r)
-    for (auto& v : vars) {
+    for (size_t j = 0; j < vars.size(); ++j) {
+      Var& v = vars[(j + (size_t)r) % vars.size()];
       v.reset();
       CK(hipEventRecord(e0, 0));
       v.run();
