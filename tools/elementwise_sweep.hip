@@ -10,7 +10,8 @@
 //                             Download_Scheduler.java:254-260) 24 B / element
 // "product" rows: the shipped kernels' VEC form; "grid-stride": their
 // unaligned fallback (round 3's only form).
-// Timing: REPS rounds, the variant order rotated by one every round.
+// Timing: REPS rounds, the variant order rotated by one every round, and
+// every timed launch from cold caches (a 1 GiB memset before it).
 // Usage: elementwise_sweep N REPS     (default 4194304 = one config-C partition;
 // at that size the operands fit the 256 MB Infinity Cache -- 67108864 is HBM)
 #include <hip/hip_runtime.h>
@@ -244,13 +245,19 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  // the order rotates every rep (variant i runs after a different neighbour
-  // each time): a kernel that directly follows one writing the same output
-  // can read ~8 points fast (caches), which a fixed order would credit to it
+  // Cold caches for every timed run: 1 GiB of memset (untimed) pushes the
+  // operands out of the L2s and the 256 MB Infinity Cache first.  Without it
+  // a kernel that follows one that read the same input with plain (cache-
+  // allocating) loads finds the input's tail in the Infinity Cache and reads
+  // up to ~8 points fast -- an artefact of the order, not of the kernel.
+  void* flush_buf = nullptr;
+  const size_t flush_bytes = (size_t)1 << 30;
+  CK(hipMalloc(&flush_buf, flush_bytes));
   for (int r = 0; r < REPS; ++r)
     for (size_t j = 0; j < vars.size(); ++j) {
       Var& v = vars[(j + (size_t)r) % vars.size()];
       v.reset();
+      CK(hipMemsetAsync(flush_buf, r & 0xFF, flush_bytes, 0));
       CK(hipEventRecord(e0, 0));
       v.run();
       CK(hipEventRecord(e1, 0));
