@@ -434,10 +434,10 @@ __global__ __launch_bounds__(BS) void k_round(const unsigned long long* const* _
 // kEwV 16-B vectors, loads first, then the arithmetic and stores; the one
 // partial tile goes element by element.  Otherwise (a bucket at an 8 mod 16
 // address, e.g. a payload inside a Java-serialised file) the 8-B grid-stride
-// loop.  Same per-element expressions, so the same bits either way.  At HBM
-// scale the tiles take k_blend from 60 to 80 %, k_scale from 63 to 87 % and
-// k_fold_n from 63 to 80 % of 8 TB/s (tools/elementwise_sweep.hip,
-// profiles/r04/v/).
+// loop.  Same per-element expressions, so the same bits either way.  From
+// cold caches at 64 Mi elements the tiles take k_blend from 56 to 75 %,
+// k_scale from 62 to 79 % and k_fold_n from 59 to 75 % of 8 TB/s
+// (tools/elementwise_sweep.hip, profiles/r04/zl/).
 constexpr int kEwV = 4;
 constexpr int64_t kEwTile = (int64_t)kBlock * 2 * kEwV;
 
