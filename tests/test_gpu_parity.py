@@ -925,14 +925,16 @@ def test_update_gradient_both_shapes(ipls, O, M, P):
         agg.close()
 
 
-def test_accumulate_range(ipls, O):
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_accumulate_range(ipls, O, devices):
     """ipls_agg_accumulate_range: one arrival folded as ranges of pinned host
     memory gets the bits of the whole-bucket fold, into a logically-zero
     target and a live one, native and big-endian; misuse is refused before
-    anything is folded."""
+    anything is folded.  devices=[0, 0]: partition 1 lives on the second
+    shard (the front's ticket bookkeeping)."""
     from ipls import _native as N
     L = 300007
-    agg = ipls.Aggregator(n_partitions=2, bucket_len=L)
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L, devices=devices)
     lib, h = agg._lib, agg._h
     pin = ipls.PinnedBuffer(8 * L + 64)
     view = pin.view()
