@@ -1862,7 +1862,22 @@ int dev_update_gradient(ipls_dev* h, const void* flat, int64_t n, int src_kind, 
   bool be;
   // only this engine's segment of the gradient vector (flat_base on)
   const int64_t seg = std::max<int64_t>(0, std::min(n, h->flat_total) - h->flat_base);
-  if (int rc = flat_to_device(h, (const char*)flat + 8 * h->flat_base, seg, src_kind, &d, &be)) return rc;
+  if (src_kind == IPLS_HOST_F64 || src_kind == IPLS_HOST_BE) {
+    // from host memory only the owned partitions' values cross PCIe: the
+    // others are split by OrganizeGradients too, but never accumulated
+    // (IPLS.java:1737-1743), so their bytes are never read here
+    if (int rc = ensure_scratch(h, (size_t)std::max<int64_t>(seg, 1) * 8)) return rc;
+    const char* base = (const char*)flat + 8 * h->flat_base;
+    for (int i = 0; i < n_owned; ++i) {
+      const int64_t lo = h->flat_off[owned[i]] - h->flat_base;
+      if (nc[owned[i]] > 0)
+        if (int rc = stage_h2d(h, (char*)h->d_scratch + 8 * lo, base + 8 * lo, (size_t)nc[owned[i]] * 8)) return rc;
+    }
+    d = (const unsigned long long*)h->d_scratch;
+    be = src_kind == IPLS_HOST_BE;
+  } else if (int rc = flat_to_device(h, (const char*)flat + 8 * h->flat_base, seg, src_kind, &d, &be)) {
+    return rc;
+  }
   for (int i = 0; i < n_owned; ++i) {
     const int p = owned[i];
     const int64_t L = h->len[p];
