@@ -290,10 +290,26 @@ JNIEXPORT void JNICALL Java_NativeAggregator_updateGradient(JNIEnv *env, jclass 
     if (!flat) return;   /* Gradients == null: no-op (IPLS.java:1738) */
     if (!owned) { throw_iae(env, "null auth list"); return; }
     jsize n = (*env)->GetArrayLength(env, flat), no = (*env)->GetArrayLength(env, owned);
-    void *src = copy_doubles(env, flat, n, 0);
+    double *src = (double *)stage(env, 0, (size_t)n * 8);
     if (!src) return;
     jint *own = (*env)->GetIntArrayElements(env, owned, NULL);
     if (!own) return;   /* OutOfMemoryError pending */
+    /* Only the owned partitions' values leave the heap: ipls_agg_update_gradient
+     * checks the length against every partition (OrganizeGradients) but reads
+     * only the owned partitions' slices [off, off + L - 1) of the vector
+     * (engine.hip dev_update_gradient), so the rest of the staging copy would
+     * never be looked at.  An owned index the library rejects copies nothing. */
+    for (jsize i = 0; i < no; ++i) {
+        int64_t off = 0, L = 0;
+        if (LIB(ipls_agg_partition_offset(H(h), own[i], &off)) < 0 || LIB(ipls_agg_partition_len(H(h), own[i], &L)) < 0)
+            continue;
+        const int64_t hi = off + (L - 1) < (int64_t)n ? off + (L - 1) : (int64_t)n;
+        if (hi > off) (*env)->GetDoubleArrayRegion(env, flat, (jsize)off, (jsize)(hi - off), src + off);
+        if ((*env)->ExceptionCheck(env)) {
+            (*env)->ReleaseIntArrayElements(env, owned, own, JNI_ABORT);
+            return;
+        }
+    }
     int rc = LIB(ipls_agg_update_gradient(H(h), src, n, IPLS_HOST_F64, (const int32_t *)own, no));
     (*env)->ReleaseIntArrayElements(env, owned, own, JNI_ABORT);
     CHECK(rc, H(h));

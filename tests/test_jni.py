@@ -316,6 +316,35 @@ def test_jni_heap_accumulate_pipelined(jvm, gpu, O):
 
 
 @pytest.mark.gpu
+def test_jni_update_gradient_owned_subset(jvm, gpu, O):
+    """updateGradient(double[], owned) copies only the owned partitions'
+    slices out of the heap (the library reads nothing else): owned {1, 3} of
+    4 folds exactly those partitions' values, twice, and leaves 0 and 2 at
+    zero; a vector one value too long is still ArrayIndexOutOfBoundsException
+    for the whole call (OrganizeGradients checks every partition)."""
+    M, P = 40009, 4
+    h = _open(jvm, M, P)
+    flats = [O.synth_bucket(M, 9, k) for k in range(2)]
+    for g in flats:
+        _, exc = jvm.call("updateGradient", h, jvm.doubles(g), jvm.ints([1, 3]))
+        assert exc is None
+    _, exc = jvm.call("updateGradient", h, jvm.doubles(np.ones(M + 1)), jvm.ints([1, 3]))
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    parts = [O.organize_gradients(g, M, P) for g in flats]
+    for p in range(P):
+        L = O.partition_len(M, P, p)
+        want = np.zeros(L)
+        if p in (1, 3):
+            for pt in parts:
+                want = O.fold(want, pt[p])
+        out = jvm.bytes_(b"\0" * (8 * L))
+        _, exc = jvm.call("finalizePartition", h, p, out)
+        assert exc is None
+        assert jvm.data(out, np.uint8).tobytes() == O.be_encode(want + 0.0), f"W[{p}]"
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
 def test_jni_exceptions_leave_state_unchanged(jvm, gpu, O):
     """A short bucket is ArrayIndexOutOfBoundsException with nothing folded
     (Updater.java:115-117 would throw mid-loop; the library rejects it first,
