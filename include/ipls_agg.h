@@ -193,6 +193,18 @@ int ipls_agg_accumulate_async(ipls_agg *h, int p, int target, const void *src, i
 int ipls_agg_accumulate_range(ipls_agg *h, int p, int target, const void *src, int64_t offset, int64_t n,
                               int src_kind, uint64_t *ticket);
 
+/* The reverse of a ranged fold, asynchronous: target[offset .. offset+n) of
+ * partition p is copied into pinned host memory dst (ipls_host_alloc), as
+ * doubles (HOST_F64) or as big-endian bytes (HOST_BE: putDouble order, what
+ * update_file writes, MyIPFSClass.java:105-116).  dst is complete when
+ * ipls_agg_wait(h, *ticket) returns.  With ipls_agg_finalize(h, p, NULL, ...)
+ * first, reading IPLS_TGT_WEIGHTS in ranges gives the commit_update bytes
+ * chunk by chunk (the JNI shim's finalizePartition(byte[]) copies each chunk
+ * into the Java array while the next is in flight).  IPLS_E_RANGE outside
+ * [0, L_p); IPLS_E_INVAL for other memory. */
+int ipls_agg_read_range(ipls_agg *h, int p, int target, void *dst, int64_t offset, int64_t n, int dst_kind,
+                        uint64_t *ticket);
+
 /* Wait until fold `ticket` (and every fold queued before it) has finished. */
 int ipls_agg_wait(ipls_agg *h, uint64_t ticket);
 

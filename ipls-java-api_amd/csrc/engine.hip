@@ -1293,6 +1293,44 @@ int dev_accumulate_range(ipls_dev* h, int p, int target, const void* src, int64_
   return end_batch(h);
 }
 
+// The reverse: target[off..off+n) of partition p into pinned host memory,
+// native or big-endian (putDouble order, as update_file writes it,
+// MyIPFSClass.java:105-116), asynchronous.  The JNI shim's byte[] outputs
+// copy chunk k into the Java array while chunk k+1 is still in flight.
+int dev_read_range(ipls_dev* h, int p, int target, void* dst, int64_t off, int64_t n, int dst_kind, uint64_t* ticket) {
+  if (!h || !ticket || !dst) return fail(h, IPLS_E_INVAL, "null argument");
+  IPLS_LOCK(h);
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (dst_kind != IPLS_HOST_F64 && dst_kind != IPLS_HOST_BE)
+    return fail(h, IPLS_E_INVAL, "a ranged read writes pinned host memory (HOST_F64 / HOST_BE), not kind %d", dst_kind);
+  const int64_t L = h->len[p];
+  if (off < 0 || n < 0 || off > L || n > L - off)
+    return fail(h, IPLS_E_RANGE, "range [%lld, %lld) outside partition %d of length %lld", (long long)off,
+                (long long)(off + n), p, (long long)L);
+  void* alias = nullptr;
+  if (!is_pinned_host(dst, &alias) || !alias)
+    return fail(h, IPLS_E_INVAL, "a ranged read writes pinned host memory (ipls_host_alloc)");
+  if (n == 0) {
+    *ticket = h->ticket_done;
+    return IPLS_OK;
+  }
+  HIP_TRY(h, dev_use(h->device));
+  if (int rc = materialize(h, p, target)) return rc;
+  const unsigned long long* src = (const unsigned long long*)(h->arena + target_off(h, p, target)) + off;
+  if (dst_kind == IPLS_HOST_BE) {
+    // byte-swapped into the same offsets of the device scratch, then copied
+    if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+    unsigned long long* sc = (unsigned long long*)h->d_scratch + off;
+    launch_bswap(h->stream, src, sc, n);
+    HIP_TRY(h, hipGetLastError());
+    src = sc;
+  }
+  HIP_TRY(h, hipMemcpyAsync(dst, src, (size_t)n * 8, hipMemcpyDeviceToHost, h->stream));
+  *ticket = h->ticket_next++;
+  return end_batch(h);
+}
+
 // GetParameters(hash, Gradient_Buff) (MyIPFSClass.java:444-455) into the
 // engine's Gradient_Buff (Updater.java:162, zeroed once, Updater.java:165-167):
 // arr[i] = getDouble() for i < data.length/8; past arr.length it throws after

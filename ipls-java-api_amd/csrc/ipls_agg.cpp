@@ -625,6 +625,32 @@ int ipls_agg_accumulate_range(ipls_agg* H, int p, int target, const void* src, i
   return IPLS_OK;
 }
 
+int ipls_agg_read_range(ipls_agg* H, int p, int target, void* dst, int64_t offset, int64_t n, int dst_kind,
+                        uint64_t* ticket) {
+  KeepDevice keep_device;
+  if (!H || !ticket) return ferr(H, IPLS_E_INVAL, "null argument");
+  if (H->S() == 1) return fwd(H, 0, dev_read_range(H->sh[0], p, target, dst, offset, n, dst_kind, ticket));
+  if (!part_ok(H, p)) return range_err(H, p);
+  int q;
+  const int s = route(H, p, &q);
+  uint64_t lt = 0;
+  if (int rc = fwd(H, s, dev_read_range(H->sh[s], q, target, dst, offset, n, dst_kind, &lt))) return rc;
+  std::vector<std::pair<int, uint64_t>> drain;
+  {
+    std::lock_guard<std::mutex> lk(H->mu);
+    *ticket = H->ticket_next++;
+    auto& dq = H->tickets[s];
+    dq.emplace_back(*ticket, lt);
+    if (dq.size() > 65536) {   // bound the bookkeeping: retire the oldest half
+      drain.emplace_back(s, dq[dq.size() / 2].second);
+      dq.erase(dq.begin(), dq.begin() + dq.size() / 2 + 1);
+    }
+  }
+  for (auto& d : drain)
+    if (int rc = fwd(H, d.first, dev_wait(H->sh[d.first], d.second))) return rc;
+  return IPLS_OK;
+}
+
 int ipls_agg_wait(ipls_agg* H, uint64_t ticket) {
   KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");

@@ -462,6 +462,47 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jcla
     }
     int64_t L = 0;
     if (sum && LIB(ipls_agg_partition_len(H(h), p, &L)) < 0) { throw_for(env, IPLS_E_RANGE, H(h)); return; }
+    if (sum && L >= 2 * RING_CHUNK) {
+        /* Pipelined: AggregatePartition on the device, then the commit_update
+         * bytes of W in ring-sized chunks (ipls_agg_read_range, big-endian,
+         * into the pinned ring): chunk k is copied into the byte[] while
+         * chunk k + 1 is still coming back. */
+        int rc = LIB(ipls_agg_finalize(H(h), p, NULL, IPLS_HOST_BE, NULL));
+        if (rc < 0) { throw_for(env, rc, H(h)); return; }
+        const int64_t K = (L + RING_CHUNK - 1) / RING_CHUNK;
+        uint64_t tk[2] = {0, 0};
+        int live[2] = {0, 0};
+        for (int64_t j = 0; j < K && j < 1 && rc >= 0; ++j) {   /* chunk 0 */
+            double *buf = ring_slot(env, 0);
+            if (!buf) { rc = 1; break; }
+            rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, buf, 0, L < RING_CHUNK ? L : RING_CHUNK,
+                                         IPLS_HOST_BE, &tk[0]));
+            live[0] = rc >= 0;
+        }
+        for (int64_t k = 0; k < K && rc >= 0; ++k) {
+            const int s = (int)(k & 1), t = 1 - s;
+            if (k + 1 < K) {   /* chunk k + 1 into the other slot (its chunk k - 1 is already out) */
+                const int64_t off = (k + 1) * RING_CHUNK, len = L - off < RING_CHUNK ? L - off : RING_CHUNK;
+                double *buf = ring_slot(env, t);
+                if (!buf) { rc = 1; break; }
+                if ((rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, buf, off, len, IPLS_HOST_BE, &tk[t]))) < 0)
+                    break;
+                live[t] = 1;
+            }
+            if ((rc = LIB(ipls_agg_wait(H(h), tk[s]))) < 0) break;
+            live[s] = 0;
+            const int64_t off = k * RING_CHUNK, len = L - off < RING_CHUNK ? L - off : RING_CHUNK;
+            (*env)->SetByteArrayRegion(env, sum, (jsize)(8 * off), (jsize)(8 * len), (const jbyte *)ring_slot(env, s));
+            if ((*env)->ExceptionCheck(env)) { rc = 1; break; }
+        }
+        for (int s = 0; s < 2; ++s)   /* reads still writing the ring, after an error too */
+            if (live[s]) {
+                const int w = LIB(ipls_agg_wait(H(h), tk[s]));
+                if (rc == 0 && w < 0) rc = w;
+            }
+        if (rc < 0) throw_for(env, rc, H(h));
+        return;
+    }
     jbyte *dst = sum ? (jbyte *)stage(env, 0, (size_t)L * 8) : NULL;
     if (sum && !dst) return;
     int rc = LIB(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL));

@@ -965,6 +965,39 @@ def test_accumulate_range(ipls, O, devices):
     pin.close()
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_read_range(ipls, O, devices):
+    """ipls_agg_read_range: a target read in ranges into pinned memory, native
+    and big-endian, equals the whole read; after ipls_agg_finalize with no
+    output, Weights in big-endian ranges are the commit_update bytes; misuse
+    is refused."""
+    from ipls import _native as N
+    L = 200003
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    a, r = O.synth_bucket(L, 1, 1), O.synth_bucket(L, 1, 2) * 3.0
+    agg.Update(a, 1)
+    agg.Update(r, 1, from_clients=False)
+    pin = ipls.PinnedBuffer(8 * L)
+    t = ctypes.c_uint64()
+    for kind, want in ((N.HOST_F64, a.tobytes()), (N.HOST_BE, O.be_encode(a))):
+        for lo, hi in ((0, 65536), (65536, 65538), (65538, L)):
+            assert lib.ipls_agg_read_range(h, 1, ipls.TGT_AGG, pin.ptr + 8 * lo, lo, hi - lo, kind, ctypes.byref(t)) == 0
+        assert lib.ipls_agg_wait(h, t.value) == 0
+        assert pin.view()[:8 * L].tobytes() == want, f"kind {kind}"
+    assert lib.ipls_agg_finalize(h, 1, None, N.HOST_BE, None) == 0
+    for lo, hi in ((0, 100000), (100000, L)):
+        assert lib.ipls_agg_read_range(h, 1, ipls.TGT_WEIGHTS, pin.ptr + 8 * lo, lo, hi - lo, N.HOST_BE, ctypes.byref(t)) == 0
+    assert lib.ipls_agg_wait(h, t.value) == 0
+    assert pin.view()[:8 * L].tobytes() == O.be_encode(a + r), "commit_update bytes"
+    host = np.zeros(8)
+    assert lib.ipls_agg_read_range(h, 1, ipls.TGT_AGG, host.ctypes.data, 0, 4, N.HOST_F64, ctypes.byref(t)) == N.IPLS_E_INVAL
+    assert lib.ipls_agg_read_range(h, 1, ipls.TGT_AGG, pin.ptr, L - 1, 2, N.HOST_F64, ctypes.byref(t)) == N.IPLS_E_RANGE
+    assert lib.ipls_agg_read_range(h, 1, ipls.TGT_AGG, pin.ptr, 0, 2, N.DEV_F64, ctypes.byref(t)) == N.IPLS_E_INVAL
+    agg.close()
+    pin.close()
+
+
 def test_encode_secure_device(ipls, O, golden):
     x = golden["enc_in"]
     t, d = dev(x)
