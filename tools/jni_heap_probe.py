@@ -1,10 +1,13 @@
 """Dev probe: what a heap-array native costs against the direct-buffer one,
 through the JNI shim and the fake JVM (tests/jni/fake_jvm.c) on the GPU box.
 One partition of L doubles (one bucket per call, as the Updater folds):
-  accumulate(double[])         -- Get<T>ArrayRegion into the shim's per-thread
-                                  staging (pinned), then the library's fold
+  accumulate(double[])         -- GetDoubleArrayRegion chunk by chunk into the
+                                  shim's pinned two-slot ring, each chunk folded
+                                  (ipls_agg_accumulate_range) while the next is copied
   accumulateDirect(ByteBuffer) -- a hostAlloc direct buffer, zero copy
-  finalizePartition(byte[])    -- the BE sum into staging, Set<T>ArrayRegion
+  finalizePartition(byte[])    -- AggregatePartition, then the BE sum back in
+                                  ring chunks (ipls_agg_read_range), each copied
+                                  into the byte[] while the next arrives
   finalizePartitionDirect      -- the BE sum straight into a direct buffer
 GB/s = bytes of the Java-side array / wall time per call (median of reps).
 Usage: jni_heap_probe.py [L] [reps]"""
