@@ -136,6 +136,9 @@ int ipls_agg_partition_len(const ipls_agg *h, int p, int64_t *len);
 
 /* Offset of partition p's first value in the flat model (p * chunk). */
 int ipls_agg_partition_offset(const ipls_agg *h, int p, int64_t *off);
+/* Values of the flat model: model_size (sum of L_p - 1), what GetPartitions
+ * writes and OrganizeGradients reads. */
+int ipls_agg_flat_size(const ipls_agg *h, int64_t *n);
 
 /* InitializeWeights(List<Double> Model), IPLS.java:1880-1901: Weights and
  * Weight_Address get the model values with count slot 0.0; AGG, REP = 0.

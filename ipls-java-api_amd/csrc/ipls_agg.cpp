@@ -470,6 +470,13 @@ int ipls_agg_partition_offset(const ipls_agg* h, int p, int64_t* off) {
   return IPLS_OK;
 }
 
+int ipls_agg_flat_size(const ipls_agg* h, int64_t* n) {
+  ipls_agg* H = const_cast<ipls_agg*>(h);
+  if (!H || !n) return ferr(H, IPLS_E_INVAL, "null argument");
+  *n = H->flat_total;
+  return IPLS_OK;
+}
+
 int ipls_agg_partition_device(ipls_agg* H, int p, int32_t* device, void** stream) {
   KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");

@@ -98,6 +98,7 @@ SIGNATURES = {
     "ipls_agg_accumulate_async": (_i, [_vp, _i, _i, _vp, _i64, _i, _P(_u64)]),
     "ipls_agg_accumulate_range": (_i, [_vp, _i, _i, _vp, _i64, _i64, _i, _P(_u64)]),
     "ipls_agg_read_range": (_i, [_vp, _i, _i, _vp, _i64, _i64, _i, _P(_u64)]),
+    "ipls_agg_flat_size": (_i, [_vp, _P(_i64)]),
     "ipls_agg_wait": (_i, [_vp, _u64]),
     "ipls_agg_set_coalesce": (_i, [_vp, _i]),
     "ipls_agg_flush": (_i, [_vp]),

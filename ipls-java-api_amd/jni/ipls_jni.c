@@ -542,11 +542,15 @@ JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c
     (void)c;
     if (!out) { throw_iae(env, "null output"); return; }
     jsize n = (*env)->GetArrayLength(env, out);   /* the library checks n against the model size */
-    /* copied in first: elements past the model keep their values when copied back */
-    double *dst = (double *)copy_doubles(env, out, n, 0);
+    /* the library writes the model's first M values; only those go back into
+     * the array (elements past the model keep theirs), so nothing is copied in */
+    int64_t M = 0;
+    int rc = LIB(ipls_agg_flat_size(H(h), &M));
+    if (rc < 0) { throw_for(env, rc, H(h)); return; }
+    double *dst = (double *)stage(env, 0, (size_t)n * 8);
     if (!dst) return;
-    int rc = LIB(ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64));
-    if (rc >= 0) (*env)->SetDoubleArrayRegion(env, out, 0, n, dst);
+    rc = LIB(ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64));
+    if (rc >= 0) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)(M < (int64_t)n ? M : (int64_t)n), dst);
     CHECK(rc, H(h));
 }
 

@@ -345,6 +345,31 @@ def test_jni_update_gradient_owned_subset(jvm, gpu, O):
 
 
 @pytest.mark.gpu
+def test_jni_get_partitions_longer_array(jvm, gpu, O):
+    """getPartitions(double[]) into an array longer than the model: the first
+    M values are GetPartitions' (IPLS.java:1159-1174), the rest keep what the
+    array held (the shim copies nothing in, and back only the model)."""
+    M, P = 30011, 3
+    h = _open(jvm, M, P)
+    w = [O.synth_bucket(O.partition_len(M, P, p), p, 5) for p in range(P)]
+    for p in range(P):
+        w[p][-1] = float(p + 2)                  # the count slot
+    # weights through a round: p's W = its one bucket (count slot included)
+    for p in range(P):
+        _, exc = jvm.call("accumulate", h, p, 0, jvm.doubles(w[p]))
+        assert exc is None
+        _, exc = jvm.call("finalizePartition", h, p, None)
+        assert exc is None
+    arr = jvm.doubles(np.full(M + 3, 7.0))
+    _, exc = jvm.call("getPartitions", h, arr)
+    assert exc is None
+    got = jvm.data(arr, np.float64)
+    assert_bits_equal(got[:M], O.get_partitions([0.0 + x for x in w]), "model")
+    assert (got[M:] == 7.0).all()
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
 def test_jni_exceptions_leave_state_unchanged(jvm, gpu, O):
     """A short bucket is ArrayIndexOutOfBoundsException with nothing folded
     (Updater.java:115-117 would throw mid-loop; the library rejects it first,
