@@ -9,6 +9,9 @@ One partition of L doubles (one bucket per call, as the Updater folds):
                                   ring chunks (ipls_agg_read_range), each copied
                                   into the byte[] while the next arrives
   finalizePartitionDirect      -- the BE sum straight into a direct buffer
+  getPartitions(double[])      -- GetPartitions (the divide) into a heap double[]
+  getPartitionsWire(ByteBuffer)-- the same as Middleware's big-endian stream into
+                                  a pinned direct buffer
 GB/s = bytes of the Java-side array / wall time per call (median of reps).
 Usage: jni_heap_probe.py [L] [reps]"""
 import ctypes
@@ -55,6 +58,9 @@ res["accumulate_heap_double[]"] = timed(lambda: jvm.call("accumulate", h, 0, 0, 
 res["accumulateDirect_pinned_BE"] = timed(lambda: jvm.call("accumulateDirect", h, 0, 0, pin_obj, 0, L64(L), 1))
 res["finalize_heap_byte[]"] = timed(lambda: jvm.call("finalizePartition", h, 0, out_heap))
 res["finalizeDirect_pinned"] = timed(lambda: jvm.call("finalizePartitionDirect", h, 0, pin_obj, 0))
+model = jvm.doubles(np.zeros(L - 1))
+res["getPartitions_heap_double[]"] = timed(lambda: jvm.call("getPartitions", h, model))
+res["getPartitionsWire_pinned"] = timed(lambda: jvm.call("getPartitionsWire", h, pin_obj, 0, L64(8 * (L - 1))))
 jvm.call("close", h)
 print(json.dumps({"L": L, "bytes_per_call": 8 * L, "reps": reps,
                   **{k: {"ms": round(v * 1e3, 3), "GBps": round(8 * L / v / 1e9, 2)} for k, v in res.items()}}))
