@@ -1963,8 +1963,9 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     Replicas_Gradients, Aggregated_Gradients_from_future, Weights): host and
     device folds, queued folds (coalescing group 1/4/32), batched folds with
     every start mode and byte order, AggregatePartition, resets, promotion of
-    future gradients, the async blend, cache_partition, the fused round and
-    GetPartitions.  Buckets include -0.0, subnormals and huge values so the
+    future gradients, the async blend, cache_partition, the fused round,
+    GetPartitions, and the JNI ring's ranged folds and reads from pinned memory
+    (ipls_agg_accumulate_range / ipls_agg_read_range at random even cuts).  Buckets include -0.0, subnormals and huge values so the
     start-value and grouping rules show in the bits.  ``devices``: the same
     sequence through a multi-device handle (shards [0,2) | [2,4), and a
     three-entry list whose last shard owns no partition), so the front's
@@ -2006,13 +2007,20 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     # map resizes through treeifyBin and grows red-black tree bins
     collide = seed % 3 == 2
     msgs = [O.pubsub_message(O.frame_encode(g, 0, 1, 3, b"QmS")) for g in pool]
+    from ipls import _native as N
+    lib, h = agg._lib, agg._h
+    pin = ipls.PinnedBuffer(8 * L + 64)          # the JNI shim's pinned ring, one slot of a whole bucket
+    tk = ctypes.c_uint64()
+
+    def cuts():                                  # even cut points: the ranges a chunked copy folds / reads
+        return sorted({0, L, *(2 * int(x) for x in rng.integers(0, L // 2 + 1, int(rng.integers(0, 4))))})
     script = list(prefix)
     for step in range(len(script) + steps):
         fixed = script[step] if step < len(script) else {}
 
         def draw(key, fn):
             return fixed[key] if key in fixed else fn()
-        op = draw("op", lambda: int(rng.integers(0, 17)))
+        op = draw("op", lambda: int(rng.integers(0, 19)))
         if collide and op in (8, 16) and "op" not in fixed:
             op = 14
         p = draw("p", lambda: int(rng.integers(0, P)))
@@ -2116,6 +2124,25 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
                 assert agg.replica_order()[0] == store.map.keys(), f"step {step}: replica order"
                 if shapes is not None and store.map.tree_bin:
                     shapes.add(("replica store", "tree bin", "", False, -1))
+        elif op == 17:                                      # a heap double[] through the ring: ranged folds
+            tg = [ipls.TGT_AGG, ipls.TGT_REP, ipls.TGT_FUTURE][int(rng.integers(0, 3))]
+            be = bool(rng.integers(0, 2))
+            raw = np.frombuffer(O.be_encode(g) if be else g.tobytes(), dtype=np.uint8)
+            pin.view()[:raw.size] = raw
+            for a, b in _pairs(cuts()):
+                assert lib.ipls_agg_accumulate_range(h, p, tg, pin.ptr + 8 * a, a, b - a,
+                                                     N.HOST_BE if be else N.HOST_F64, ctypes.byref(tk)) == 0
+            assert lib.ipls_agg_wait(h, tk.value) == 0
+            M[T[tg]][p] = M[T[tg]][p] + g
+        elif op == 18:                                      # a byte[] / double[] output through the ring
+            tg = list(T)[int(rng.integers(0, len(T)))]
+            be = bool(rng.integers(0, 2))
+            for a, b in _pairs(cuts()):
+                assert lib.ipls_agg_read_range(h, p, tg, pin.ptr + 8 * a, a, b - a,
+                                               N.HOST_BE if be else N.HOST_F64, ctypes.byref(tk)) == 0
+            assert lib.ipls_agg_wait(h, tk.value) == 0
+            want = O.be_encode(M[T[tg]][p]) if be else M[T[tg]][p].tobytes()
+            assert pin.view()[:8 * L].tobytes() == want, f"step {step}: read_range p{p} {T[tg]} be={be}"
         elif op == 15 and collide and rng.integers(0, 6):  # (collide: most collects skipped)
             pass
         elif op == 15:                                      # Collect_Replicas
@@ -2139,6 +2166,11 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
         for tg in T:
             check(p, tg, "end")
     agg.close()
+    pin.close()
+
+
+def _pairs(c):
+    return list(zip(c[:-1], c[1:]))
 
 
 def production_prefix(ipls, P):
