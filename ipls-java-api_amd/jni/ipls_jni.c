@@ -325,7 +325,10 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
         /* Pipelined: chunk k is copied out of the heap (GetDoubleArrayRegion)
          * into ring slot k % 2 while chunk k - 1 folds from the other slot
          * (ipls_agg_accumulate_range, zero copy).  Each element of the
-         * bucket's first L is added once, in order: the whole-bucket bits. */
+         * bucket's first L is added once, in order: the whole-bucket bits.
+         * Both slots exist before the first fold, so an OutOfMemoryError
+         * leaves the target unchanged. */
+        if (!ring_slot(env, 0) || !ring_slot(env, 1)) return;
         uint64_t tk[2] = {0, 0};
         int used[2] = {0, 0}, rc = 0;
         for (int64_t off = 0, k = 0; off < L; off += RING_CHUNK, ++k) {
@@ -334,7 +337,6 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
             if (used[s] && (rc = LIB(ipls_agg_wait(H(h), tk[s]))) < 0) break;
             used[s] = 0;
             double *buf = ring_slot(env, s);
-            if (!buf) { rc = 1; break; }                              /* OutOfMemoryError pending */
             (*env)->GetDoubleArrayRegion(env, g, (jsize)off, len, buf);
             if ((*env)->ExceptionCheck(env)) { rc = 1; break; }
             if ((rc = LIB(ipls_agg_accumulate_range(H(h), p, tgt, buf, off, len, IPLS_HOST_F64, &tk[s]))) < 0) break;
@@ -466,26 +468,22 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jcla
         /* Pipelined: AggregatePartition on the device, then the commit_update
          * bytes of W in ring-sized chunks (ipls_agg_read_range, big-endian,
          * into the pinned ring): chunk k is copied into the byte[] while
-         * chunk k + 1 is still coming back. */
+         * chunk k + 1 is still coming back.  Both slots exist before the
+         * round is consumed, so an OutOfMemoryError leaves it in place. */
+        if (!ring_slot(env, 0) || !ring_slot(env, 1)) return;
         int rc = LIB(ipls_agg_finalize(H(h), p, NULL, IPLS_HOST_BE, NULL));
         if (rc < 0) { throw_for(env, rc, H(h)); return; }
-        const int64_t K = (L + RING_CHUNK - 1) / RING_CHUNK;
+        const int64_t K = (L + RING_CHUNK - 1) / RING_CHUNK;   /* >= 2 */
         uint64_t tk[2] = {0, 0};
         int live[2] = {0, 0};
-        for (int64_t j = 0; j < K && j < 1 && rc >= 0; ++j) {   /* chunk 0 */
-            double *buf = ring_slot(env, 0);
-            if (!buf) { rc = 1; break; }
-            rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, buf, 0, L < RING_CHUNK ? L : RING_CHUNK,
-                                         IPLS_HOST_BE, &tk[0]));
-            live[0] = rc >= 0;
-        }
+        rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, ring_slot(env, 0), 0, RING_CHUNK, IPLS_HOST_BE, &tk[0]));
+        live[0] = rc >= 0;
         for (int64_t k = 0; k < K && rc >= 0; ++k) {
             const int s = (int)(k & 1), t = 1 - s;
             if (k + 1 < K) {   /* chunk k + 1 into the other slot (its chunk k - 1 is already out) */
                 const int64_t off = (k + 1) * RING_CHUNK, len = L - off < RING_CHUNK ? L - off : RING_CHUNK;
-                double *buf = ring_slot(env, t);
-                if (!buf) { rc = 1; break; }
-                if ((rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, buf, off, len, IPLS_HOST_BE, &tk[t]))) < 0)
+                if ((rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, ring_slot(env, t), off, len, IPLS_HOST_BE,
+                                                  &tk[t]))) < 0)
                     break;
                 live[t] = 1;
             }
