@@ -1583,6 +1583,58 @@ def test_maximum_sizes(ipls, O, P, L, K):
     torch.cuda.empty_cache()
 
 
+def test_maximum_sizes_elementwise(ipls, O):
+    """The elementwise kernels in their 16-B tile shape on Java's largest
+    partition (L = Integer.MAX_VALUE - 2, byte offsets up to 2^34):
+    UpdateGradient's own accumulate into a logically-zero AGG and then a live
+    one (k_split, IPLS.java:1737-1743), AggregatePartition, the async replica
+    fold and the leaving-peer blend (k_blend, Updater.java:57-59,65-69) and the
+    publish scale (k_scale, Updater.java:197-199).  Each state is checked by
+    its position-keyed checksum against the same IEEE operations in torch fp64
+    on the device (one rounding per multiply and per add, as the kernels do:
+    -ffp-contract=off); the oracle's Python loops would take minutes here."""
+    L = 2**31 - 3
+    M = L - 1
+    need = 8 * L * 10 + (1 << 30)        # AGG/REP/W/FUT + v + two expected states + temporaries
+    if _free_hbm() < need:
+        pytest.skip(f"needs {need / 2**30:.0f} GiB of free HBM")
+    v = torch.empty(L, dtype=torch.float64, device="cuda")
+    ipls.synth_fill(ipls.DeviceBuffer.from_tensor(v), 0, 3, O.SEED)
+    torch.cuda.synchronize()
+    v[M] = 1.0                           # OrganizeGradients' count slot (IPLS.java:1033)
+    torch.cuda.synchronize()             # torch's stream; the handle's stream does not wait on it
+    flat = ipls.DeviceBuffer(int(v.data_ptr()), M)
+    agg = ipls.Aggregator(M, 1)
+    assert agg.lengths == [L]
+
+    def same(target, want, what):
+        torch.cuda.synchronize()
+        assert agg.checksum(0, target) == ipls.checksum_dev(ipls.DeviceBuffer.from_tensor(want)), what
+
+    agg.UpdateGradient(flat, [0])
+    exp = v + 0.0
+    same(ipls.TGT_AGG, exp, "own accumulate into a logically-zero AGG")
+    agg.UpdateGradient(flat, [0])
+    exp = exp + v
+    same(ipls.TGT_AGG, exp, "own accumulate into a live AGG")
+    agg.AggregatePartition(0)
+    w = exp + 0.0
+    del exp
+    same(ipls.TGT_WEIGHTS, w, "AggregatePartition")
+    agg.UpdateAsyncReplica(ipls.DeviceBuffer.from_tensor(v), 0)
+    w = w * 0.75 + v * 1.0
+    same(ipls.TGT_WEIGHTS, w, "async replica fold")
+    a = agg.LEAVING_A
+    agg.UpdateLeavingPeer(ipls.DeviceBuffer.from_tensor(v), 0)
+    w = w * a + v * (1 - a)
+    same(ipls.TGT_WEIGHTS, w, "leaving-peer blend")
+    agg.AsyncPublishScale(0)
+    same(ipls.TGT_AGG, w * 0.25, "publish scale")
+    agg.close()
+    del v, w
+    torch.cuda.empty_cache()
+
+
 def test_async_pinned_arrivals(ipls, O):
     """ipls_agg_accumulate_async: queued zero-copy folds give the same bits as
     synchronous Updates, in call order, across more folds than the ticket ring."""
