@@ -1589,7 +1589,8 @@ def test_maximum_sizes_elementwise(ipls, O):
     UpdateGradient's own accumulate into a logically-zero AGG and then a live
     one (k_split, IPLS.java:1737-1743), AggregatePartition, the async replica
     fold and the leaving-peer blend (k_blend, Updater.java:57-59,65-69) and the
-    publish scale (k_scale, Updater.java:197-199).  Each state is checked by
+    publish scale (k_scale, Updater.java:197-199), and a ranged fold and
+    ranged read (the JNI ring's) near the partition's end.  Each state is checked by
     its position-keyed checksum against the same IEEE operations in torch fp64
     on the device (one rounding per multiply and per add, as the kernels do:
     -ffp-contract=off); the oracle's Python loops would take minutes here."""
@@ -1630,8 +1631,27 @@ def test_maximum_sizes_elementwise(ipls, O):
     same(ipls.TGT_WEIGHTS, w, "leaving-peer blend")
     agg.AsyncPublishScale(0)
     same(ipls.TGT_AGG, w * 0.25, "publish scale")
+    del w
+    # the JNI ring's ranged fold and read at element offsets past 2^31 - 2^20
+    from ipls import _native as N
+    n = 1 << 20
+    off = (L - n - 1) & ~1
+    chunk = O.synth_bucket(n, 5, 1)
+    pin = ipls.PinnedBuffer(8 * n)
+    pin.view()[:] = np.frombuffer(chunk.tobytes(), dtype=np.uint8)
+    t = ctypes.c_uint64()
+    assert agg._lib.ipls_agg_accumulate_range(agg._h, 0, ipls.TGT_REP, pin.ptr, off, n, N.HOST_F64,
+                                              ctypes.byref(t)) == 0
+    assert agg._lib.ipls_agg_wait(agg._h, t.value) == 0
+    assert agg._lib.ipls_agg_read_range(agg._h, 0, ipls.TGT_REP, pin.ptr, off, n, N.HOST_BE, ctypes.byref(t)) == 0
+    assert agg._lib.ipls_agg_wait(agg._h, t.value) == 0
+    assert pin.view()[:8 * n].tobytes() == O.be_encode(chunk + 0.0), "ranged fold, then ranged read"
+    rep = torch.zeros(L, dtype=torch.float64, device="cuda")
+    rep[off:off + n] = torch.from_numpy(chunk + 0.0).to("cuda")
+    same(ipls.TGT_REP, rep, "ranged fold into a logically-zero REP")
+    pin.close()
     agg.close()
-    del v, w
+    del v, rep
     torch.cuda.empty_cache()
 
 
