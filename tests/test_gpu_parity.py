@@ -273,6 +273,23 @@ def test_split_device_and_be(ipls, O):
     agg.close()
 
 
+@pytest.mark.parametrize("M,P,devices", [(443610, 3, None), (50001, 5, None), (10, 4, None), (100003, 7, [0, 0, 0]),
+                                         (7, 8, [0, 0])])
+def test_flat_size_and_offsets(ipls, O, M, P, devices):
+    """ipls_agg_flat_size (what the JNI getPartitions copies back) is the
+    model size, and partition_offset / partition_len follow the chunk rule
+    (IPLS.java:1019-1029), on one- and multi-shard handles; in (7, 8) the
+    last partition holds only its count slot (L_p = 1)."""
+    agg = ipls.Aggregator(M, P, devices=devices)
+    n = ctypes.c_int64()
+    assert agg._lib.ipls_agg_flat_size(agg._h, ctypes.byref(n)) == 0
+    assert n.value == agg.flat_size == M
+    c = O.chunk_size(M, P)
+    assert agg.offsets == [p * c for p in range(P)]
+    assert agg.lengths == [O.partition_len(M, P, p) for p in range(P)]
+    agg.close()
+
+
 def test_update_gradient_owned_subset(ipls, O):
     M, P = 50001, 5
     g1, g2 = O.synth_bucket(M, 0, 1), O.synth_bucket(M, 0, 2)
