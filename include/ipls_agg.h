@@ -390,6 +390,18 @@ int ipls_agg_set_weights(ipls_agg *h, int p, const void *src, int64_t n, int src
  * doubles; out_kind HOST_F64, HOST_BE_CANON (Middleware task-3 stream), DEV_F64. */
 int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
 
+/* GetPartitions (IPLS.java:1159-1174) delivered in chunks of `chunk` doubles
+ * (even, >= 2) to sink(ctx, values, offset, n) on the calling thread, in
+ * model order: the divide runs once on the GPU, then each chunk comes back
+ * through a pinned two-slot ring, so the sink's copy of chunk k overlaps the
+ * transfer of chunk k + 1 (the JNI getPartitions(double[]) copies each chunk
+ * into the Java array with SetDoubleArrayRegion).  `values` is valid only
+ * during the sink call.  A non-zero sink return stops the transfer: the call
+ * returns IPLS_E_INVAL and no further chunk is delivered.  The sink must not
+ * call into this handle.  Replaces the same loop as ipls_agg_get_partitions. */
+typedef int (*ipls_chunk_sink)(void *ctx, const double *values, int64_t offset, int64_t n);
+int ipls_agg_get_partitions_chunked(ipls_agg *h, int64_t chunk, ipls_chunk_sink sink, void *ctx);
+
 /* Copy an accumulator out (tests, replica publish IPLS.java:1423-1431).
  * dst_kind HOST_F64, HOST_BE, DEV_F64, DEV_BE; n >= L_p. */
 int ipls_agg_read(ipls_agg *h, int p, int target, void *dst, int64_t n, int dst_kind);

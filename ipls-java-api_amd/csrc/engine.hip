@@ -85,6 +85,8 @@ struct ipls_dev {
   std::vector<unsigned char> last_table;  // cache of the last uploaded table
   int last_slot = -1;
 
+  // pinned two-slot ring of dev_get_partitions_chunked (lazily, freed at close)
+  PinnedSlot out_ring[2];
   // staging
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -955,6 +957,10 @@ int dev_close(ipls_dev* h) {
   dev_use(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   for (auto& s : h->ring) {
+    if (s.host) hipHostFree(s.host);
+    if (s.ev) hipEventDestroy(s.ev);
+  }
+  for (auto& s : h->out_ring) {
     if (s.host) hipHostFree(s.host);
     if (s.ev) hipEventDestroy(s.ev);
   }
@@ -1962,6 +1968,52 @@ int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind) {
   if (int rc = divide_range(h, 0, h->P, d_out, out_kind == IPLS_HOST_BE_CANON)) return rc;
   if (out_kind == IPLS_DEV_F64) return IPLS_OK;
   return d2h(h, out, d_out, (size_t)M * 8);
+}
+
+// GetPartitions (IPLS.java:1159-1174) handed to the caller chunk by chunk:
+// the divide runs once into the device scratch, then chunk k + 1 is copied
+// into one slot of a pinned two-slot ring while sink() consumes chunk k from
+// the other, on the calling thread (the JNI shim's sink is
+// SetDoubleArrayRegion, so the heap copy overlaps the transfer).  sink gets
+// flat model offsets (this engine's segment starts at flat_base); a non-zero
+// return stops the transfer
+// (IPLS_E_INVAL, nothing further is delivered).  The sink must not call
+// into this handle.
+int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  if (!h || !sink) return fail(h, IPLS_E_INVAL, "null argument");
+  if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld doubles: even and >= 2", (long long)chunk);
+  IPLS_LOCK(h);
+  const int64_t M = h->flat_total - h->flat_base;
+  if (M <= 0) return IPLS_OK;
+  HIP_TRY(h, dev_use(h->device));
+  if (int rc = ensure_scratch(h, (size_t)M * 8)) return rc;
+  const double* d_out = (const double*)h->d_scratch;
+  if (int rc = divide_range(h, 0, h->P, (unsigned long long*)h->d_scratch, false)) return rc;
+  const int64_t c = std::min(chunk, M);
+  for (auto& sl : h->out_ring)
+    if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;
+  const int64_t K = (M + c - 1) / c;
+  auto issue = [&](int64_t k) -> int {
+    PinnedSlot& sl = h->out_ring[k & 1];
+    const int64_t off = k * c, len = std::min(c, M - off);
+    HIP_TRY(h, hipMemcpyAsync(sl.host, d_out + off, (size_t)len * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipEventRecord(sl.ev, h->stream));
+    return IPLS_OK;
+  };
+  if (int rc = issue(0)) return rc;
+  for (int64_t k = 0; k < K; ++k) {
+    // chunk k + 1 goes into the slot chunk k - 1 used, whose sink has returned
+    if (k + 1 < K)
+      if (int rc = issue(k + 1)) return rc;
+    PinnedSlot& sl = h->out_ring[k & 1];
+    HIP_TRY(h, hipEventSynchronize(sl.ev));
+    const int64_t off = k * c, len = std::min(c, M - off);
+    if (sink(ctx, (const double*)sl.host, h->flat_base + off, len) != 0) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));   // the copy still writing the other slot
+      return fail(h, IPLS_E_INVAL, "the chunk sink stopped the transfer at offset %lld", (long long)(h->flat_base + off));
+    }
+  }
+  return IPLS_OK;
 }
 
 // ---- device utilities ----

@@ -1003,6 +1003,16 @@ int ipls_agg_get_partitions(ipls_agg* H, void* out, int64_t n, int out_kind) {
   });
 }
 
+int ipls_agg_get_partitions_chunked(ipls_agg* H, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  KeepDevice keep_device;
+  if (!H || !sink) return ferr(H, IPLS_E_INVAL, "null argument");
+  // shard by shard on the calling thread, in model order: the sink runs
+  // where the caller is (a JNIEnv belongs to its thread)
+  for (int s : nonempty_shards(H))
+    if (int rc = fwd(H, s, dev_get_partitions_chunked(H->sh[s], chunk, sink, ctx))) return rc;
+  return IPLS_OK;
+}
+
 int ipls_agg_read(ipls_agg* H, int p, int target, void* dst, int64_t n, int dst_kind) {
   KeepDevice keep_device;
   if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");

@@ -29,6 +29,10 @@ ABI_VERSION = 3
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1
 
+# ipls_chunk_sink: int (*)(void *ctx, const double *values, int64_t offset, int64_t n)
+CHUNK_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64,
+                              ctypes.c_int64)
+
 ERROR_NAMES = {
     IPLS_E_INVAL: "IllegalArgument",
     IPLS_E_RANGE: "ArrayIndexOutOfBounds",
@@ -99,6 +103,7 @@ SIGNATURES = {
     "ipls_agg_accumulate_range": (_i, [_vp, _i, _i, _vp, _i64, _i64, _i, _P(_u64)]),
     "ipls_agg_read_range": (_i, [_vp, _i, _i, _vp, _i64, _i64, _i, _P(_u64)]),
     "ipls_agg_flat_size": (_i, [_vp, _P(_i64)]),
+    "ipls_agg_get_partitions_chunked": (_i, [_vp, _i64, _vp, _vp]),   # sink: a CHUNK_SINK instance
     "ipls_agg_wait": (_i, [_vp, _u64]),
     "ipls_agg_set_coalesce": (_i, [_vp, _i]),
     "ipls_agg_flush": (_i, [_vp]),

@@ -536,6 +536,15 @@ JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass
     CHECK(LIB(ipls_agg_set_weights(H(h), p, src, n, IPLS_HOST_FRAME)), H(h));
 }
 
+/* The chunk sink of getPartitions: each chunk of the model straight from
+ * the library's pinned ring into the Java array. */
+struct model_sink { JNIEnv *env; jdoubleArray out; };
+static int model_sink_fn(void *ctx, const double *values, int64_t off, int64_t n) {
+    struct model_sink *m = (struct model_sink *)ctx;
+    (*m->env)->SetDoubleArrayRegion(m->env, m->out, (jsize)off, (jsize)n, values);
+    return (*m->env)->ExceptionCheck(m->env) ? 1 : 0;
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c, jlong h, jdoubleArray out) {
     (void)c;
     if (!out) { throw_iae(env, "null output"); return; }
@@ -545,6 +554,15 @@ JNIEXPORT void JNICALL Java_NativeAggregator_getPartitions(JNIEnv *env, jclass c
     int64_t M = 0;
     int rc = LIB(ipls_agg_flat_size(H(h), &M));
     if (rc < 0) { throw_for(env, rc, H(h)); return; }
+    if (M >= 2 * RING_CHUNK && M <= n) {
+        /* Pipelined: the divide once on the GPU, then the model comes back in
+         * ring-sized chunks, each copied into the array while the next is in
+         * flight (ipls_agg_get_partitions_chunked). */
+        struct model_sink ms = {env, out};
+        rc = LIB(ipls_agg_get_partitions_chunked(H(h), RING_CHUNK, model_sink_fn, &ms));
+        if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_for(env, rc, H(h));
+        return;
+    }
     double *dst = (double *)stage(env, 0, (size_t)n * 8);
     if (!dst) return;
     rc = LIB(ipls_agg_get_partitions(H(h), dst, n, IPLS_HOST_F64));

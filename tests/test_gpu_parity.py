@@ -273,6 +273,64 @@ def test_split_device_and_be(ipls, O):
     agg.close()
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0], [0, 0, 0]])
+def test_get_partitions_chunked(ipls, O, devices):
+    """ipls_agg_get_partitions_chunked: GetPartitions (IPLS.java:1159-1174)
+    delivered to a sink chunk by chunk, in model order, on the calling thread;
+    the chunks tile [0, M) exactly and carry the bits of the oracle's model,
+    for chunks of 2 doubles, an odd chunk count, and one chunk larger than the
+    model, on one- and multi-shard handles (shard segments in order).  A sink
+    that returns non-zero stops the transfer; an odd chunk is refused."""
+    from ipls import _native as N
+    M, P = 300007, 3
+    agg = ipls.Aggregator(M, P, devices=devices)
+    lib, h = agg._lib, agg._h
+    flats = [O.synth_bucket(M, 6, k) for k in range(2)]
+    for g in flats:
+        agg.UpdateGradient(g, range(P))
+    for p in range(P):
+        agg.AggregatePartition(p)
+    parts = [O.organize_gradients(g, M, P) for g in flats]
+    want = O.get_partitions([O.reduce([pt[p] for pt in parts], agg.lengths[p]) + 0.0 for p in range(P)])
+    for chunk in (65536, 2, 100002, 1 << 22):
+        got = np.full(M, np.nan)
+        seen = []
+
+        @N.CHUNK_SINK
+        def sink(ctx, vals, off, n):
+            got[off:off + n] = np.ctypeslib.as_array(vals, shape=(n,))
+            seen.append((off, n))
+            return 0
+        if chunk == 2:                            # 150,004 sink calls: check a slice only
+            got_small = []
+
+            @N.CHUNK_SINK
+            def sink(ctx, vals, off, n):          # noqa: F811
+                if off < 1000:
+                    got_small.append((off, vals[0], vals[1]))
+                seen.append((off, n))
+                return 0
+            assert lib.ipls_agg_get_partitions_chunked(h, chunk, sink, None) == 0
+            assert [o for o, _ in seen] == sorted(o for o, _ in seen) and sum(n for _, n in seen) == M
+            assert all(want[o] == a and want[o + 1] == b for o, a, b in got_small)
+            continue
+        assert lib.ipls_agg_get_partitions_chunked(h, chunk, sink, None) == 0
+        assert [o for o, _ in seen] == sorted(o for o, _ in seen)
+        assert sum(n for _, n in seen) == M and all(n <= chunk for _, n in seen)
+        assert_bits_equal(got, want, f"chunk {chunk}")
+    calls = []
+
+    @N.CHUNK_SINK
+    def stop(ctx, vals, off, n):
+        calls.append(off)
+        return 1 if len(calls) == 2 else 0
+    assert lib.ipls_agg_get_partitions_chunked(h, 65536, stop, None) == N.IPLS_E_INVAL
+    assert calls == [0, 65536]
+    assert lib.ipls_agg_get_partitions_chunked(h, 65537, stop, None) == N.IPLS_E_INVAL
+    assert_bits_equal(agg.GetPartitions(), want, "model after a stopped transfer")
+    agg.close()
+
+
 @pytest.mark.parametrize("M,P,devices", [(443610, 3, None), (50001, 5, None), (10, 4, None), (100003, 7, [0, 0, 0]),
                                          (7, 8, [0, 0])])
 def test_flat_size_and_offsets(ipls, O, M, P, devices):

@@ -370,6 +370,37 @@ def test_jni_get_partitions_longer_array(jvm, gpu, O):
 
 
 @pytest.mark.gpu
+def test_jni_get_partitions_pipelined(jvm, gpu, O):
+    """getPartitions(double[]) for a model of >= 2 ring chunks goes through
+    ipls_agg_get_partitions_chunked: each chunk is copied into the Java array
+    (SetDoubleArrayRegion, from the library's pinned ring) while the next is
+    in flight.  The model's bits equal the oracle's, elements past the model
+    keep their values, and a short array is still
+    ArrayIndexOutOfBoundsException with the array untouched."""
+    M, P = 2 * 1048576 + 4099, 2
+    h = _open(jvm, M, P)
+    g = O.synth_bucket(M, 8, 1)
+    _, exc = jvm.call("updateGradient", h, jvm.doubles(g), jvm.ints([0, 1]))
+    assert exc is None
+    for p in range(P):
+        _, exc = jvm.call("finalizePartition", h, p, None)
+        assert exc is None
+    parts = O.organize_gradients(g, M, P)
+    want = O.get_partitions([O.reduce([parts[p]], O.partition_len(M, P, p)) + 0.0 for p in range(P)])
+    arr = jvm.doubles(np.full(M + 3, 7.0))
+    _, exc = jvm.call("getPartitions", h, arr)
+    assert exc is None
+    got = jvm.data(arr, np.float64)
+    assert_bits_equal(got[:M], want, "model")
+    assert (got[M:] == 7.0).all()
+    short = jvm.doubles(np.full(M - 1, 5.0))
+    _, exc = jvm.call("getPartitions", h, short)
+    assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    assert (jvm.data(short, np.float64) == 5.0).all()
+    jvm.call("close", h)
+
+
+@pytest.mark.gpu
 def test_jni_exceptions_leave_state_unchanged(jvm, gpu, O):
     """A short bucket is ArrayIndexOutOfBoundsException with nothing folded
     (Updater.java:115-117 would throw mid-loop; the library rejects it first,
