@@ -111,3 +111,30 @@ def test_bucket_table_size_checks():
     assert _bucket_table([], lengths, 0) == ([], 0)
     # a partition out of range is the library's IPLS_E_RANGE, not a size error here
     assert _bucket_table([[ipls.DeviceBuffer(8, 1)]], lengths, 5) == ([8], 1)
+
+
+def test_committed_pmc_entries_carry_their_build():
+    """Every committed PMC entry names the build it was taken on and the
+    profile it came from; an entry without them would make bench.py report
+    `traffic: null` (tools/pmc_traffic.py stores nothing without --bench-log)."""
+    d = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())
+    for k in ("C", "C-round", "C-finalize", "C-divide", "B", "D-be", "F"):   # the entries bench.py reads
+        e = d[k]                                                             # (C_r02 ... are history)
+        b = e.get("build") or {}
+        assert b.get("so_sha256") and b.get("device_code_sha256"), k
+        assert (ROOT / e["source"]).is_dir(), (k, e.get("source"))
+        assert 0.99 <= e["traffic_over_algorithmic"] <= 1.1, k
+
+
+def test_pmc_tool_stores_nothing_without_a_build(tmp_path):
+    sys.path.insert(0, str(ROOT / "tools"))
+    fetch = tmp_path / "f.csv"
+    write = tmp_path / "w.csv"
+    hdr = "Dispatch_Id,Kernel_Name,Grid_Size,Workgroup_Size,VGPR_Count,Counter_Name,Counter_Value\n"
+    fetch.write_text(hdr + "1,k_reduce,1,1,1,FETCH_SIZE,4.0\n")
+    write.write_text(hdr + "1,k_reduce,1,1,1,WRITE_SIZE,8.0\n")
+    out = tmp_path / "pmc.json"
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "pmc_traffic.py"), "C", str(fetch), str(write), "16384",
+                        str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert not out.exists() and "not stored" in r.stderr

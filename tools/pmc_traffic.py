@@ -78,7 +78,10 @@ def main():
                                                          "git_rev", "sources_dirty")}
     if source:
         d[wl]["source"] = source
-    out.write_text(json.dumps(d, indent=1) + "\n")
+    if builds:
+        out.write_text(json.dumps(d, indent=1) + "\n")
+    else:   # an entry without a build record would hide its traffic from every bench line: report only
+        print("not stored: no --bench-log, so no build record", file=sys.stderr)
     print(json.dumps(d[wl]))
 
 
