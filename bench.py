@@ -1330,8 +1330,30 @@ def claim_stdout() -> None:
         os.dup2(2, 1)
 
 
+TAIL_KEYS = ("verified", "verified_partitions", "build")
+BUILD_TAIL = ("so_sha256", "device_code_sha256", "built_utc", "stamp_matches_so", "sources_match")
+
+
+def proof_last(obj: dict) -> dict:
+    """The line with the headline's proof as its LAST keys: whether every
+    timed partition matched the oracle, and which library ran (ending with
+    sources_match).  The driver's record keeps only the tail of stdout, so
+    these are what it must still hold when the side legs have made the line
+    long."""
+    out = {k: v for k, v in obj.items() if k not in TAIL_KEYS}
+    for k in TAIL_KEYS:
+        if k in obj:
+            v = obj[k]
+            if k == "build" and isinstance(v, dict):
+                v = {**{b: x for b, x in v.items() if b not in BUILD_TAIL}, **{b: v[b] for b in BUILD_TAIL if b in v}}
+            out[k] = v
+    return out
+
+
 def emit(obj) -> None:
-    """Write the JSON line to the real stdout."""
+    """Write the JSON line to the real stdout (the proof of the headline last)."""
+    if isinstance(obj, dict):
+        obj = proof_last(obj)
     out = _JSON_OUT if _JSON_OUT is not None else sys.stdout
     out.write(json.dumps(obj) + "\n")
     out.flush()

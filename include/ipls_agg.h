@@ -22,10 +22,19 @@
  *    stream (the null stream included) must be complete, or ordered before
  *    the call by an event the handle's stream waits on (ipls_agg_stream /
  *    ipls_agg_partition_device give the stream).
- *  - A handle is internally serialised (one mutex): it may be called from
- *    the Updater thread and the daemon thread concurrently, as the Java code
- *    does under PeerData.mtx (PeerData.java:27).  Calls on one partition
- *    take effect in call order -- the reference's arrival order.
+ *  - A handle is internally serialised (one mutex per GPU shard): it may be
+ *    called from the Updater thread and the daemon thread concurrently, as the
+ *    Java code does under PeerData.mtx (PeerData.java:27).  Each CALL is one
+ *    ordered unit: calls on one partition take effect in call order -- the
+ *    reference's arrival order.  A SEQUENCE of calls is not a unit: another
+ *    thread's call may land between two calls of one thread.  So what one
+ *    Java-side step must do atomically is one call here: a whole arriving
+ *    bucket (ipls_agg_accumulate, or ipls_agg_accumulate_chunked for a
+ *    caller that produces the bucket chunk by chunk), AggregatePartition plus
+ *    its commit_update bytes (ipls_agg_finalize, ipls_agg_finalize_chunked).
+ *    ipls_agg_accumulate_range / ipls_agg_read_range are single calls too:
+ *    a caller that splits one arrival into ranges holds its own lock across
+ *    them (PeerData.mtx, Updater.java:72-149) or gets a mixed order.
  *  - Every ipls_agg_* call returns with the calling thread's current HIP
  *    device unchanged, whichever GPUs the handle's shards live on.
  *  - Arithmetic is IEEE binary64 with no contraction and no reassociation:
@@ -43,7 +52,7 @@
 extern "C" {
 #endif
 
-#define IPLS_AGG_ABI_VERSION 3
+#define IPLS_AGG_ABI_VERSION 4
 
 /* ---- error codes (Java exception the reference would raise) ---- */
 #define IPLS_OK           0
@@ -114,6 +123,13 @@ typedef struct ipls_agg_cfg {
     int32_t n_devices;
     int32_t reserved;            /* must be 0 */
 } ipls_agg_cfg;
+
+/* Caller callbacks of the chunked calls (ipls_agg_get_partitions_chunked,
+ * ipls_agg_finalize_chunked: sink; ipls_agg_accumulate_chunked: source).
+ * They run on the calling thread, inside the call, and must not call into
+ * the same handle. */
+typedef int (*ipls_chunk_sink)(void *ctx, const double *values, int64_t offset, int64_t n);
+typedef int (*ipls_chunk_source)(void *ctx, void *dst, int64_t offset, int64_t n);
 
 /* ABI version of the loaded library (IPLS_AGG_ABI_VERSION). */
 int ipls_agg_abi_version(void);
@@ -192,9 +208,35 @@ int ipls_agg_accumulate_async(ipls_agg *h, int p, int target, const void *src, i
  * first copy the bucket (the JNI shim's double[] natives) overlap that copy
  * with the fold, chunk by chunk.  Keep src untouched until
  * ipls_agg_wait(h, *ticket) returns.  IPLS_E_RANGE outside [0, L_p);
- * IPLS_E_INVAL for other memory or a misaligned range. */
+ * IPLS_E_INVAL for other memory or a misaligned range.
+ * Each range is its own call: another thread's fold into the same target
+ * can land between two ranges of one arrival, and the elements of the
+ * earlier ranges then see a different order than those of the later ones.
+ * Hold a lock across the ranges, or use ipls_agg_accumulate_chunked. */
 int ipls_agg_accumulate_range(ipls_agg *h, int p, int target, const void *src, int64_t offset, int64_t n,
                               int src_kind, uint64_t *ticket);
+
+/* One arriving bucket that the caller produces chunk by chunk, as ONE call
+ * (Updater._Update's whole-bucket fold under PeerData.mtx, Updater.java:72-149,
+ * 115-117): the library calls source(ctx, dst, offset, n) on the calling
+ * thread for consecutive chunks of `chunk` values (even, >= 2) covering
+ * [0, L_p); the source writes the bucket's values [offset, offset + n) into
+ * dst -- 8 * n bytes of pinned staging owned by the library, native doubles
+ * (HOST_F64) or big-endian bytes (HOST_BE) -- and returns 0.  Each chunk is
+ * sent to the GPU while the source fills the next one; once every chunk has
+ * landed, the bucket is folded into target[p] in one launch.
+ *  - n is the caller's bucket length: n < L_p is IPLS_E_RANGE before any
+ *    source call (the ArrayIndexOutOfBoundsException of Updater.java:115);
+ *    values past L_p are never asked for.
+ *  - All or nothing: a non-zero source return stops the call with
+ *    IPLS_E_INVAL and nothing folded.
+ *  - The shard's lock is held from the first source call to the fold's
+ *    launch, so no other caller's call on this GPU shard lands in between:
+ *    the bits are those of ipls_agg_accumulate on the whole bucket, in call
+ *    order.  The source must not call into this handle.
+ * The JNI shim's accumulate(double[]) source is GetDoubleArrayRegion. */
+int ipls_agg_accumulate_chunked(ipls_agg *h, int p, int target, int64_t n, int src_kind, int64_t chunk,
+                                ipls_chunk_source source, void *ctx);
 
 /* The reverse of a ranged fold, asynchronous: target[offset .. offset+n) of
  * partition p is copied into pinned host memory dst (ipls_host_alloc), as
@@ -202,9 +244,10 @@ int ipls_agg_accumulate_range(ipls_agg *h, int p, int target, const void *src, i
  * update_file writes, MyIPFSClass.java:105-116).  dst is complete when
  * ipls_agg_wait(h, *ticket) returns.  With ipls_agg_finalize(h, p, NULL, ...)
  * first, reading IPLS_TGT_WEIGHTS in ranges gives the commit_update bytes
- * chunk by chunk (the JNI shim's finalizePartition(byte[]) copies each chunk
- * into the Java array while the next is in flight).  IPLS_E_RANGE outside
- * [0, L_p); IPLS_E_INVAL for other memory. */
+ * chunk by chunk -- but as separate calls, so a set_weights or a finalize
+ * from another thread between them tears the bytes: ipls_agg_finalize_chunked
+ * is the one-call form.  IPLS_E_RANGE outside [0, L_p); IPLS_E_INVAL for
+ * other memory. */
 int ipls_agg_read_range(ipls_agg *h, int p, int target, void *dst, int64_t offset, int64_t n, int dst_kind,
                         uint64_t *ticket);
 
@@ -362,6 +405,21 @@ int ipls_agg_scale(ipls_agg *h, int p, int dst_target, int src_target, double c)
  * (L_p - 1 averaged values, the GetPartitions divide).  Either may be NULL. */
 int ipls_agg_finalize(ipls_agg *h, int p, void *sum_out, int sum_kind, double *avg_out);
 
+/* ipls_agg_finalize of one partition with its sum handed to a sink chunk by
+ * chunk, as ONE call: AggregatePartition (IPLS.java:1248-1274), then W[p]
+ * comes back through a pinned two-slot ring in chunks of `chunk` values
+ * (even, >= 2), sink(ctx, values, offset, n) on the calling thread for
+ * consecutive ranges of [0, L_p), so the sink's copy of one chunk overlaps
+ * the transfer of the next.  values: n 8-byte values, doubles (HOST_F64) or
+ * the commit_update file bytes (HOST_BE, update_file's putDouble order,
+ * MyIPFSClass.java:105-116), valid during the sink call only.  The shard's
+ * lock is held throughout, so no set_weights, fold or finalize of another
+ * thread tears the bytes.  A non-zero sink return stops the delivery with
+ * IPLS_E_INVAL; the round is consumed either way (W is written, AGG = REP =
+ * 0), as after a failed update_file.  The sink must not call into this
+ * handle.  The JNI shim's finalizePartition(byte[]) sink is SetByteArrayRegion. */
+int ipls_agg_finalize_chunked(ipls_agg *h, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void *ctx);
+
 /* A whole aggregation round for partitions [p_first, p_first+n_parts) in ONE
  * kernel launch (one pass over the buckets):
  *   AGG[p]   = AGG[p] + b_0 + ... + b_{k-1}     Updater._Update folds (Updater.java:115-117)
@@ -399,7 +457,6 @@ int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
  * during the sink call.  A non-zero sink return stops the transfer: the call
  * returns IPLS_E_INVAL and no further chunk is delivered.  The sink must not
  * call into this handle.  Replaces the same loop as ipls_agg_get_partitions. */
-typedef int (*ipls_chunk_sink)(void *ctx, const double *values, int64_t offset, int64_t n);
 int ipls_agg_get_partitions_chunked(ipls_agg *h, int64_t chunk, ipls_chunk_sink sink, void *ctx);
 
 /* Copy an accumulator out (tests, replica publish IPLS.java:1423-1431).

@@ -85,8 +85,11 @@ struct ipls_dev {
   std::vector<unsigned char> last_table;  // cache of the last uploaded table
   int last_slot = -1;
 
-  // pinned two-slot ring of dev_get_partitions_chunked (lazily, freed at close)
+  // pinned two-slot rings of the chunked calls (lazily, freed at close):
+  // device -> host (get_partitions_chunked, finalize_chunked) and host ->
+  // device (accumulate_chunked)
   PinnedSlot out_ring[2];
+  PinnedSlot in_ring[2];
   // staging
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -964,6 +967,10 @@ int dev_close(ipls_dev* h) {
     if (s.host) hipHostFree(s.host);
     if (s.ev) hipEventDestroy(s.ev);
   }
+  for (auto& s : h->in_ring) {
+    if (s.host) hipHostFree(s.host);
+    if (s.ev) hipEventDestroy(s.ev);
+  }
   if (h->copy_ev) hipEventDestroy(h->copy_ev);
   for (hipStream_t cs : h->copy_stream)
     if (cs) {
@@ -1299,6 +1306,49 @@ int dev_accumulate_range(ipls_dev* h, int p, int target, const void* src, int64_
   return end_batch(h);
 }
 
+// One arrival produced by the caller chunk by chunk, as one call (Updater's
+// whole-bucket fold under PeerData.mtx, Updater.java:72-149, 115-117).  The
+// engine lock is held from the first source call to the fold's launch, so no
+// other caller's call on this shard lands inside the arrival -- the ordering
+// that per-range calls (dev_accumulate_range) cannot give.  Chunk k is filled
+// by source() into pinned slot k % 2 and sent to the device scratch by the
+// copy engine while the source fills chunk k + 1; the fold of the whole
+// bucket runs once every chunk has landed (one launch from HBM, 24 B per
+// element), so a source that stops leaves the target untouched.
+int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_kind, int64_t chunk,
+                           ipls_chunk_source source, void* ctx) {
+  if (!h || !source) return fail(h, IPLS_E_INVAL, "null argument");
+  if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
+  IPLS_LOCK(h);   // earlier queued device buckets fold first
+  if (int rc = check_part(h, p)) return rc;
+  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (src_kind != IPLS_HOST_F64 && src_kind != IPLS_HOST_BE)
+    return fail(h, IPLS_E_INVAL, "a chunked fold takes HOST_F64 or HOST_BE values, not kind %d", src_kind);
+  const int64_t L = h->len[p];
+  if (int rc = host_decode_count(src_kind, n, L, h)) return rc;   // before any source call
+  HIP_TRY(h, dev_use(h->device));
+  if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+  const int64_t c = std::min(chunk, L);
+  for (auto& sl : h->in_ring)
+    if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;
+  unsigned long long* d_in = (unsigned long long*)h->d_scratch;
+  for (int64_t k = 0, off = 0; off < L; ++k, off += c) {
+    PinnedSlot& sl = h->in_ring[k & 1];
+    if (sl.pending) {   // the copy of chunk k - 2 still reads this slot
+      HIP_TRY(h, hipEventSynchronize(sl.ev));
+      sl.pending = false;
+    }
+    const int64_t len = std::min(c, L - off);
+    if (source(ctx, sl.host, off, len) != 0)
+      return fail(h, IPLS_E_INVAL, "the chunk source stopped at offset %lld: nothing folded", (long long)off);
+    HIP_TRY(h, hipMemcpyAsync(d_in + off, sl.host, (size_t)len * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(sl.ev, h->stream));
+    sl.pending = true;
+  }
+  const void* bl[1] = {d_in};
+  return reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target);
+}
+
 // The reverse: target[off..off+n) of partition p into pinned host memory,
 // native or big-endian (putDouble order, as update_file writes it,
 // MyIPFSClass.java:105-116), asynchronous.  The JNI shim's byte[] outputs
@@ -1596,6 +1646,58 @@ int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_ou
       if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
       if (int rc = divide_range(h, p0, 1, (unsigned long long*)h->d_scratch, false)) return rc;
       if (int rc = d2h(h, avg_out, h->d_scratch, (size_t)(L - 1) * 8)) return rc;
+    }
+  }
+  return IPLS_OK;
+}
+
+// AggregatePartition of one partition with the commit_update bytes (or the
+// sum as doubles) handed to a sink chunk by chunk, as one call: W = AGG + REP,
+// then W comes back through the pinned two-slot ring, chunk k + 1 in flight
+// while sink() copies chunk k.  The engine lock spans the whole sequence, so
+// no set_weights / fold / finalize of another caller tears the bytes (the
+// per-range reads of dev_read_range cannot promise that).
+int dev_finalize_chunked(ipls_dev* h, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  if (!h || !sink) return fail(h, IPLS_E_INVAL, "null argument");
+  if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
+  IPLS_LOCK(h);
+  if (int rc = check_part(h, p)) return rc;
+  if (sum_kind != IPLS_HOST_F64 && sum_kind != IPLS_HOST_BE)
+    return fail(h, IPLS_E_INVAL, "sum_kind must be HOST_F64 or HOST_BE");
+  const int64_t L = h->len[p];
+  HIP_TRY(h, dev_use(h->device));
+  // every buffer first: a failure here leaves the round in place
+  if (sum_kind == IPLS_HOST_BE)
+    if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+  const int64_t c = std::min(chunk, L);
+  for (auto& sl : h->out_ring)
+    if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;
+  if (int rc = finalize_range(h, p, 1)) return rc;
+  const unsigned long long* w = (const unsigned long long*)(h->arena + h->w_off[p]);
+  if (sum_kind == IPLS_HOST_BE) {
+    launch_bswap(h->stream, w, (unsigned long long*)h->d_scratch, L);
+    HIP_TRY(h, hipGetLastError());
+    w = (const unsigned long long*)h->d_scratch;
+  }
+  const int64_t K = (L + c - 1) / c;
+  auto issue = [&](int64_t k) -> int {
+    PinnedSlot& sl = h->out_ring[k & 1];
+    const int64_t off = k * c, len = std::min(c, L - off);
+    HIP_TRY(h, hipMemcpyAsync(sl.host, w + off, (size_t)len * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipEventRecord(sl.ev, h->stream));
+    return IPLS_OK;
+  };
+  if (int rc = issue(0)) return rc;
+  for (int64_t k = 0; k < K; ++k) {
+    if (k + 1 < K)   // into the slot chunk k - 1 used, whose sink has returned
+      if (int rc = issue(k + 1)) return rc;
+    PinnedSlot& sl = h->out_ring[k & 1];
+    HIP_TRY(h, hipEventSynchronize(sl.ev));
+    const int64_t off = k * c, len = std::min(c, L - off);
+    if (sink(ctx, (const double*)sl.host, off, len) != 0) {
+      HIP_TRY(h, hipStreamSynchronize(h->stream));   // the copy still writing the other slot
+      return fail(h, IPLS_E_INVAL, "the chunk sink stopped the transfer at offset %lld (the round is consumed)",
+                  (long long)off);
     }
   }
   return IPLS_OK;

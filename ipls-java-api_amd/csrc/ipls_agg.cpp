@@ -632,6 +632,27 @@ int ipls_agg_accumulate_range(ipls_agg* H, int p, int target, const void* src, i
   return IPLS_OK;
 }
 
+// The chunked calls run entirely on p's shard, on the calling thread (the
+// source / sink are the caller's code and must run there).
+int ipls_agg_accumulate_chunked(ipls_agg* H, int p, int target, int64_t n, int src_kind, int64_t chunk,
+                                ipls_chunk_source source, void* ctx) {
+  KeepDevice keep_device;
+  if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
+  if (!part_ok(H, p)) return range_err(H, p);
+  int q;
+  const int s = route(H, p, &q);
+  return fwd(H, s, dev_accumulate_chunked(H->sh[s], q, target, n, src_kind, chunk, source, ctx));
+}
+
+int ipls_agg_finalize_chunked(ipls_agg* H, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  KeepDevice keep_device;
+  if (!H) return ferr(nullptr, IPLS_E_INVAL, "null handle");
+  if (!part_ok(H, p)) return range_err(H, p);
+  int q;
+  const int s = route(H, p, &q);
+  return fwd(H, s, dev_finalize_chunked(H->sh[s], q, sum_kind, chunk, sink, ctx));
+}
+
 int ipls_agg_read_range(ipls_agg* H, int p, int target, void* dst, int64_t offset, int64_t n, int dst_kind,
                         uint64_t* ticket) {
   KeepDevice keep_device;

@@ -25,13 +25,15 @@ HOST_F64, HOST_BE, HOST_FRAME, DEV_F64, DEV_BE, HOST_BE_CANON, HOST_PAIR = 0, 1,
 HOST_TEXT, DEV_TEXT = 7, 8
 KERNEL_REDUCE, KERNEL_ROUND, KERNEL_FOLD1, KERNEL_REDUCE_SCALAR = 1, 2, 3, 4
 SHAPE_BIG, SHAPE_MID, SHAPE_SMALL, SHAPE_HALF = 1, 2, 3, 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 START_ACCUM, START_ZERO, START_FIRST = 0, 1, 2
 ALL_PARTITIONS = -1
 
 # ipls_chunk_sink: int (*)(void *ctx, const double *values, int64_t offset, int64_t n)
 CHUNK_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64,
                               ctypes.c_int64)
+# ipls_chunk_source: int (*)(void *ctx, void *dst, int64_t offset, int64_t n)
+CHUNK_SOURCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64)
 
 ERROR_NAMES = {
     IPLS_E_INVAL: "IllegalArgument",
@@ -104,6 +106,8 @@ SIGNATURES = {
     "ipls_agg_read_range": (_i, [_vp, _i, _i, _vp, _i64, _i64, _i, _P(_u64)]),
     "ipls_agg_flat_size": (_i, [_vp, _P(_i64)]),
     "ipls_agg_get_partitions_chunked": (_i, [_vp, _i64, _vp, _vp]),   # sink: a CHUNK_SINK instance
+    "ipls_agg_accumulate_chunked": (_i, [_vp, _i, _i, _i64, _i, _i64, _vp, _vp]),   # source: a CHUNK_SOURCE
+    "ipls_agg_finalize_chunked": (_i, [_vp, _i, _i, _i64, _vp, _vp]),   # sink: a CHUNK_SINK instance
     "ipls_agg_wait": (_i, [_vp, _u64]),
     "ipls_agg_set_coalesce": (_i, [_vp, _i]),
     "ipls_agg_flush": (_i, [_vp]),

@@ -530,11 +530,21 @@ class Aggregator:
 
     def GetPartitions(self, *, wire: bool = False, out=None):
         """IPLS.java:1140-1174: the averaged flat model.  ``wire=True`` returns
-        the Middleware task-3 byte stream (DataOutputStream.writeDouble)."""
+        the Middleware task-3 byte stream (DataOutputStream.writeDouble);
+        with ``out`` a PinnedBuffer it is written there (the D2H at the PCIe
+        rate) and a memoryview of those 8*M bytes is returned, ready for
+        ``sendall`` without another copy."""
         n = self.flat_size
         if isinstance(out, DeviceBuffer):
             self._chk(self._lib.ipls_agg_get_partitions(self._h, out.ptr, out.n, N.DEV_F64))
             return out
+        if isinstance(out, PinnedBuffer):
+            if out.nbytes < 8 * n:
+                raise ValueError(f"PinnedBuffer of {out.nbytes} bytes < the model's {8 * n}")
+            kind = N.HOST_BE_CANON if wire else N.HOST_F64
+            self._chk(self._lib.ipls_agg_get_partitions(self._h, out.ptr, n, kind))
+            v = out.view()[:8 * n]
+            return memoryview(v) if wire else v.view(np.float64)
         if wire:
             buf = np.empty(8 * n, dtype=np.uint8)
             self._chk(self._lib.ipls_agg_get_partitions(self._h, buf.ctypes.data, n, N.HOST_BE_CANON))

@@ -185,9 +185,13 @@ class LoopbackAggregator:
                 self.pending = 0
                 self.rounds += 1
 
-    def get_partitions_wire(self) -> bytes:
+    def get_partitions_wire(self) -> memoryview:
+        """Task 3: GetPartitions' writeDouble stream, written by the divide
+        kernel's big-endian output (NaN canonicalised) into the pinned staging
+        and handed to ``sendall`` from there.  The view is valid until the
+        next task 2 lands in the same staging (the server is sequential)."""
         with self.lock:
-            return self.agg.GetPartitions(wire=True)
+            return self.agg.GetPartitions(wire=True, out=self.staging)
 
     def close(self):
         self.agg.close()
@@ -195,12 +199,15 @@ class LoopbackAggregator:
 
 
 def serve(opts: Options, max_connections: int | None = None, device: int = 0, initial_model=None,
-          ready: threading.Event | None = None, host: str = "127.0.0.1"):
-    """Middleware.main (Middleware.java:212-268): one connection per task."""
+          ready: threading.Event | None = None, host: str = "127.0.0.1", on_listen=None):
+    """Middleware.main (Middleware.java:212-268): one connection per task.
+    ``opts.port`` 0 binds a free port; ``on_listen(port)`` is told which."""
     srv = socket.socket()
     srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     srv.bind((host, opts.port))
     srv.listen(16)
+    if on_listen is not None:
+        on_listen(srv.getsockname()[1])
     if ready is not None:
         ready.set()
     daemon = None

@@ -73,23 +73,20 @@ void IPLS_JNI_CALL_HOOK(const char *call);
 /* ---- per-thread staging for heap arrays ----
  * Two slots per thread, each grown to the largest array that thread has
  * passed so far and kept for reuse (no allocation and no page faults per
- * call); freed when the thread ends.  Plain malloc'd memory: pinned slots
- * (ipls_host_alloc) measured no faster as whole-array copies -- the
- * Get/Set<T>ArrayRegion copy bounds a heap-array call either way
- * (tools/jni_heap_probe.py, profiles/r04/i/: accumulate(double[]) 21.8 GB/s
- * pinned vs 21.4 pageable, finalize 15.0 vs 19.0; direct buffers 52-55 GB/s).
- * What does help is overlapping that copy with the fold: large double[]
- * arrivals go chunk by chunk through a pinned two-slot ring (ring_slot,
- * accumulate below). */
-struct stage { void *p[2]; size_t cap[2]; void *ring[2]; };
+ * call); freed when the thread ends.  The two hot heap-array natives,
+ * accumulate(double[]) and finalizePartition(byte[]), need no staging here:
+ * the library calls back into the shim for each chunk
+ * (ipls_agg_accumulate_chunked / ipls_agg_finalize_chunked), which copies it
+ * between the Java array and the library's pinned ring while the previous
+ * chunk is on the bus -- one library call per Java call, so the whole
+ * arrival (or AggregatePartition plus its bytes) is one ordered unit. */
+struct stage { void *p[2]; size_t cap[2]; };
 static pthread_key_t g_stage_key;
 static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
 static void stage_free(void *v) {
     struct stage *st = (struct stage *)v;
     free(st->p[0]);
     free(st->p[1]);
-    for (int i = 0; i < 2; ++i)
-        if (st->ring[i]) (void)LIB(ipls_host_free(st->ring[i]));
     free(st);
 }
 static void stage_init(void) { (void)pthread_key_create(&g_stage_key, stage_free); }
@@ -117,24 +114,8 @@ static void *stage(JNIEnv *env, int slot, size_t bytes) {
     return st->p[slot];
 }
 
-/* The pinned ring of the pipelined double[] fold (accumulate below): two
- * slots of RING_CHUNK doubles per thread, pinned once (ipls_host_alloc) so
- * the library folds each chunk straight from them over PCIe.  NULL with an
- * OutOfMemoryError pending. */
-#define RING_CHUNK ((jsize)1 << 19)   /* doubles per slot: 4 MiB */
-static double *ring_slot(JNIEnv *env, int slot) {
-    if (!stage(env, slot, 1)) return NULL;   /* the per-thread record */
-    struct stage *st = (struct stage *)pthread_getspecific(g_stage_key);
-    if (!st->ring[slot]) {
-        void *q = NULL;
-        if (LIB(ipls_host_alloc((size_t)RING_CHUNK * 8, &q)) < 0 || !q) {
-            throw_msg(env, "java/lang/OutOfMemoryError", "JNI pinned staging ring");
-            return NULL;
-        }
-        st->ring[slot] = q;
-    }
-    return (double *)st->ring[slot];
-}
+/* Values per chunk of the chunked natives: 4 MiB. */
+#define RING_CHUNK ((jsize)1 << 19)
 
 /* A copy of the whole double[] / byte[] in staging slot `slot`. */
 static void *copy_doubles(JNIEnv *env, jdoubleArray a, jsize n, int slot) {
@@ -315,44 +296,30 @@ JNIEXPORT void JNICALL Java_NativeAggregator_updateGradient(JNIEnv *env, jclass 
     CHECK(rc, H(h));
 }
 
+/* The chunk source of accumulate(double[]): the library asks for the
+ * bucket's values [off, off + n) and the shim copies them out of the heap. */
+struct heap_source { JNIEnv *env; jdoubleArray a; };
+static int heap_source_fn(void *ctx, void *dst, int64_t off, int64_t n) {
+    struct heap_source *s = (struct heap_source *)ctx;
+    (*s->env)->GetDoubleArrayRegion(s->env, s->a, (jsize)off, (jsize)n, (jdouble *)dst);
+    return (*s->env)->ExceptionCheck(s->env) ? 1 : 0;
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
                                                           jdoubleArray g) {
     (void)c;
     if (!g) return;   /* Gradient == null: the Updater loops do nothing (Updater.java:115) */
-    jsize n = (*env)->GetArrayLength(env, g);
-    int64_t L = 0;
-    if (n >= 2 * RING_CHUNK && LIB(ipls_agg_partition_len(H(h), p, &L)) == 0 && L >= 2 * RING_CHUNK && L <= n) {
-        /* Pipelined: chunk k is copied out of the heap (GetDoubleArrayRegion)
-         * into ring slot k % 2 while chunk k - 1 folds from the other slot
-         * (ipls_agg_accumulate_range, zero copy).  Each element of the
-         * bucket's first L is added once, in order: the whole-bucket bits.
-         * Both slots exist before the first fold, so an OutOfMemoryError
-         * leaves the target unchanged. */
-        if (!ring_slot(env, 0) || !ring_slot(env, 1)) return;
-        uint64_t tk[2] = {0, 0};
-        int used[2] = {0, 0}, rc = 0;
-        for (int64_t off = 0, k = 0; off < L; off += RING_CHUNK, ++k) {
-            const int s = (int)(k & 1);
-            const jsize len = (jsize)(L - off < RING_CHUNK ? L - off : RING_CHUNK);
-            if (used[s] && (rc = LIB(ipls_agg_wait(H(h), tk[s]))) < 0) break;
-            used[s] = 0;
-            double *buf = ring_slot(env, s);
-            (*env)->GetDoubleArrayRegion(env, g, (jsize)off, len, buf);
-            if ((*env)->ExceptionCheck(env)) { rc = 1; break; }
-            if ((rc = LIB(ipls_agg_accumulate_range(H(h), p, tgt, buf, off, len, IPLS_HOST_F64, &tk[s]))) < 0) break;
-            used[s] = 1;
-        }
-        for (int s = 0; s < 2; ++s)   /* the folds still reading the ring, after an error too */
-            if (used[s]) {
-                const int w = LIB(ipls_agg_wait(H(h), tk[s]));
-                if (rc == 0 && w < 0) rc = w;
-            }
-        if (rc < 0) throw_for(env, rc, H(h));
-        return;
-    }
-    void *src = copy_doubles(env, g, n, 0);
-    if (!src) return;
-    CHECK(LIB(ipls_agg_accumulate(H(h), p, tgt, src, n, IPLS_HOST_F64)), H(h));
+    /* One call for the whole arrival (Updater._Update under PeerData.mtx,
+     * Updater.java:72-149): the library pulls the bucket's first L values
+     * chunk by chunk through heap_source_fn (GetDoubleArrayRegion into its
+     * pinned ring) while the previous chunk crosses PCIe, then folds the
+     * bucket in one launch.  No other caller's call on the partition's GPU
+     * lands inside it, a short array is ArrayIndexOutOfBoundsException before
+     * any copy, and a failed copy folds nothing. */
+    struct heap_source hs = {env, g};
+    const jsize n = (*env)->GetArrayLength(env, g);
+    const int rc = LIB(ipls_agg_accumulate_chunked(H(h), p, tgt, n, IPLS_HOST_F64, RING_CHUNK, heap_source_fn, &hs));
+    if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_for(env, rc, H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_accumulateDirect(JNIEnv *env, jclass c, jlong h, jint p, jint tgt,
@@ -455,57 +422,31 @@ out:
     return rc;
 }
 
+/* The chunk sink of finalizePartition(byte[]): the commit_update bytes of
+ * values [off, off + n) straight from the library's pinned ring into the array. */
+struct bytes_sink { JNIEnv *env; jbyteArray out; };
+static int bytes_sink_fn(void *ctx, const double *values, int64_t off, int64_t n) {
+    struct bytes_sink *b = (struct bytes_sink *)ctx;
+    (*b->env)->SetByteArrayRegion(b->env, b->out, (jsize)(8 * off), (jsize)(8 * n), (const jbyte *)values);
+    return (*b->env)->ExceptionCheck(b->env) ? 1 : 0;
+}
+
 JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jclass c, jlong h, jint p,
                                                                  jbyteArray sum) {
     (void)c;
-    if (sum) {
-        const int64_t L = part_len(env, h, p);
-        if (L < 0 || !need_len(env, sum, 8 * L, "commit_update bytes")) return;
-    }
-    int64_t L = 0;
-    if (sum && LIB(ipls_agg_partition_len(H(h), p, &L)) < 0) { throw_for(env, IPLS_E_RANGE, H(h)); return; }
-    if (sum && L >= 2 * RING_CHUNK) {
-        /* Pipelined: AggregatePartition on the device, then the commit_update
-         * bytes of W in ring-sized chunks (ipls_agg_read_range, big-endian,
-         * into the pinned ring): chunk k is copied into the byte[] while
-         * chunk k + 1 is still coming back.  Both slots exist before the
-         * round is consumed, so an OutOfMemoryError leaves it in place. */
-        if (!ring_slot(env, 0) || !ring_slot(env, 1)) return;
-        int rc = LIB(ipls_agg_finalize(H(h), p, NULL, IPLS_HOST_BE, NULL));
-        if (rc < 0) { throw_for(env, rc, H(h)); return; }
-        const int64_t K = (L + RING_CHUNK - 1) / RING_CHUNK;   /* >= 2 */
-        uint64_t tk[2] = {0, 0};
-        int live[2] = {0, 0};
-        rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, ring_slot(env, 0), 0, RING_CHUNK, IPLS_HOST_BE, &tk[0]));
-        live[0] = rc >= 0;
-        for (int64_t k = 0; k < K && rc >= 0; ++k) {
-            const int s = (int)(k & 1), t = 1 - s;
-            if (k + 1 < K) {   /* chunk k + 1 into the other slot (its chunk k - 1 is already out) */
-                const int64_t off = (k + 1) * RING_CHUNK, len = L - off < RING_CHUNK ? L - off : RING_CHUNK;
-                if ((rc = LIB(ipls_agg_read_range(H(h), p, IPLS_TGT_WEIGHTS, ring_slot(env, t), off, len, IPLS_HOST_BE,
-                                                  &tk[t]))) < 0)
-                    break;
-                live[t] = 1;
-            }
-            if ((rc = LIB(ipls_agg_wait(H(h), tk[s]))) < 0) break;
-            live[s] = 0;
-            const int64_t off = k * RING_CHUNK, len = L - off < RING_CHUNK ? L - off : RING_CHUNK;
-            (*env)->SetByteArrayRegion(env, sum, (jsize)(8 * off), (jsize)(8 * len), (const jbyte *)ring_slot(env, s));
-            if ((*env)->ExceptionCheck(env)) { rc = 1; break; }
-        }
-        for (int s = 0; s < 2; ++s)   /* reads still writing the ring, after an error too */
-            if (live[s]) {
-                const int w = LIB(ipls_agg_wait(H(h), tk[s]));
-                if (rc == 0 && w < 0) rc = w;
-            }
-        if (rc < 0) throw_for(env, rc, H(h));
+    if (!sum) {
+        CHECK(LIB(ipls_agg_finalize(H(h), p, NULL, IPLS_HOST_BE, NULL)), H(h));
         return;
     }
-    jbyte *dst = sum ? (jbyte *)stage(env, 0, (size_t)L * 8) : NULL;
-    if (sum && !dst) return;
-    int rc = LIB(ipls_agg_finalize(H(h), p, dst, IPLS_HOST_BE, NULL));
-    if (sum && rc >= 0) (*env)->SetByteArrayRegion(env, sum, 0, (jsize)(8 * L), dst);
-    CHECK(rc, H(h));
+    const int64_t L = part_len(env, h, p);
+    if (L < 0 || !need_len(env, sum, 8 * L, "commit_update bytes")) return;
+    /* One call: AggregatePartition on the device, then W's big-endian bytes
+     * come back chunk by chunk through the library's pinned ring, each
+     * copied into the byte[] while the next is in flight.  No set_weights or
+     * finalize of another thread can land between the sum and its bytes. */
+    struct bytes_sink bs = {env, sum};
+    const int rc = LIB(ipls_agg_finalize_chunked(H(h), p, IPLS_HOST_BE, RING_CHUNK, bytes_sink_fn, &bs));
+    if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_for(env, rc, H(h));
 }
 
 JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartitionDirect(JNIEnv *env, jclass c, jlong h, jint p,

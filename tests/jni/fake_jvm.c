@@ -19,13 +19,20 @@
  *     built with -DIPLS_JNI_CALL_HOOK=fj_library_call, reports every library
  *     call here): such a call may wait on the GPU, and a real JVM cannot
  *     collect garbage while a critical region is held.
+ * It can also start a second "Java thread" in the middle of a native
+ * (fj_inject): a library call on the same handle made between two chunks of
+ * a chunked native, to show whether the native's work is one ordered unit.
  * tests/test_jni.py drives it through ctypes.
  */
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
+#include "ipls_agg.h"
 #include "jni.h"
 
 enum { K_BYTES = 1, K_INTS, K_LONGS, K_DOUBLES, K_OBJECTS, K_DIRECT, K_CLASS };
@@ -187,8 +194,11 @@ static void JNICALL ReleaseLongArrayElements(JNIEnv *env, jlongArray a, jlong *e
     release(a, K_LONGS, "ReleaseLongArrayElements");
 }
 
+static void inject_tick(void);
+
 static void region(jarray a, int kind, jsize start, jsize len, const void *buf, const char *fn) {
     guarded_call(fn);
+    inject_tick();
     if (!a || a->kind != kind || start < 0 || len < 0 || start + len > a->n) {
         violation(fn);   /* a JVM throws ArrayIndexOutOfBoundsException here */
         return;
@@ -210,6 +220,7 @@ static void JNICALL SetDoubleArrayRegion(JNIEnv *env, jdoubleArray a, jsize s, j
 
 static void region_out(jarray a, int kind, jsize start, jsize len, void *buf, const char *fn) {
     guarded_call(fn);
+    inject_tick();
     if (!a || a->kind != kind || start < 0 || len < 0 || start + len > a->n) {
         violation(fn);   /* a JVM throws ArrayIndexOutOfBoundsException here */
         return;
@@ -223,6 +234,81 @@ static void JNICALL GetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize s, jsize
 static void JNICALL GetDoubleArrayRegion(JNIEnv *env, jdoubleArray a, jsize s, jsize l, jdouble *b) {
     (void)env;
     region_out(a, K_DOUBLES, s, l, b, "GetDoubleArrayRegion");
+}
+
+/* ---- a second Java thread inside a native ----
+ * fj_inject arms a one-shot.  At the `after`-th array-region copy
+ * (Get/Set<T>ArrayRegion) from then on -- inside a chunked native, that is
+ * between two chunks of its library call -- a second thread calls the
+ * library on the same handle by itself:
+ *   op 0: ipls_agg_accumulate(h, p, tgt, src, n, IPLS_HOST_F64)
+ *         (another Updater arrival into the same partition),
+ *   op 1: ipls_agg_set_weights(h, p, src, n, IPLS_HOST_F64)
+ *         (Download_Scheduler.cache_partition on the same partition).
+ * The copy that triggered it waits until the thread has started and then
+ * `window_ms` more before it returns to the shim.  fj_inject_state: 0 not
+ * triggered, 1 the thread's call had returned inside the window (it ran in
+ * the middle of the native's work), 2 it was still waiting at the end of
+ * the window (ordered after the native's call).  fj_inject_join waits for
+ * the thread and returns its library return code.  src stays the caller's. */
+struct inject {
+    int armed, after, ticks, op, window_ms, state;
+    ipls_agg *h;
+    int p, tgt;
+    const double *src;
+    int64_t n;
+    pthread_t th;
+    int started_th;
+    volatile int started, done, rc;
+};
+static struct inject g_inj;
+
+static void *inject_run(void *arg) {
+    struct inject *j = (struct inject *)arg;
+    __atomic_store_n(&j->started, 1, __ATOMIC_SEQ_CST);
+    int rc = j->op == 0 ? ipls_agg_accumulate(j->h, j->p, j->tgt, j->src, j->n, IPLS_HOST_F64)
+                        : ipls_agg_set_weights(j->h, j->p, j->src, j->n, IPLS_HOST_F64);
+    j->rc = rc;
+    __atomic_store_n(&j->done, 1, __ATOMIC_SEQ_CST);
+    return NULL;
+}
+
+static void sleep_ms(int ms) {
+    struct timespec t = {ms / 1000, (long)(ms % 1000) * 1000000L};
+    while (nanosleep(&t, &t) != 0) {}
+}
+
+static void inject_tick(void) {
+    if (!g_inj.armed || ++g_inj.ticks < g_inj.after) return;
+    g_inj.armed = 0;
+    if (pthread_create(&g_inj.th, NULL, inject_run, &g_inj) != 0) {
+        violation("fj_inject: pthread_create failed");
+        return;
+    }
+    g_inj.started_th = 1;
+    while (!__atomic_load_n(&g_inj.started, __ATOMIC_SEQ_CST)) sleep_ms(1);
+    sleep_ms(g_inj.window_ms);
+    g_inj.state = __atomic_load_n(&g_inj.done, __ATOMIC_SEQ_CST) ? 1 : 2;
+}
+
+JNIEXPORT void fj_inject(int op, int after, int window_ms, jlong h, int p, int tgt, const double *src, int64_t n) {
+    memset(&g_inj, 0, sizeof g_inj);
+    g_inj.op = op;
+    g_inj.after = after;
+    g_inj.window_ms = window_ms;
+    g_inj.h = (ipls_agg *)(intptr_t)h;
+    g_inj.p = p;
+    g_inj.tgt = tgt;
+    g_inj.src = src;
+    g_inj.n = n;
+    g_inj.armed = 1;
+}
+JNIEXPORT int fj_inject_state(void) { return g_inj.state; }
+JNIEXPORT int fj_inject_join(void) {
+    if (!g_inj.started_th) return 1;   /* never triggered */
+    pthread_join(g_inj.th, NULL);
+    g_inj.started_th = 0;
+    return g_inj.rc;
 }
 
 /* The shim's report of a call into libipls_agg (IPLS_JNI_CALL_HOOK). */

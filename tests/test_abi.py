@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for s in declared_symbols():
         assert hasattr(L, s), f"{s} declared in include/ipls_agg.h but not exported"
         assert s in N.SIGNATURES, f"{s} has no ctypes signature"
-    assert L.ipls_agg_abi_version() == N.ABI_VERSION == 3
+    assert L.ipls_agg_abi_version() == N.ABI_VERSION == 4
 
 
 def test_header_constants_match_binding():
@@ -203,7 +203,7 @@ def test_ctypes_signatures_match_the_header():
             continue
         for i, (c, a) in enumerate(zip(params, args)):
             ctype = re.sub(r"\b\w+$", "", c).strip() if re.search(r"[*\s]\w+$", c) else c   # drop the name
-            if ctype == "ipls_chunk_sink":                # a function pointer: travels as void*
+            if ctype in ("ipls_chunk_sink", "ipls_chunk_source"):   # a function pointer: travels as void*
                 if a is not ctypes.c_void_p:
                     bad.append(f"{name} arg {i}: C '{c}' bound {a}")
                 continue

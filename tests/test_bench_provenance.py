@@ -138,3 +138,22 @@ def test_pmc_tool_stores_nothing_without_a_build(tmp_path):
                         str(out)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert not out.exists() and "not stored" in r.stderr
+
+
+def test_bench_line_ends_with_the_proof(bench):
+    """the driver keeps only the tail of stdout, so the
+    line's last keys are `verified`, `verified_partitions` and `build`, and
+    `build` ends with the library's identity and sources_match -- whatever
+    order the legs were added in."""
+    line = {"metric": "m", "value": 1.0, "verified": True, "verified_partitions": "16/16",
+            "build": {"sources_match": True, "so_sha256": "s", "git_rev": "g", "device_code_sha256": "d",
+                      "stamp_matches_so": True, "built_utc": "t", "kernel_src_sha256": "k"},
+            "roofline": {"frac": 0.88, "traffic_provenance": {"x": 1}}, "round": {"a": 1}, "few_partitions": {"b": 2}}
+    out = bench.proof_last(line)
+    assert list(out)[-3:] == ["verified", "verified_partitions", "build"]
+    assert list(out["build"])[-5:] == ["so_sha256", "device_code_sha256", "built_utc", "stamp_matches_so",
+                                       "sources_match"]
+    assert out["roofline"] == line["roofline"] and set(out) == set(line)
+    text = json.dumps(out)
+    assert text.endswith('"sources_match": true}}')
+    assert '"verified_partitions": "16/16"' in text[-600:]

@@ -1073,6 +1073,120 @@ def test_read_range(ipls, O, devices):
     pin.close()
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_accumulate_chunked(ipls, O, devices):
+    """ipls_agg_accumulate_chunked: one arrival pulled from a caller source
+    chunk by chunk, as one call (Updater._Update's whole-bucket fold,
+    Updater.java:115-117).  The source is asked for consecutive ranges that
+    tile [0, L) exactly (never past L, even when the caller's bucket is
+    longer), and the bits equal the oracle's whole-bucket folds: native and
+    big-endian values, a logically-zero target and a live one, AGG and REP,
+    chunks of 2 values, an odd chunk count and one chunk larger than L.  A
+    short bucket is IPLS_E_RANGE before any source call; a source that stops
+    folds nothing (all or nothing); an odd chunk is refused."""
+    from ipls import _native as N
+    L = 300007
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    acc = {0: np.zeros(L), 1: np.zeros(L)}
+    for k, (tgt, be, chunk, extra) in enumerate(((0, False, 65536, 0), (0, True, 100002, 9), (1, False, 1 << 22, 0),
+                                                   (1, True, 65536, 0), (0, False, 2, 0))):
+        g = O.synth_bucket(L + extra, 1, 70 + k) * 10.0 ** (k - 2)
+        g[::997] = -0.0
+        raw = np.frombuffer(O.be_encode(g) if be else g.tobytes(), dtype=np.uint8)
+        seen = []
+
+        @N.CHUNK_SOURCE
+        def src(ctx, dst, off, n):
+            seen.append((off, n))
+            ctypes.memmove(dst, raw.ctypes.data + 8 * off, 8 * n)
+            return 0
+        kind = N.HOST_BE if be else N.HOST_F64
+        assert lib.ipls_agg_accumulate_chunked(h, 1, tgt, L + extra, kind, chunk, src, None) == 0
+        assert [o for o, _ in seen] == list(range(0, L, min(chunk, L))), "consecutive chunks"
+        assert sum(n for _, n in seen) == L and all(n <= chunk for _, n in seen)
+        acc[tgt] = O.fold(acc[tgt], g[:L])
+        assert_bits_equal(agg.read(1, tgt), acc[tgt], f"chunked fold {k}")
+    calls = []
+
+    @N.CHUNK_SOURCE
+    def stop(ctx, dst, off, n):
+        calls.append(off)
+        ctypes.memset(dst, 0x7F, 8 * n)            # garbage that must never be folded
+        return 1 if len(calls) == 3 else 0
+    assert lib.ipls_agg_accumulate_chunked(h, 1, 0, L, N.HOST_F64, 65536, stop, None) == N.IPLS_E_INVAL
+    assert calls == [0, 65536, 131072]
+    assert lib.ipls_agg_accumulate_chunked(h, 0, 0, L, N.HOST_F64, 65536, stop, None) == N.IPLS_E_INVAL
+    calls.clear()
+    assert lib.ipls_agg_accumulate_chunked(h, 1, 0, L - 1, N.HOST_F64, 65536, stop, None) == N.IPLS_E_RANGE
+    assert lib.ipls_agg_accumulate_chunked(h, 1, 0, L, N.HOST_F64, 65537, stop, None) == N.IPLS_E_INVAL
+    assert lib.ipls_agg_accumulate_chunked(h, 1, 0, L, N.DEV_F64, 65536, stop, None) == N.IPLS_E_INVAL
+    assert calls == [], "refused before any source call"
+    assert_bits_equal(agg.read(1, 0), acc[0], "a stopped source folded nothing")
+    assert_bits_equal(agg.read(0, 0), np.zeros(L), "partition 0 untouched (logically zero)")
+    agg.Update(np.ones(L), 0)                       # partition 0 is still a +0.0 start
+    assert_bits_equal(agg.read(0, 0), O.fold(np.zeros(L), np.ones(L)), "p0 after the stopped source")
+    agg.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_finalize_chunked(ipls, O, devices):
+    """ipls_agg_finalize_chunked: AggregatePartition (W = AGG + REP,
+    IPLS.java:1248-1274) with W handed to a sink chunk by chunk, as one call:
+    the commit_update bytes (big-endian) or doubles equal the oracle's, for
+    several chunk sizes; a sink that stops gets IPLS_E_INVAL after the round
+    is consumed; an odd chunk or a bad kind is refused with the round left in
+    place."""
+    from ipls import _native as N
+    L = 200003
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    for k, (kind, chunk) in enumerate(((N.HOST_BE, 65536), (N.HOST_F64, 100002), (N.HOST_BE, 1 << 22), (N.HOST_BE, 2))):
+        a, r = O.synth_bucket(L, 1, 80 + k), O.synth_bucket(L, 1, 90 + k) * 3.0
+        agg.Update(a, 1)
+        agg.Update(r, 1, from_clients=False)
+        if k == 0:   # refused calls leave the round in place
+            assert lib.ipls_agg_finalize_chunked(h, 1, N.HOST_BE, 65537, N.CHUNK_SINK(lambda *x: 0), None) == N.IPLS_E_INVAL
+            assert lib.ipls_agg_finalize_chunked(h, 1, N.DEV_F64, 65536, N.CHUNK_SINK(lambda *x: 0), None) == N.IPLS_E_INVAL
+            assert lib.ipls_agg_finalize_chunked(h, 2, N.HOST_BE, 65536, N.CHUNK_SINK(lambda *x: 0), None) == N.IPLS_E_RANGE
+        out = bytearray(8 * L)
+        seen = []
+
+        @N.CHUNK_SINK
+        def sink(ctx, vals, off, n):
+            seen.append((off, n))
+            out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+            return 0
+        if chunk == 2:                                   # 100,002 sink calls: keep them cheap
+            @N.CHUNK_SINK
+            def sink(ctx, vals, off, n):                 # noqa: F811
+                seen.append((off, n))
+                if off < 4096 or off > L - 4096:
+                    out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+                return 0
+        assert lib.ipls_agg_finalize_chunked(h, 1, kind, chunk, sink, None) == 0
+        assert [o for o, _ in seen] == list(range(0, L, min(chunk, L))) and sum(n for _, n in seen) == L
+        w = O.fold(np.zeros(L), a) + O.fold(np.zeros(L), r)
+        want = O.be_encode(w) if kind == N.HOST_BE else w.tobytes()
+        if chunk == 2:
+            assert out[:8 * 4096] == want[:8 * 4096] and out[-8 * 4000:] == want[-8 * 4000:]
+        else:
+            assert bytes(out) == want, f"finalize chunked {k}"
+        assert_bits_equal(agg.read(1, ipls.TGT_AGG), np.zeros(L), "AGG zeroed")
+    a = O.synth_bucket(L, 1, 99)
+    agg.Update(a, 1)
+    calls = []
+
+    @N.CHUNK_SINK
+    def stop(ctx, vals, off, n):
+        calls.append(off)
+        return 1
+    assert lib.ipls_agg_finalize_chunked(h, 1, N.HOST_BE, 65536, stop, None) == N.IPLS_E_INVAL
+    assert calls == [0]
+    assert_bits_equal(agg.read(1, ipls.TGT_WEIGHTS), O.fold(np.zeros(L), a) + 0.0, "the round is consumed")
+    agg.close()
+
+
 def test_encode_secure_device(ipls, O, golden):
     x = golden["enc_in"]
     t, d = dev(x)
