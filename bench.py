@@ -63,6 +63,8 @@ def parse():
                          "(fused unpack + pack, config D's timed pack/unpack)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-inclusive (H2D+D2H) leg")
     ap.add_argument("--e2e-reps", type=int, default=4)
+    ap.add_argument("--no-middleware", action="store_true",
+                    help="N=1: skip the Middleware loopback-socket leg (task 2 x 32 + task 3 at model scale)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-passes", type=int, default=16,
                     help="CPU baseline sample: passes over one partition's K buckets")
@@ -325,6 +327,159 @@ def f_stream_leg(ipls, torch, device: int, P: int = 16, L: int = 8388608, K: int
                     f"a direct ByteBuffer); per arrival one ipls_agg_accumulate_async zero-copy fold over PCIe, "
                     f"<= {lag + 1} folds in flight; per partition ipls_agg_finalize with the BE sum into pinned "
                     f"memory; Python caller"}
+
+
+def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 4194303, K: int = 32, D: int = 4,
+                          verify: bool = True) -> dict:
+    """The north_star's host boundary at model scale: the Middleware loopback
+    socket (Middleware.java:212-268) carrying K task-2 updates of M = P x Lv
+    doubles (Deserialize, :156-160, 537 MB each) and one task-3 reply
+    (Serialize, :164-170), through ipls.middleware.serve on TCP 127.0.0.1.
+
+    Server (ipls.middleware.LoopbackAggregator, -pa P -n K): each task-2
+    update is UpdateGradient over every partition (IPLS.java:1737-1743),
+    streamed: partition p's slice is one ipls_agg_accumulate_chunked call
+    whose source receives each 4 MiB chunk straight into the library's
+    pinned ring, so the H2D copy of a chunk overlaps the receive of the next
+    and the BE decode is fused into the fold; after K updates the round
+    closes (AggregatePartition for every p, IPLS.java:1248-1274).  Task 3 is
+    GetPartitions (IPLS.java:1159-1174): the divide kernel writes the
+    writeDouble stream (big-endian, NaN canonical) and
+    ipls_agg_get_partitions_wire_chunked hands it to sendall() chunk by chunk
+    from the pinned ring.  Client: the Python IPLS API's side, one
+    connection per task (D distinct update vectors cycled).
+
+    Ceiling: the same client against a server that receives each payload into
+    one pinned buffer and answers task 3 from it, with no aggregator --
+    the loopback socket alone, measured in the same process.  Two rounds:
+    the first (cold: first-use allocations) is reported beside the second.
+    The reply is checked byte for byte against the oracle's writeDouble
+    stream of the fixed-order average ((((+0.0 + u_0) + u_1) ...) + 0.0) / K."""
+    import socket
+    import struct
+    import threading
+    from ipls import middleware as MW
+    M = P * Lv
+    nbytes = 8 * M
+    t_prep = time.perf_counter()
+    ups = []
+    tmp = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", device))
+    for d in range(D):
+        ipls.synth_fill(ipls.DeviceBuffer(int(tmp.data_ptr()), M, big_endian=True), 200 + d, 0, ipls.SEED)
+        torch.cuda.synchronize()
+        ups.append(tmp.cpu().numpy())
+    del tmp
+    reply = np.empty(nbytes, dtype=np.uint8)
+    reply[::4096] = 0
+    prep_s = time.perf_counter() - t_prep
+    hdr2, hdr3 = struct.pack(">h", 2), struct.pack(">h", 3)
+
+    def task(port, hdr, payload, n_reply, into=None):
+        with socket.create_connection(("127.0.0.1", port)) as s:
+            s.sendall(hdr)
+            if payload is not None:
+                s.sendall(memoryview(payload))
+            return MW._recv_exact(s, n_reply, into)
+
+    def one_round(port):
+        """K task 2 + one task 3; per-task client wall times."""
+        t2 = []
+        t0 = time.perf_counter()
+        for k in range(K):
+            a = time.perf_counter()
+            assert bytes(task(port, hdr2, ups[k % D], 2)) == MW.ACK
+            t2.append(time.perf_counter() - a)
+        a = time.perf_counter()
+        task(port, hdr3, None, nbytes, reply)
+        t3 = time.perf_counter() - a
+        return time.perf_counter() - t0, t2, t3
+
+    def summary(dt, t2, t3):
+        moved = (K + 1) * nbytes
+        return {"seconds": round(dt, 3), "GBps": round(moved / dt / 1e9, 3),
+                "task2_ms_mean": round(1e3 * float(np.mean(t2)), 2), "task2_GBps": round(nbytes / float(np.mean(t2)) / 1e9, 3),
+                "task3_ms": round(1e3 * t3, 2), "task3_GBps": round(nbytes / t3 / 1e9, 3)}
+
+    def listener():
+        srv = socket.socket()
+        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        srv.bind(("127.0.0.1", 0))
+        srv.listen(16)
+        return srv
+
+    # --- the ceiling: the loopback socket alone, same staging, same client
+    staging = ipls.PinnedBuffer(nbytes)
+    staging.view()[::4096] = 0
+    srv = listener()
+    port = srv.getsockname()[1]
+
+    def null_server(n_conn):
+        for _ in range(n_conn):
+            conn, _ = srv.accept()
+            with conn:
+                (t,) = struct.unpack(">h", MW._recv_exact(conn, 2))
+                if t == 2:
+                    MW._recv_exact(conn, nbytes, staging.view())
+                    conn.sendall(MW.ACK)
+                elif t == 3:
+                    conn.sendall(memoryview(staging.view())[:nbytes])
+    th = threading.Thread(target=null_server, args=(2 * (K + 1),), daemon=True)
+    th.start()
+    ceil = [one_round(port) for _ in range(2)]
+    th.join(60)
+    srv.close()
+    staging.close()
+    progress("middleware leg: socket ceiling done")
+
+    # --- the aggregator behind the same socket
+    opts = MW.parse_arguments(f"-p 0 -pa {P} -mp 1 -n {K} -i 0 -training 0 -aggr 0".split())
+    got_port, daemons = [], []
+    ready = threading.Event()
+    th = threading.Thread(target=MW.serve, kwargs=dict(opts=opts, max_connections=1 + 2 * (K + 1), device=device,
+                                                       ready=ready, on_listen=got_port.append,
+                                                       on_daemon=daemons.append), daemon=True)
+    th.start()
+    if not ready.wait(60):
+        return {"error": "the middleware server did not start"}
+    port = got_port[0]
+    assert bytes(task(port, MW.encode_init(False, [], "/ip4/127.0.0.1/tcp/5001", "bench", M), None, 2)) == MW.ACK
+    runs = []
+    for r in range(2):
+        st0 = dict(daemons[0].stats)
+        dt, t2, t3 = one_round(port)
+        st1 = daemons[0].stats
+        runs.append((dt, t2, t3, {"update_s": st1["update_s"] - st0["update_s"],
+                                  "reply_s": st1["reply_s"] - st0["reply_s"]}))
+    th.join(120)
+    ok = None
+    if verify:
+        from oracle import oracle as O   # checker only
+        acc = np.zeros(M)
+        vals = [np.frombuffer(u, dtype=">f8").astype(np.float64) for u in ups]
+        for k in range(K):
+            O.fold(acc, vals[k % D])
+        want = O.be_encode_canonical((acc + 0.0) / float(K))
+        ok = bool(reply.tobytes() == want)
+        del vals, acc, want
+    cold, warm = summary(*ceil[0]), summary(*ceil[1])
+    g_cold, g_warm = summary(*runs[0][:3]), summary(*runs[1][:3])
+    for g, rr in ((g_cold, runs[0]), (g_warm, runs[1])):
+        g["server_ms_per_task2"] = round(1e3 * rr[3]["update_s"] / K, 2)
+        g["server_ms_task3"] = round(1e3 * rr[3]["reply_s"], 2)
+    del ups, reply
+    return {"workload": f"Middleware over TCP loopback: -pa {P} -n {K}, model {M} doubles ({nbytes / 1e6:.0f} MB per "
+                        f"task): {K} task-2 updates + 1 task-3 reply per round, one connection per task",
+            "GBps": g_warm["GBps"], "ceiling_GBps": warm["GBps"], "frac_of_ceiling": round(g_warm["GBps"] / warm["GBps"], 4),
+            "aggregator": g_warm, "aggregator_cold_round": g_cold, "socket_ceiling": warm,
+            "socket_ceiling_cold_round": cold, "verified_task3_bytes": ok, "prep_s": round(prep_s, 1),
+            "note": "bytes = (K + 1) x 8M moved over the socket per round / client wall time.  Task 2: each "
+                    "partition's slice is received chunk by chunk (4 MiB) straight into the library's pinned ring "
+                    "by ipls_agg_accumulate_chunked's source, sent to the GPU while the next chunk is received, "
+                    "folded once landed; sync before the ACK.  Task 3: the divide kernel's writeDouble stream "
+                    "sent chunk by chunk from the pinned ring (ipls_agg_get_partitions_wire_chunked).  "
+                    "server_ms_*: time inside the aggregator's socket handlers (socket reads/writes included).  "
+                    "Ceiling = the same socket traffic into / out of one pinned buffer with no aggregator.  "
+                    "Python server and client threads in one process"}
 
 
 def e2e_multi(ipls, torch, dist, group, rank, world, local, L, K, reps, verify) -> dict:
@@ -677,7 +832,9 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
     'double<->byte pack/unpack in the timed region', or F (one GPU's slice of
     config F: 16 x 8M x 64, 69.8 GB of buckets resident).  Same algorithmic-bytes
     accounting as the headline; kernel time by HIP events on the handle's
-    stream, `rounds` rounds of `steps` launches, the median round reported
+    stream at the two ends of each of `rounds` rounds of `steps` back-to-back
+    launches (so it includes the ~1.6 us boundary between launches), the
+    median round reported
     (the first launches after a fresh allocation can run a few % slow);
     partition 0 checked against the oracle's checksum."""
     P, L, K = CONFIGS[name]
@@ -700,15 +857,19 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
     step()
     step()
     agg.sync()
+    # one HIP event at each end of a round of back-to-back launches: an event
+    # packet after every launch added 4.6 us to each 0.18 ms B launch (2.5 % of
+    # the line, tools/b_gap_probe.py, profiles/r05/b_gap/); what remains
+    # between launches is the in-order dependent-launch boundary (~1.6 us)
     per_round = []
     for _ in range(rounds):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-        ev[0].record(stream)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
         for i in range(steps):
             step()
-            ev[i + 1].record(stream)
+        ev1.record(stream)
         agg.sync()
-        per_round.append(float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])))
+        per_round.append(ev0.elapsed_time(ev1) / steps)
     ms = float(np.median(per_round))
     launch = agg.last_launch()
     nbytes = P * (K + 1) * L * 8
@@ -1636,6 +1797,8 @@ def main():
             out["per_arrival"] = side(per_arrival_leg, ipls, torch, agg, rows, P, L, K, stream, not args.no_verify)
         if world == 1 and not args.no_e2e:
             out["host_inclusive"] = side(host_inclusive, ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
+        if world == 1 and not args.no_e2e and not args.no_middleware:
+            out["middleware_socket"] = side(middleware_socket_leg, ipls, torch, local, verify=not args.no_verify)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = side(cpu_baseline, L, K, args.cpu_passes)
         if world == 1 and not args.no_other_configs and args.config == "C" and not args.be:

@@ -459,6 +459,13 @@ int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
  * call into this handle.  Replaces the same loop as ipls_agg_get_partitions. */
 int ipls_agg_get_partitions_chunked(ipls_agg *h, int64_t chunk, ipls_chunk_sink sink, void *ctx);
 
+/* The same delivery as Middleware task 3's reply (Serialize, Middleware.java:
+ * 164-170): each chunk is n values of the writeDouble stream -- big-endian
+ * bytes, NaN canonicalised, written by the divide kernel -- so a socket sink
+ * sends chunk k while chunk k + 1 comes back over PCIe (ipls.middleware's
+ * loopback server).  Rules as ipls_agg_get_partitions_chunked. */
+int ipls_agg_get_partitions_wire_chunked(ipls_agg *h, int64_t chunk, ipls_chunk_sink sink, void *ctx);
+
 /* Copy an accumulator out (tests, replica publish IPLS.java:1423-1431).
  * dst_kind HOST_F64, HOST_BE, DEV_F64, DEV_BE; n >= L_p. */
 int ipls_agg_read(ipls_agg *h, int p, int target, void *dst, int64_t n, int dst_kind);

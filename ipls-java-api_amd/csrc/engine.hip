@@ -2081,7 +2081,9 @@ int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind) {
 // return stops the transfer
 // (IPLS_E_INVAL, nothing further is delivered).  The sink must not call
 // into this handle.
-int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+// wire: the same chunks as Middleware's task-3 writeDouble stream (big-endian,
+// NaN canonical: k_divide's OUT_BE form), e.g. for a socket sink.
+int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire) {
   if (!h || !sink) return fail(h, IPLS_E_INVAL, "null argument");
   if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld doubles: even and >= 2", (long long)chunk);
   IPLS_LOCK(h);
@@ -2090,7 +2092,7 @@ int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink,
   HIP_TRY(h, dev_use(h->device));
   if (int rc = ensure_scratch(h, (size_t)M * 8)) return rc;
   const double* d_out = (const double*)h->d_scratch;
-  if (int rc = divide_range(h, 0, h->P, (unsigned long long*)h->d_scratch, false)) return rc;
+  if (int rc = divide_range(h, 0, h->P, (unsigned long long*)h->d_scratch, wire)) return rc;
   const int64_t c = std::min(chunk, M);
   for (auto& sl : h->out_ring)
     if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;

@@ -51,7 +51,7 @@ int dev_read_range(ipls_dev* h, int p, int target, void* dst, int64_t off, int64
 int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_kind, int64_t chunk,
                            ipls_chunk_source source, void* ctx);
 int dev_finalize_chunked(ipls_dev* h, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void* ctx);
-int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx);
+int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire);
 int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64_t n_bytes);
 int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** gbuf, int64_t* glen);
 int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind);

@@ -1024,14 +1024,24 @@ int ipls_agg_get_partitions(ipls_agg* H, void* out, int64_t n, int out_kind) {
   });
 }
 
-int ipls_agg_get_partitions_chunked(ipls_agg* H, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+namespace {
+int get_partitions_chunked(ipls_agg* H, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire) {
   KeepDevice keep_device;
   if (!H || !sink) return ferr(H, IPLS_E_INVAL, "null argument");
   // shard by shard on the calling thread, in model order: the sink runs
   // where the caller is (a JNIEnv belongs to its thread)
   for (int s : nonempty_shards(H))
-    if (int rc = fwd(H, s, dev_get_partitions_chunked(H->sh[s], chunk, sink, ctx))) return rc;
+    if (int rc = fwd(H, s, dev_get_partitions_chunked(H->sh[s], chunk, sink, ctx, wire))) return rc;
   return IPLS_OK;
+}
+}  // namespace
+
+int ipls_agg_get_partitions_chunked(ipls_agg* H, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  return get_partitions_chunked(H, chunk, sink, ctx, false);
+}
+
+int ipls_agg_get_partitions_wire_chunked(ipls_agg* H, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  return get_partitions_chunked(H, chunk, sink, ctx, true);
 }
 
 int ipls_agg_read(ipls_agg* H, int p, int target, void* dst, int64_t n, int dst_kind) {

@@ -106,6 +106,7 @@ SIGNATURES = {
     "ipls_agg_read_range": (_i, [_vp, _i, _i, _vp, _i64, _i64, _i, _P(_u64)]),
     "ipls_agg_flat_size": (_i, [_vp, _P(_i64)]),
     "ipls_agg_get_partitions_chunked": (_i, [_vp, _i64, _vp, _vp]),   # sink: a CHUNK_SINK instance
+    "ipls_agg_get_partitions_wire_chunked": (_i, [_vp, _i64, _vp, _vp]),   # sink: a CHUNK_SINK instance
     "ipls_agg_accumulate_chunked": (_i, [_vp, _i, _i, _i64, _i, _i64, _vp, _vp]),   # source: a CHUNK_SOURCE
     "ipls_agg_finalize_chunked": (_i, [_vp, _i, _i, _i64, _vp, _vp]),   # sink: a CHUNK_SINK instance
     "ipls_agg_wait": (_i, [_vp, _u64]),

@@ -283,6 +283,56 @@ class Aggregator:
                                                       N.HOST_BE if big_endian else N.HOST_F64, ctypes.byref(t)))
         return t.value
 
+    def UpdateChunked(self, partition: int, n: int, source, *, big_endian: bool = True, from_clients: bool = True,
+                      chunk: int = 1 << 19):
+        """Updater._Update of one bucket that the caller produces chunk by
+        chunk, as ONE library call (ipls_agg_accumulate_chunked): ``source(dst,
+        offset, count)`` writes the bucket's values [offset, offset + count)
+        -- 8*count bytes, big-endian unless ``big_endian=False`` -- at the
+        address ``dst`` (the library's pinned ring) and returns True; False
+        stops the call with nothing folded.  ``n`` is the bucket's length
+        (shorter than the partition: ArrayIndexOutOfBounds, before any
+        source call)."""
+        target = N.TGT_AGG if from_clients else N.TGT_REP
+
+        @N.CHUNK_SOURCE
+        def cb(ctx, dst, off, cnt):
+            try:
+                return 0 if source(dst, off, cnt) else 1
+            except Exception:   # noqa: BLE001 -- an exception must not unwind through C
+                return 1
+        self._chk(self._lib.ipls_agg_accumulate_chunked(self._h, partition, target, n,
+                                                        N.HOST_BE if big_endian else N.HOST_F64, chunk, cb, None))
+
+    def GetPartitionsChunked(self, sink, *, wire: bool = False, chunk: int = 1 << 19):
+        """GetPartitions (IPLS.java:1159-1174) handed to ``sink(ptr, offset,
+        count)`` chunk by chunk in model order (ipls_agg_get_partitions_chunked,
+        or with ``wire=True`` the Middleware task-3 writeDouble stream,
+        ipls_agg_get_partitions_wire_chunked): 8*count bytes at ``ptr`` in
+        the library's pinned ring, valid during the call; the sink returns
+        True to go on."""
+        @N.CHUNK_SINK
+        def cb(ctx, vals, off, cnt):
+            try:
+                return 0 if sink(ctypes.cast(vals, ctypes.c_void_p).value, off, cnt) else 1
+            except Exception:   # noqa: BLE001
+                return 1
+        fn = self._lib.ipls_agg_get_partitions_wire_chunked if wire else self._lib.ipls_agg_get_partitions_chunked
+        self._chk(fn(self._h, chunk, cb, None))
+
+    def AggregatePartitionChunked(self, partition: int, sink, *, big_endian: bool = True, chunk: int = 1 << 19):
+        """AggregatePartition with the committed sum handed to ``sink(ptr,
+        offset, count)`` chunk by chunk, as one call (ipls_agg_finalize_chunked:
+        no other caller's call lands between the sum and its bytes)."""
+        @N.CHUNK_SINK
+        def cb(ctx, vals, off, cnt):
+            try:
+                return 0 if sink(ctypes.cast(vals, ctypes.c_void_p).value, off, cnt) else 1
+            except Exception:   # noqa: BLE001
+                return 1
+        self._chk(self._lib.ipls_agg_finalize_chunked(self._h, partition, N.HOST_BE if big_endian else N.HOST_F64,
+                                                      chunk, cb, None))
+
     def flush(self):
         """Launch the folds of every queued device bucket now (no wait)."""
         self._chk(self._lib.ipls_agg_flush(self._h))

@@ -25,9 +25,11 @@ the responsibility protocol are out of scope.
 """
 from __future__ import annotations
 
+import ctypes
 import socket
 import struct
 import threading
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -128,12 +130,13 @@ def _recv_exact(sock: socket.socket, n: int, into=None) -> memoryview:
     return mv
 
 
-def read_task(sock: socket.socket, model_size: int, payload_buffer=None):
+def read_task(sock: socket.socket, model_size: int, payload_buffer=None, task: int | None = None):
     """Deserialize (Middleware.java:121-162).  Returns (task, data): task 1 ->
     dict of the init fields; task 2 -> the model_size*8 BE bytes (a memoryview
     into payload_buffer when one is supplied, e.g. a PinnedBuffer view);
-    task 3 -> None."""
-    (task,) = struct.unpack(">h", _recv_exact(sock, 2))
+    task 3 -> None.  ``task``: the task short was already read."""
+    if task is None:
+        (task,) = struct.unpack(">h", _recv_exact(sock, 2))
     if task == 1:
         boot, nb = struct.unpack(">hh", _recv_exact(sock, 4))
         bs = []
@@ -167,23 +170,86 @@ class LoopbackAggregator:
                               partial_aggregation=int(opts.partial_aggregation), device=device)
         if initial_model is not None:
             self.agg.InitializeWeights(initial_model)
-        self.staging = PinnedBuffer(8 * model_size)   # task-2 payload lands here (DMA source)
+        self._pinned = PinnedBuffer
+        self._staging = None   # whole-payload pinned staging of update_model / get_partitions_wire, on first use
         self.pending = 0
         self.rounds = 0
         self.lock = threading.Lock()
+        # host seconds inside the aggregator per task (the rest of a task is the socket)
+        self.stats = {"updates": 0, "update_s": 0.0, "replies": 0, "reply_s": 0.0}
 
     def update_model(self, be_bytes):
         """Task 2: one peer's update vector (BE bytes) folded into every
         partition as an arrival (Updater._Update / UpdateGradient fold)."""
         with self.lock:
+            t0 = time.perf_counter()
             flat = np.frombuffer(be_bytes, dtype=np.uint8)
             self.agg.UpdateGradient(flat, range(self.opts.partitions))
-            self.pending += 1
-            if self.pending >= self.opts.min_peers:
-                for p in range(self.opts.partitions):
-                    self.agg.AggregatePartition(p)
-                self.pending = 0
-                self.rounds += 1
+            self._close_round_if_due()
+            self.agg.sync()
+            self.stats["update_s"] += time.perf_counter() - t0
+            self.stats["updates"] += 1
+
+    @property
+    def staging(self):
+        """Pinned staging of one whole payload (8 * model_size bytes)."""
+        if self._staging is None:
+            self._staging = self._pinned(8 * self.model_size)
+        return self._staging
+
+    def _close_round_if_due(self):
+        self.pending += 1
+        if self.pending >= self.opts.min_peers:
+            for p in range(self.opts.partitions):
+                self.agg.AggregatePartition(p)
+            self.pending = 0
+            self.rounds += 1
+
+    def update_from_socket(self, sock: socket.socket):
+        """Task 2 streamed off the socket (Deserialize, Middleware.java:156-160,
+        then UpdateGradient, IPLS.java:1737-1743): partition p's slice of the
+        update -- the next L_p - 1 big-endian doubles of the stream, then its
+        count slot 1.0 (OrganizeGradients, IPLS.java:1018-1040) -- is one
+        ipls_agg_accumulate_chunked call whose source receives each chunk
+        straight into the library's pinned ring; the copy engine sends it to
+        the GPU while the next chunk is received, and the partition is folded
+        once its slice has landed.  Same bits as update_model on the whole
+        payload.  A connection that ends mid-update raises (Java's
+        EOFException ends the Middleware, Middleware.java:262-265), with the
+        partitions received before it already folded."""
+        one = struct.pack(">d", 1.0)
+        with self.lock:
+            t0 = time.perf_counter()
+            for p in range(self.opts.partitions):
+                L = self.agg.lengths[p]
+
+                def source(dst, off, n, L=L):
+                    wire = min(off + n, L - 1) - off     # values of this chunk that come off the socket
+                    if wire > 0:
+                        _recv_exact(sock, 8 * wire, (ctypes.c_char * (8 * wire)).from_address(dst))
+                    if off + n == L:                     # the count slot
+                        ctypes.memmove(dst + 8 * (n - 1), one, 8)
+                    return True
+                self.agg.UpdateChunked(p, L, source)
+            self._close_round_if_due()
+            self.agg.sync()
+            self.stats["update_s"] += time.perf_counter() - t0
+            self.stats["updates"] += 1
+
+    def reply_to_socket(self, sock: socket.socket):
+        """Task 3 (Return_Global_model, Middleware.java:178-184): GetPartitions'
+        writeDouble stream produced by the divide kernel and sent chunk by
+        chunk straight from the library's pinned ring, each chunk on the wire
+        while the next crosses PCIe (ipls_agg_get_partitions_wire_chunked)."""
+        with self.lock:
+            t0 = time.perf_counter()
+
+            def sink(ptr, off, n):
+                sock.sendall((ctypes.c_char * (8 * n)).from_address(ptr))
+                return True
+            self.agg.GetPartitionsChunked(sink, wire=True)
+            self.stats["reply_s"] += time.perf_counter() - t0
+            self.stats["replies"] += 1
 
     def get_partitions_wire(self) -> memoryview:
         """Task 3: GetPartitions' writeDouble stream, written by the divide
@@ -191,17 +257,23 @@ class LoopbackAggregator:
         and handed to ``sendall`` from there.  The view is valid until the
         next task 2 lands in the same staging (the server is sequential)."""
         with self.lock:
-            return self.agg.GetPartitions(wire=True, out=self.staging)
+            t0 = time.perf_counter()
+            v = self.agg.GetPartitions(wire=True, out=self.staging)
+            self.stats["reply_s"] += time.perf_counter() - t0
+            self.stats["replies"] += 1
+            return v
 
     def close(self):
         self.agg.close()
-        self.staging.close()
+        if self._staging is not None:
+            self._staging.close()
 
 
 def serve(opts: Options, max_connections: int | None = None, device: int = 0, initial_model=None,
-          ready: threading.Event | None = None, host: str = "127.0.0.1", on_listen=None):
+          ready: threading.Event | None = None, host: str = "127.0.0.1", on_listen=None, on_daemon=None):
     """Middleware.main (Middleware.java:212-268): one connection per task.
-    ``opts.port`` 0 binds a free port; ``on_listen(port)`` is told which."""
+    ``opts.port`` 0 binds a free port; ``on_listen(port)`` is told which, and
+    ``on_daemon(aggregator)`` gets the LoopbackAggregator task 1 creates."""
     srv = socket.socket()
     srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     srv.bind((host, opts.port))
@@ -217,16 +289,18 @@ def serve(opts: Options, max_connections: int | None = None, device: int = 0, in
             conn, _ = srv.accept()
             served += 1
             with conn:
-                ms = daemon.model_size if daemon else 0
-                task, data = read_task(conn, ms, daemon.staging.view() if daemon else None)
+                (task,) = struct.unpack(">h", _recv_exact(conn, 2))
                 if task == 1:
+                    _, data = read_task(conn, 0, task=1)
                     daemon = LoopbackAggregator(opts, data["model_size"], device, initial_model)
+                    if on_daemon is not None:
+                        on_daemon(daemon)
                     conn.sendall(ACK)
                 elif task == 2:
-                    daemon.update_model(data)
+                    daemon.update_from_socket(conn)
                     conn.sendall(ACK)
                 elif task == 3:
-                    conn.sendall(daemon.get_partitions_wire())
+                    daemon.reply_to_socket(conn)
     finally:
         srv.close()
         if daemon is not None:

@@ -1116,6 +1116,7 @@ def test_accumulate_chunked(ipls, O, devices):
         return 1 if len(calls) == 3 else 0
     assert lib.ipls_agg_accumulate_chunked(h, 1, 0, L, N.HOST_F64, 65536, stop, None) == N.IPLS_E_INVAL
     assert calls == [0, 65536, 131072]
+    calls.clear()
     assert lib.ipls_agg_accumulate_chunked(h, 0, 0, L, N.HOST_F64, 65536, stop, None) == N.IPLS_E_INVAL
     calls.clear()
     assert lib.ipls_agg_accumulate_chunked(h, 1, 0, L - 1, N.HOST_F64, 65536, stop, None) == N.IPLS_E_RANGE

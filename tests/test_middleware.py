@@ -73,3 +73,49 @@ def test_config_a_loopback_over_tcp(ethmodel, golden_meta):
     wire = client_call(port, encode_get(), 8 * M)
     th.join(60)
     assert hashlib.sha256(wire).hexdigest() == golden_meta["config_a"]["wire_sha256"]
+
+
+@pytest.mark.gpu
+def test_streamed_tasks_match_the_oracle_across_chunk_edges():
+    """Task 2 streamed off the socket chunk by chunk (update_from_socket:
+    ipls_agg_accumulate_chunked per partition with the socket as the source)
+    and task 3 sent chunk by chunk (ipls_agg_get_partitions_wire_chunked),
+    at a geometry whose partitions end exactly on a chunk edge, so the count
+    slot 1.0 is a chunk of its own (L = 524,289 = 2^19 + 1), plus a short last
+    partition: the reply equals the oracle's writeDouble stream of the
+    fixed-order average, for two rounds on one connection-per-task server,
+    and equals what the whole-payload path (update_model) gives."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    from oracle import oracle as O
+    from ipls.middleware import (LoopbackAggregator, client_call, encode_get, encode_init, encode_update,
+                                 parse_arguments, serve)
+    M, P, K = 3 * 524287, 3, 3
+    assert [O.partition_len(M, P, p) for p in range(P)] == [524289, 524289, 524286]
+    ports = []
+    opts = parse_arguments(f"-p 0 -pa {P} -mp 1 -n {K} -i 0 -training 60 -aggr 0".split())
+    ready = threading.Event()
+    th = threading.Thread(target=serve, kwargs=dict(opts=opts, max_connections=1 + 2 * (K + 1), ready=ready,
+                                                    on_listen=ports.append), daemon=True)
+    th.start()
+    assert ready.wait(30)
+    port = ports[0]
+    assert client_call(port, encode_init(False, [], "/ip4/127.0.0.1/tcp/5001", "m", M), 2) == b"\x00A"
+    peers = [O.synth_bucket(M, 7, k) * (1.0 + k) for k in range(K)]
+    peers[1][::1013] = -0.0
+    parts = [O.organize_gradients(g, M, P) for g in peers]
+    sums = [O.reduce([parts[k][p] for k in range(K)], O.partition_len(M, P, p)) + 0.0 for p in range(P)]
+    want = O.be_encode_canonical(O.get_partitions(sums))
+    for _ in range(2):
+        for g in peers:
+            assert client_call(port, encode_update(g), 2) == b"\x00A"
+        wire = client_call(port, encode_get(), 8 * M)
+        assert wire == want
+    th.join(60)
+    # the whole-payload path gives the same bytes
+    la = LoopbackAggregator(opts, M)
+    for g in peers:
+        la.update_model(g.astype(">f8").tobytes())
+    assert bytes(la.get_partitions_wire()) == want
+    la.close()
