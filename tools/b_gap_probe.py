@@ -8,6 +8,8 @@ buckets (16 partitions x 1,048,576 doubles x 8 peers, 1.21 GB per launch):
                 event packets in between)
   host_us       host time per reduce_batch call (Python -> C-ABI -> launch),
                 to see whether the GPU ever waits on the host
+  out_ends      as events_ends, but reduce_batch_out into caller buffers
+                (what bench.py's config_leg launches)
 
 Run it under `rocprofv3 --kernel-trace` and feed the trace to
 tools/gap_split.py for the kernel-only time and the gap between launches.
@@ -41,13 +43,21 @@ def main():
     agg = ipls.Aggregator(n_partitions=P, bucket_len=L)
     stream = torch.cuda.ExternalStream(agg.stream)
 
+    out_arena = torch.empty(P * elem + 32, dtype=torch.float64, device="cuda")
+    obase = (int(out_arena.data_ptr()) + 255) // 256 * 256
+    dsts = [obase + 8 * q * elem for q in range(P)]
+
     def step():
         agg.reduce_batch(0, rows, start_mode=ipls.START_ZERO)
+
+    def step_out():
+        agg.reduce_batch_out(0, rows, dsts, start_mode=ipls.START_ZERO)
     for _ in range(20):
         step()
+        step_out()
     agg.sync()
     nbytes = P * (K + 1) * L * 8
-    each, ends, host = [], [], []
+    each, ends, host, outs = [], [], [], []
     for _ in range(ROUNDS):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(N + 1)]
         ev[0].record(stream)
@@ -66,10 +76,19 @@ def main():
         agg.sync()
         ends.append(a.elapsed_time(b) / N)
         host.append((t1 - t0) / N * 1e6)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for i in range(N):
+            step_out()
+        b.record(stream)
+        agg.sync()
+        outs.append(a.elapsed_time(b) / N)
     me, mn = float(np.median(each)), float(np.median(ends))
     out = {"workload": f"B: {P} x {L} x {K}, {nbytes} B per launch", "launches_per_round": N, "rounds": ROUNDS,
            "events_each_ms": round(me, 5), "events_each_frac": round(nbytes / me / 8e9, 4),
            "events_ends_ms": round(mn, 5), "events_ends_frac": round(nbytes / mn / 8e9, 4),
+           "out_ends_ms": round(float(np.median(outs)), 5),
+           "out_ends_frac": round(nbytes / float(np.median(outs)) / 8e9, 4),
            "host_us_per_call": round(float(np.median(host)), 2), "launch": agg.last_launch(),
            "per_round_each_ms": [round(x, 5) for x in each], "per_round_ends_ms": [round(x, 5) for x in ends]}
     agg.close()

@@ -1,13 +1,15 @@
 """Dev probe: what a heap-array native costs against the direct-buffer one,
 through the JNI shim and the fake JVM (tests/jni/fake_jvm.c) on the GPU box.
 One partition of L doubles (one bucket per call, as the Updater folds):
-  accumulate(double[])         -- GetDoubleArrayRegion chunk by chunk into the
-                                  shim's pinned two-slot ring, each chunk folded
-                                  (ipls_agg_accumulate_range) while the next is copied
+  accumulate(double[])         -- one ipls_agg_accumulate_chunked call: the library
+                                  pulls the array chunk by chunk (the shim's
+                                  GetDoubleArrayRegion source) into its pinned ring,
+                                  each chunk sent while the next is copied, one fold
   accumulateDirect(ByteBuffer) -- a hostAlloc direct buffer, zero copy
-  finalizePartition(byte[])    -- AggregatePartition, then the BE sum back in
-                                  ring chunks (ipls_agg_read_range), each copied
-                                  into the byte[] while the next arrives
+  finalizePartition(byte[])    -- one ipls_agg_finalize_chunked call:
+                                  AggregatePartition, then the BE sum back in ring
+                                  chunks, each copied into the byte[] (the shim's
+                                  SetByteArrayRegion sink) while the next arrives
   finalizePartitionDirect      -- the BE sum straight into a direct buffer
   getPartitions(double[])      -- GetPartitions (the divide) into a heap double[]
   getPartitionsWire(ByteBuffer)-- the same as Middleware's big-endian stream into
