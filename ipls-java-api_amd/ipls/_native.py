@@ -172,15 +172,14 @@ def lib() -> ctypes.CDLL:
     there is deliberately no CPU path behind this package."""
     global _lib
     if _lib is None:
-        # torch (when installed) first: its bundled HIP runtime must be the
-        # process's runtime before the library's own link to /opt/rocm's is
-        # resolved.  In the other order -- this library loaded, then torch
-        # initialised -- the library finds "no HIP device available"
-        # (tools/jni_open_probe.py, profiles/r04/i/).
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # Load order with torch (ADVICE r4): a process that uses torch as well
+        # must import torch BEFORE the first call that loads this library --
+        # torch's bundled HIP runtime has to be the process's runtime before
+        # the library's link to /opt/rocm's is resolved; in the other order the
+        # library finds "no HIP device available" (tools/jni_open_probe.py,
+        # profiles/r04/i/).  The entry points that mix the two do so
+        # (tests/conftest.py, bench.py, the tools); a caller without torch
+        # pays no torch import here.
         _lib = load(LIB_PATH)
     return _lib
 
