@@ -55,6 +55,16 @@ public final class NativeAggregator implements AutoCloseable {
         if (gradients != null) updateGradient(handle, gradients, authList);
     }
 
+    /** Middleware task 2 (Deserialize, Middleware.java:156-160) + UpdateModel's
+     *  own accumulate, without the List&lt;Double&gt;: the update's model_size
+     *  big-endian doubles, as read off the socket into a hostAlloc direct buffer
+     *  (e.g. Channels.newChannel(in).read(buf) until full), folded from there
+     *  (the byte swap is fused into the fold; only the owned partitions' bytes
+     *  cross PCIe). */
+    public void updateGradientWire(ByteBuffer direct, int[] authList) {
+        updateGradientDirect(handle, direct, direct.position(), direct.remaining() / 8, authList);
+    }
+
     /** OrganizeGradients (IPLS.java:1018-1040) for partition p (count slot 1.0). */
     public double[] organize(double[] gradients, int p) {
         double[] out = new double[partitionLength(p)];
@@ -287,6 +297,7 @@ public final class NativeAggregator implements AutoCloseable {
     private static native void loadModel(long h, double[] model);
     private static native void split(long h, double[] flat, int p, double[] out);
     private static native void updateGradient(long h, double[] flat, int[] owned);
+    private static native void updateGradientDirect(long h, ByteBuffer buf, int pos, long n, int[] owned);
     private static native void accumulate(long h, int p, int target, double[] g);
     private static native void accumulateDirect(long h, int p, int target, ByteBuffer buf, int pos, long n, int kind);
     private static native long accumulateAsyncDirect(long h, int p, int target, ByteBuffer buf, int pos, long n,

@@ -296,6 +296,24 @@ JNIEXPORT void JNICALL Java_NativeAggregator_updateGradient(JNIEnv *env, jclass 
     CHECK(rc, H(h));
 }
 
+/* Middleware task 2 without the List<Double>: the update's big-endian bytes
+ * in a direct buffer (as read off the socket) folded into the owned
+ * partitions (ipls_agg_update_gradient, HOST_BE: the byte swap fused into
+ * the fold, only the owned partitions' bytes cross PCIe). */
+JNIEXPORT void JNICALL Java_NativeAggregator_updateGradientDirect(JNIEnv *env, jclass c, jlong h, jobject buf,
+                                                                    jint pos, jlong n, jintArray owned) {
+    (void)c;
+    void *src = direct_span(env, buf, pos, n, 8);
+    if (!src) return;
+    if (!owned) { throw_iae(env, "null auth list"); return; }
+    const jsize no = (*env)->GetArrayLength(env, owned);
+    jint *own = (*env)->GetIntArrayElements(env, owned, NULL);
+    if (!own) return;   /* OutOfMemoryError pending */
+    int rc = LIB(ipls_agg_update_gradient(H(h), src, n, IPLS_HOST_BE, (const int32_t *)own, no));
+    (*env)->ReleaseIntArrayElements(env, owned, own, JNI_ABORT);
+    CHECK(rc, H(h));
+}
+
 /* The chunk source of accumulate(double[]): the library asks for the
  * bucket's values [off, off + n) and the shim copies them out of the heap. */
 struct heap_source { JNIEnv *env; jdoubleArray a; };

@@ -40,6 +40,7 @@ void Java_NativeAggregator_close(JNIEnv *, jclass, jlong);
 jintArray Java_NativeAggregator_shardPlan(JNIEnv *, jclass, jint, jint);
 void Java_NativeAggregator_loadModel(JNIEnv *, jclass, jlong, jdoubleArray);
 void Java_NativeAggregator_updateGradient(JNIEnv *, jclass, jlong, jdoubleArray, jintArray);
+void Java_NativeAggregator_updateGradientDirect(JNIEnv *, jclass, jlong, jobject, jint, jlong, jintArray);
 void Java_NativeAggregator_accumulate(JNIEnv *, jclass, jlong, jint, jint, jdoubleArray);
 void Java_NativeAggregator_accumulateDirect(JNIEnv *, jclass, jlong, jint, jint, jobject, jint, jlong, jint);
 void Java_NativeAggregator_updateIndirect(JNIEnv *, jclass, jlong, jint, jint, jobject, jint, jlong);
@@ -120,6 +121,9 @@ int main(void) {
     CALL(IAE, Java_NativeAggregator_accumulateDirect(env, NULL, 0, 0, 0, dir, -8, 1, 1));
     CALL(IAE, Java_NativeAggregator_accumulateDirect(env, NULL, 0, 0, 0, dir, 0, -1, 1));
     CALL(IAE, Java_NativeAggregator_updateIndirect(env, NULL, 0, 0, 0, dir, 8, 57));
+    CALL(IAE, Java_NativeAggregator_updateGradientDirect(env, NULL, 0, heap, 0, 1, io));
+    CALL(IAE, Java_NativeAggregator_updateGradientDirect(env, NULL, 0, dir, 8, 8, io));    /* 8 + 64 > 64 */
+    CALL(IAE, Java_NativeAggregator_updateGradientDirect(env, NULL, 0, dir, 0, 8, io));    /* in range: null handle */
     CALL(IAE, Java_NativeAggregator_getPartitionsWire(env, NULL, 0, heap, 0, 8));
     CALL(IAE, Java_NativeAggregator_getPartitionsWire(env, NULL, 0, dir, 60, 8));
     CALL(IAE, Java_NativeAggregator_accumulateDirect(env, NULL, 0, 0, 0, dir, 0, 8, 1));     /* in range: null handle */

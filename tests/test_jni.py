@@ -186,7 +186,9 @@ def test_direct_buffer_checks_before_the_library(jvm):
                        ("accumulateAsyncDirect", (L64(0), 0, 0, buf, 0, L64((1 << 61) + 1), 1)),
                        ("setWeightsDirect", (L64(0), 0, buf, 0, L64(1 << 62))),
                        ("otherReplicaDirect", (L64(0), 0, 1, 0, buf, 0, L64(1 << 61))),
-                       ("updateIndirect", (L64(0), 0, 0, buf, 65, L64(0)))]:          # pos past the end
+                       ("updateIndirect", (L64(0), 0, 0, buf, 65, L64(0))),           # pos past the end
+                       ("updateGradientDirect", (L64(0), heap, 0, L64(1), jvm.ints([0]))),
+                       ("updateGradientDirect", (L64(0), buf, 8, L64(8), jvm.ints([0])))]:   # 8 + 64 > 64
         _, exc = jvm.call(name, *args)
         assert exc == "java/lang/IllegalArgumentException", (name, exc)
 
@@ -410,17 +412,27 @@ def test_jni_heap_natives_are_one_ordered_unit(jvm, gpu, O):
 def test_jni_update_gradient_owned_subset(jvm, gpu, O):
     """updateGradient(double[], owned) copies only the owned partitions'
     slices out of the heap (the library reads nothing else): owned {1, 3} of
-    4 folds exactly those partitions' values, twice, and leaves 0 and 2 at
-    zero; a vector one value too long is still ArrayIndexOutOfBoundsException
-    for the whole call (OrganizeGradients checks every partition)."""
+    4 folds exactly those partitions' values, and leaves 0 and 2 at zero; the
+    second update arrives as Middleware task 2's big-endian bytes in a direct
+    buffer (updateGradientDirect); a vector one value too long is still
+    ArrayIndexOutOfBoundsException for the whole call (OrganizeGradients
+    checks every partition)."""
     M, P = 40009, 4
     h = _open(jvm, M, P)
     flats = [O.synth_bucket(M, 9, k) for k in range(2)]
-    for g in flats:
-        _, exc = jvm.call("updateGradient", h, jvm.doubles(g), jvm.ints([1, 3]))
-        assert exc is None
+    _, exc = jvm.call("updateGradient", h, jvm.doubles(flats[0]), jvm.ints([1, 3]))
+    assert exc is None
+    # Middleware task 2 without the List<Double>: the second update's BE bytes
+    # in a direct buffer at position 8 (updateGradientDirect, HOST_BE)
+    be = O.be_encode(flats[1])
+    buf, mem = jvm.direct(8 + len(be))
+    mem[8:] = np.frombuffer(be, dtype=np.uint8)
+    _, exc = jvm.call("updateGradientDirect", h, buf, 8, L64(M), jvm.ints([1, 3]))
+    assert exc is None
     _, exc = jvm.call("updateGradient", h, jvm.doubles(np.ones(M + 1)), jvm.ints([1, 3]))
     assert exc == "java/lang/ArrayIndexOutOfBoundsException"
+    _, exc = jvm.call("updateGradientDirect", h, buf, 8, L64(M + 1), jvm.ints([1, 3]))
+    assert exc == "java/lang/IllegalArgumentException"          # past the buffer: refused by the shim
     parts = [O.organize_gradients(g, M, P) for g in flats]
     for p in range(P):
         L = O.partition_len(M, P, p)
