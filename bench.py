@@ -452,26 +452,47 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
                                   "reply_s": st1["reply_s"] - st0["reply_s"]}))
     th.join(120)
     ok = None
+    want_sum = None
     if verify:
         from oracle import oracle as O   # checker only
         acc = np.zeros(M)
         vals = [np.frombuffer(u, dtype=">f8").astype(np.float64) for u in ups]
         for k in range(K):
             O.fold(acc, vals[k % D])
-        want = O.be_encode_canonical((acc + 0.0) / float(K))
+        avg = (acc + 0.0) / float(K)
+        want = O.be_encode_canonical(avg)
         ok = bool(reply.tobytes() == want)
-        del vals, acc, want
+        want_sum = O.checksum(avg)
+        del vals, acc, want, avg
     cold, warm = summary(*ceil[0]), summary(*ceil[1])
     g_cold, g_warm = summary(*runs[0][:3]), summary(*runs[1][:3])
     for g, rr in ((g_cold, runs[0]), (g_warm, runs[1])):
         g["server_ms_per_task2"] = round(1e3 * rr[3]["update_s"] / K, 2)
         g["server_ms_task3"] = round(1e3 * rr[3]["reply_s"], 2)
     del ups, reply
+    # the same traffic through the native server (host/ipls_middleware.hpp, Middleware.main in C++ over the
+    # C-ABI) and a native client: tools/middleware_e2e.cpp, a child process, the same update vectors
+    native = None
+    exe = ROOT / "ipls-java-api_amd" / "lib" / "middleware_e2e"
+    if exe.exists():
+        import subprocess
+        r = subprocess.run([str(exe), str(M), str(P), str(K), str(D)], capture_output=True, text=True, timeout=300)
+        if r.returncode == 0:
+            native = json.loads(r.stdout.strip().splitlines()[-1])
+            native["frac_of_ceiling"] = round(native["aggregator"]["GBps"] / native["socket_ceiling"]["GBps"], 4)
+            native["verified_task3_checksum"] = (int(native["reply_checksum"]) == want_sum) if want_sum is not None else None
+            native["source"] = "tools/middleware_e2e.cpp: ipls_host::MiddlewareServer + MiddlewareClient, C++"
+        else:
+            native = {"error": f"rc {r.returncode}: {r.stderr[-400:]}"}
+    else:
+        native = {"error": "ipls-java-api_amd/lib/middleware_e2e not built (make -C ipls-java-api_amd host_e2e)"}
+    progress("middleware leg: native server done")
     return {"workload": f"Middleware over TCP loopback: -pa {P} -n {K}, model {M} doubles ({nbytes / 1e6:.0f} MB per "
                         f"task): {K} task-2 updates + 1 task-3 reply per round, one connection per task",
             "GBps": g_warm["GBps"], "ceiling_GBps": warm["GBps"], "frac_of_ceiling": round(g_warm["GBps"] / warm["GBps"], 4),
             "aggregator": g_warm, "aggregator_cold_round": g_cold, "socket_ceiling": warm,
             "socket_ceiling_cold_round": cold, "verified_task3_bytes": ok, "prep_s": round(prep_s, 1),
+            "native": native,
             "note": "bytes = (K + 1) x 8M moved over the socket per round / client wall time.  Task 2: each "
                     "partition's slice is received chunk by chunk (4 MiB) straight into the library's pinned ring "
                     "by ipls_agg_accumulate_chunked's source, sent to the GPU while the next chunk is received, "

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "ipls_host.hpp"
+#include "ipls_middleware.hpp"
 #include "ipls_oracle.h"
 
 using namespace ipls_host;
@@ -191,6 +192,55 @@ int main(int argc, char** argv) {
         expect.insert(expect.end(), d.begin(), d.end());
       }
       CHECK(avg.size() == expect.size() && bits_equal(avg.data(), expect.data(), avg.size()), "averaged model");
+    });
+
+    run("Middleware.main over TCP loopback (config A, -pa 3 -n 3), two rounds", [&] {
+      // the native server (host/ipls_middleware.hpp) with a chunk of 73,934
+      // values: partition 2 (L = 147,869 = 2 x 73,934 + 1) ends with a chunk
+      // that is its count slot alone, partitions 0 and 1 with 3 values + the slot
+      const auto model = read_ethmodel(golden + "/ethmodel.f64be.gz");
+      const int64_t M = (int64_t)model.size();
+      PeerData opts = Middleware::parse_arguments({"-p", "0", "-pa", "3", "-mp", "1", "-n", "3", "-i", "0",
+                                                   "-training", "60", "-aggr", "0"});
+      MiddlewareServer server(opts, 73934);
+      const int port = server.listen(0);
+      std::thread srv([&] { server.serve(1 + 2 * 4); });
+      std::vector<std::vector<double>> peers(3, model);
+      std::vector<std::vector<uint8_t>> wire(3, std::vector<uint8_t>((size_t)M * 8));
+      for (int k = 0; k < 3; ++k) {
+        auto noise = synth(M + 1, 0, k);
+        for (int64_t i = 0; i < M; ++i) peers[k][i] = model[i] + noise[i];
+        peers[k][7 * k + 1] = -0.0;
+        ipls_oracle_be_encode(peers[k].data(), M, wire[k].data());
+      }
+      std::vector<uint8_t> want;
+      for (int p = 0; p < 3; ++p) {   // oracle: fixed-order sum from +0.0, the divide, writeDouble bytes
+        const int64_t L = ipls_oracle_partition_len(M, 3, p);
+        std::vector<double> sum((size_t)L), avg((size_t)L - 1);
+        std::vector<std::vector<double>> b;
+        for (int k = 0; k < 3; ++k) b.push_back(organize(peers[k], M, 3, p));
+        const double* bp[3] = {b[0].data(), b[1].data(), b[2].data()};
+        ipls_oracle_reduce(sum.data(), bp, 3, L, 1);
+        ipls_oracle_divide(sum.data(), L, 0, avg.data());
+        std::vector<uint8_t> bytes((size_t)(L - 1) * 8);
+        ipls_oracle_be_encode_canonical(avg.data(), L - 1, bytes.data());
+        want.insert(want.end(), bytes.begin(), bytes.end());
+      }
+      try {
+        MiddlewareClient::init(port, (int32_t)M, "/ip4/127.0.0.1/tcp/5001", "ETHModel");
+        for (int round = 0; round < 2; ++round) {
+          for (int k = 0; k < 3; ++k) MiddlewareClient::update(port, wire[k].data(), wire[k].size());
+          std::vector<uint8_t> got((size_t)M * 8);
+          MiddlewareClient::get(port, got.data(), got.size());
+          CHECK(got == want, "task-3 reply == the oracle's writeDouble stream");
+        }
+      } catch (...) {
+        srv.detach();
+        throw;
+      }
+      srv.join();
+      CHECK(server.stats().rounds == 2 && server.stats().updates == 6 && server.init().file_name == "ETHModel",
+            "two rounds of three updates");
     });
 
     run("Updater file + frame arrivals, replicas, commit bytes", [&] {
