@@ -34,7 +34,10 @@ using namespace ipls;
 namespace ipls {
 // The round-4 A/B form of k_divide (not shipped): ALIGNED = true reads W with
 // 16-B loads whatever its alignment to the output; false is the shipped form.
-template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV, bool ALIGNED = false>
+// SWZ (round 5): blocks that share an XCD (b % 8) take a contiguous run of
+// tiles (the guide's bijective T1 remap), so the W line a tile boundary splits
+// is read by two blocks on one L2 instead of two L2s.
+template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV, bool ALIGNED = false, bool SWZ = false>
 __global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ parts,
                                                const double* __restrict__ arena,
                                                unsigned long long* __restrict__ out,
@@ -55,8 +58,13 @@ __global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ pa
   constexpr int kBlock = BS;
   constexpr int kV = V;
   constexpr int64_t kTile = (int64_t)kBlock * 2 * kV;
-  const int q = blockIdx.x / tiles_per_part;
-  const int t = blockIdx.x - q * tiles_per_part;
+  unsigned b = blockIdx.x;
+  if constexpr (SWZ) {
+    const unsigned nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
+    b = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+  }
+  const int q = (int)b / tiles_per_part;
+  const int t = (int)b - q * tiles_per_part;
   const DivDesc d = parts[q];
   const int64_t n = d.len - 1;
   const double* w = arena + d.w_off;
@@ -176,31 +184,23 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_finalize<true, false, BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_fd, arena, tpp);                                                    \
                   }})
-#define DIVX(BS, V, AL, TAG)                                                                                \
+#define DIVX(BS, V, AL, SW, TAG)                                                                            \
   vars.push_back({"divide   BS=" #BS " V=" #V TAG, div_bytes, [=](hipStream_t s) {                          \
                     const int64_t tile = (int64_t)BS * 2 * V;                                                \
                     const int tpp = (int)((L - 1 + tile - 1) / tile);                                        \
-                    hipLaunchKernelGGL((k_divide_ab<false, false, BS, V, AL>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
+                    hipLaunchKernelGGL((k_divide_ab<false, false, BS, V, AL, SW>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_dd, (const double*)arena, model, tpp);                              \
                   }})
-#define DIV(BS, V) DIVX(BS, V, false, "")
-  FIN(256, 4);   // shipped
-  FIN(256, 8);
-  FIN(256, 16);
-  FIN(512, 8);
-  FIN(512, 16);
-  FIN(1024, 4);
-  FIN(1024, 8);
-  FIN(1024, 16);
-  DIVX(256, 4, false, " 8B");   // shipped: two 8-B loads per lane
-  DIVX(256, 4, true, " 16B");   // round-4 A/B: 16-B loads whatever the alignment
-  DIVX(512, 4, true, " 16B");
+#define DIV(BS, V) DIVX(BS, V, false, false, "")
+  FIN(256, 8);   // shipped (kFinV = 8)
+  FIN(256, 4);
+  DIVX(256, 4, false, false, " 8B");   // shipped: two 8-B loads per lane
+  DIVX(256, 4, false, true, " 8B xcd");   // round 5: the XCD-contiguous tile order
+  DIVX(256, 8, false, true, " 8B xcd");
+  DIVX(256, 4, true, false, " 16B");   // round-4 A/B: 16-B loads whatever the alignment
+  DIVX(256, 4, true, true, " 16B xcd");
   DIV(256, 8);
-  DIV(256, 16);
   DIV(512, 8);
-  DIV(1024, 4);
-  DIV(1024, 8);
-  DIV(1024, 16);
 #undef FIN
 #undef DIV
 #undef DIVX
