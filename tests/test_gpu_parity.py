@@ -1131,6 +1131,62 @@ def test_accumulate_chunked(ipls, O, devices):
 
 
 @pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_accumulate_chunked_threads_serialise(ipls, O, devices):
+    """Four threads fold four buckets into the same partition, each as one
+    ipls_agg_accumulate_chunked call whose source sleeps between chunks (so
+    that, were the calls not units, they would interleave).  Each call holds
+    its shard's lock from its first source call to its fold, so the order in
+    which the threads made their first source call is the serial order, and
+    the target equals the oracle's fold in that order, bit for bit.  A fifth
+    thread keeps folding into another partition of the same shard meanwhile."""
+    import threading
+    import time
+    from ipls import _native as N
+    L = 262147
+    agg = ipls.Aggregator(n_partitions=2, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    gs = [O.synth_bucket(L, 1, 300 + i) * (1.0 + i) for i in range(4)]
+    order, lock = [], threading.Lock()
+    errs = []
+
+    def worker(i):
+        raw = gs[i].tobytes()
+
+        @N.CHUNK_SOURCE
+        def src(ctx, dst, off, n):
+            if off == 0:
+                with lock:
+                    order.append(i)
+            ctypes.memmove(dst, ctypes.c_char_p(raw[8 * off:8 * (off + n)]), 8 * n)
+            time.sleep(0.002)
+            return 0
+        rc = lib.ipls_agg_accumulate_chunked(h, 1, ipls.TGT_AGG, L, N.HOST_F64, 32768, src, None)
+        if rc != 0:
+            errs.append(rc)
+
+    other = O.synth_bucket(L, 0, 9)
+
+    def side():
+        for _ in range(20):
+            agg.Update(other, 0)
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(4)] + [threading.Thread(target=side)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    assert not errs and sorted(order) == [0, 1, 2, 3]
+    want = np.zeros(L)
+    for i in order:
+        want = O.fold(want, gs[i])
+    assert_bits_equal(agg.read(1, ipls.TGT_AGG), want, f"serial order {order}")
+    side_want = np.zeros(L)
+    for _ in range(20):
+        side_want = O.fold(side_want, other)
+    assert_bits_equal(agg.read(0, ipls.TGT_AGG), side_want, "the other partition")
+    agg.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_finalize_chunked(ipls, O, devices):
     """ipls_agg_finalize_chunked: AggregatePartition (W = AGG + REP,
     IPLS.java:1248-1274) with W handed to a sink chunk by chunk, as one call:
