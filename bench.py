@@ -1199,7 +1199,18 @@ def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: f
         agg.sync()
         fin.append(e[0].elapsed_time(e[1]))
         div.append(e[1].elapsed_time(e[2]))
-    fin_ms, div_ms = float(np.median(fin)), float(np.median(div))
+    fin_ms, div_single_ms = float(np.median(fin)), float(np.median(div))
+    # GetPartitions only reads W, so the divide can also run back to back: 20
+    # launches between two events (no event packet between launches, like the
+    # config legs), the steady-state per-launch time
+    agg.sync()
+    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    d0.record(stream)
+    for _ in range(20):
+        agg.GetPartitions(out=fb)
+    d1.record(stream)
+    agg.sync()
+    div_ms = d0.elapsed_time(d1) / 20
     n_el = P * L
     ref_flat = flat.clone()
     # the same round as ONE launch (ipls_agg_aggregate_round): folds + W + averages;
@@ -1222,15 +1233,17 @@ def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: f
         "finalize_ms": round(fin_ms, 4), "finalize_GBps": round(16 * n_el / fin_ms / 1e6, 1),
         "finalize_frac": round(16 * n_el / fin_ms / 1e6 / HBM_PEAK_GBS, 4),
         "finalize_algorithmic_bytes": 16 * n_el, "finalize_traffic": fin_t, "finalize_traffic_provenance": fin_prov,
-        "divide_ms": round(div_ms, 4), "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
+        "divide_ms": round(div_ms, 4), "divide_ms_single_launch": round(div_single_ms, 4),
+        "divide_GBps": round(16 * (n_el - P) / div_ms / 1e6, 1),
         "divide_frac": round(16 * (n_el - P) / div_ms / 1e6 / HBM_PEAK_GBS, 4),
         "divide_algorithmic_bytes": 16 * (n_el - P), "divide_traffic": div_t, "divide_traffic_provenance": div_prov,
-        "round_ms": round(kern_ms + fin_ms + div_ms, 4),
+        "round_ms": round(kern_ms + fin_ms + div_single_ms, 4),
         "fused_round_ms": round(fused_ms, 4),
         "fused_round_GBps": round(fused_bytes / fused_ms / 1e6, 1),
         "fused_round_bit_identical": fused_same,
         "note": "one aggregation round on device: reduce (K buckets) + AggregatePartition(all) + GetPartitions "
-                "as three launches (round_ms), and fused into one (fused_round_ms)",
+                "as three launches (round_ms), and fused into one (fused_round_ms); finalize_ms: one launch "
+                "between two events (it consumes AGG, so it cannot repeat); divide_ms: 20 back-to-back launches",
     }
     del flat, ref_flat
     return info
