@@ -1130,6 +1130,53 @@ def test_accumulate_chunked(ipls, O, devices):
     agg.close()
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_chunked_calls_tiny_partitions_and_wire(ipls, O, devices):
+    """The chunked calls at the smallest shapes: partitions of 1 value (the
+    count slot alone) and 3 values, every target (AGG, REP, FUTURE, Weights)
+    through ipls_agg_accumulate_chunked, finalize_chunked of both, and
+    ipls_agg_get_partitions_wire_chunked over a three-shard handle equal to
+    the whole-model wire bytes of ipls_agg_get_partitions (and the oracle)."""
+    from ipls import _native as N
+    for L in (1, 3):
+        agg = ipls.Aggregator(n_partitions=3, bucket_len=L, devices=devices)
+        lib, h = agg._lib, agg._h
+        want = {}
+        for p in range(3):
+            for tgt in (N.TGT_AGG, N.TGT_REP, N.TGT_FUTURE):
+                g = O.synth_bucket(L, p, 40 + tgt) * (2.0 + tgt)
+
+                @N.CHUNK_SOURCE
+                def src(ctx, dst, off, n, g=g):
+                    ctypes.memmove(dst, g.ctypes.data + 8 * off, 8 * n)
+                    return 0
+                assert lib.ipls_agg_accumulate_chunked(h, p, tgt, L, N.HOST_F64, 2, src, None) == 0
+                want[(p, tgt)] = O.fold(np.zeros(L), g)
+                assert_bits_equal(agg.read(p, tgt), want[(p, tgt)], f"L={L} p={p} tgt={tgt}")
+        for p in range(3):
+            out = bytearray(8 * L)
+
+            @N.CHUNK_SINK
+            def sink(ctx, vals, off, n, out=out):
+                out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+                return 0
+            assert lib.ipls_agg_finalize_chunked(h, p, N.HOST_BE, 2, sink, None) == 0
+            w = want[(p, N.TGT_AGG)] + want[(p, N.TGT_REP)]
+            assert bytes(out) == O.be_encode(w), f"L={L} W[{p}]"
+        whole = agg.GetPartitions(wire=True)
+        got = bytearray()
+
+        @N.CHUNK_SINK
+        def wsink(ctx, vals, off, n):
+            got.extend(ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n))
+            return 0
+        assert lib.ipls_agg_get_partitions_wire_chunked(h, 2, wsink, None) == 0
+        assert bytes(got) == whole
+        ws = [want[(p, N.TGT_AGG)] + want[(p, N.TGT_REP)] for p in range(3)]
+        assert whole == O.be_encode_canonical(O.get_partitions(ws))
+        agg.close()
+
+
 @pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_accumulate_chunked_threads_serialise(ipls, O, devices):
     """Four threads fold four buckets into the same partition, each as one
