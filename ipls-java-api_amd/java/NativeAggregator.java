@@ -72,7 +72,12 @@ public final class NativeAggregator implements AutoCloseable {
         return out;
     }
 
-    /** Updater._Update: client buckets -> TGT_AGG, replica partials -> TGT_REP. */
+    /** Updater._Update: client buckets -> TGT_AGG, replica partials -> TGT_REP.
+     *  One library call for the whole bucket (ipls_agg_accumulate_chunked: the
+     *  array is copied out chunk by chunk inside it), so no other thread's call
+     *  on the partition lands between two of its chunks -- the whole-bucket fold
+     *  the Updater does under PeerData.mtx (Updater.java:72-149).  A failed copy
+     *  folds nothing. */
     public void update(double[] gradient, int p, boolean fromClients) {
         if (gradient != null) accumulate(handle, p, fromClients ? TGT_AGG : TGT_REP, gradient);
     }
@@ -184,7 +189,9 @@ public final class NativeAggregator implements AutoCloseable {
         return ingestTexts(handle, fromClients ? TGT_AGG : TGT_REP, texts, layers, partitions, status);
     }
 
-    /** AggregatePartition (IPLS.java:1248-1274); returns the commit_update file bytes. */
+    /** AggregatePartition (IPLS.java:1248-1274); returns the commit_update file bytes.
+     *  One library call (ipls_agg_finalize_chunked): no cache_partition or fold of
+     *  another thread lands between the sum and its bytes. */
     public byte[] aggregatePartition(int p) {
         byte[] sum = new byte[8 * partitionLength(p)];
         finalizePartition(handle, p, sum);
