@@ -2329,8 +2329,11 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
     device folds, queued folds (coalescing group 1/4/32), batched folds with
     every start mode and byte order, AggregatePartition, resets, promotion of
     future gradients, the async blend, cache_partition, the fused round,
-    GetPartitions, and the JNI ring's ranged folds and reads from pinned memory
-    (ipls_agg_accumulate_range / ipls_agg_read_range at random even cuts).  Buckets include -0.0, subnormals and huge values so the
+    GetPartitions, the ranged folds and reads from pinned memory
+    (ipls_agg_accumulate_range / ipls_agg_read_range at random even cuts), and
+    the chunked calls (accumulate_chunked with a source that sometimes stops,
+    finalize_chunked, get_partitions_wire_chunked at random even chunk
+    sizes).  Buckets include -0.0, subnormals and huge values so the
     start-value and grouping rules show in the bits.  ``devices``: the same
     sequence through a multi-device handle (shards [0,2) | [2,4), and a
     three-entry list whose last shard owns no partition), so the front's
@@ -2385,9 +2388,11 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
 
         def draw(key, fn):
             return fixed[key] if key in fixed else fn()
-        op = draw("op", lambda: int(rng.integers(0, 19)))
+        op = draw("op", lambda: int(rng.integers(0, 22)))
         if collide and op in (8, 16) and "op" not in fixed:
             op = 14
+        if op == 21 and L > (1 << 20) and "op" not in fixed and rng.integers(0, 3):
+            op = 11                                         # the whole-model check costs ~1 s at production lengths
         p = draw("p", lambda: int(rng.integers(0, P)))
         k = int(rng.integers(0, len(pool)))
         g = pool[k]
@@ -2508,6 +2513,52 @@ def test_stateful_random_sequence(ipls, O, seed, group, devices, P=4, L=5003, st
             assert lib.ipls_agg_wait(h, tk.value) == 0
             want = O.be_encode(M[T[tg]][p]) if be else M[T[tg]][p].tobytes()
             assert pin.view()[:8 * L].tobytes() == want, f"step {step}: read_range p{p} {T[tg]} be={be}"
+        elif op == 19:                                      # one arrival pulled chunk by chunk, as one call
+            tg = [ipls.TGT_AGG, ipls.TGT_REP, ipls.TGT_FUTURE][int(rng.integers(0, 3))]
+            be = bool(rng.integers(0, 2))
+            raw = np.frombuffer(O.be_encode(g) if be else g.tobytes(), dtype=np.uint8)
+            ch = 2 * int(rng.integers(max(1, L // 4096), L // 2 + 2))
+            stop_at = int(rng.integers(0, 4)) if rng.integers(0, 5) == 0 else -1   # a failing source folds nothing
+            calls = []
+
+            @N.CHUNK_SOURCE
+            def src(ctx, dst, off, n, raw=raw, calls=calls, stop_at=stop_at):
+                calls.append(off)
+                if len(calls) - 1 == stop_at:
+                    return 1
+                ctypes.memmove(dst, raw.ctypes.data + 8 * off, 8 * n)
+                return 0
+            rc = lib.ipls_agg_accumulate_chunked(h, p, tg, L, N.HOST_BE if be else N.HOST_F64, ch, src, None)
+            if 0 <= stop_at < -(-L // min(ch, L)):
+                assert rc == N.IPLS_E_INVAL, f"step {step}: stopped source"
+            else:
+                assert rc == 0, f"step {step}: accumulate_chunked"
+                M[T[tg]][p] = M[T[tg]][p] + g
+        elif op == 20:                                      # AggregatePartition, its bytes handed over in chunks
+            be = bool(rng.integers(0, 2))
+            ch = 2 * int(rng.integers(max(1, L // 4096), L // 2 + 2))
+            out = bytearray(8 * L)
+
+            @N.CHUNK_SINK
+            def sink(ctx, vals, off, n, out=out):
+                out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+                return 0
+            assert lib.ipls_agg_finalize_chunked(h, p, N.HOST_BE if be else N.HOST_F64, ch, sink, None) == 0
+            M["w"][p] = M["agg"][p] + M["rep"][p]
+            M["agg"][p] = np.zeros(L)
+            M["rep"][p] = np.zeros(L)
+            want = O.be_encode(M["w"][p]) if be else M["w"][p].tobytes()
+            assert bytes(out) == want, f"step {step}: finalize_chunked p{p}"
+        elif op == 21:                                      # Middleware task 3, chunk by chunk
+            ch = 2 * int(rng.integers(max(1, P * L // 4096), P * L // 2 + 2))
+            got = bytearray()
+
+            @N.CHUNK_SINK
+            def wsink(ctx, vals, off, n, got=got):
+                got.extend(ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n))
+                return 0
+            assert lib.ipls_agg_get_partitions_wire_chunked(h, ch, wsink, None) == 0
+            assert bytes(got) == O.be_encode_canonical(O.get_partitions(M["w"])), f"step {step}: wire chunked"
         elif op == 15 and collide and rng.integers(0, 6):  # (collide: most collects skipped)
             pass
         elif op == 15:                                      # Collect_Replicas
