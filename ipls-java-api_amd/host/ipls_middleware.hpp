@@ -136,7 +136,7 @@ class MiddlewareServer {
   // The accept loop of Middleware.main: one task per connection.  Stops after
   // max_connections (< 0: never).  A task that fails (a short read, a library
   // error) throws, as the reference's main ends on its first exception
-  // (Middleware.java:262-265).
+  // (Middleware.java:262-265); a caller running it on a thread catches there.
   void serve(int max_connections = -1) {
     for (int served = 0; max_connections < 0 || served < max_connections; ++served) {
       const int fd = ::accept(lfd_, nullptr, nullptr);

@@ -204,7 +204,14 @@ int main(int argc, char** argv) {
                                                    "-training", "60", "-aggr", "0"});
       MiddlewareServer server(opts, 73934);
       const int port = server.listen(0);
-      std::thread srv([&] { server.serve(1 + 2 * 4); });
+      std::string srv_err;   // an exception must not leave the server thread (std::terminate)
+      std::thread srv([&] {
+        try {
+          server.serve(1 + 2 * 4);
+        } catch (const std::exception& e) {
+          srv_err = e.what();
+        }
+      });
       std::vector<std::vector<double>> peers(3, model);
       std::vector<std::vector<uint8_t>> wire(3, std::vector<uint8_t>((size_t)M * 8));
       for (int k = 0; k < 3; ++k) {
@@ -239,6 +246,7 @@ int main(int argc, char** argv) {
         throw;
       }
       srv.join();
+      CHECK(srv_err.empty(), ("server: " + srv_err).c_str());
       CHECK(server.stats().rounds == 2 && server.stats().updates == 6 && server.init().file_name == "ETHModel",
             "two rounds of three updates");
     });

@@ -152,13 +152,24 @@ int main(int argc, char** argv) {
     opts.Min_Members = K;
     MiddlewareServer server(opts, chunk);
     const int port = server.listen(0);
-    std::thread srv([&] { server.serve(1 + 2 * (K + 1)); });
+    std::string srv_err;   // an exception must not leave the server thread (std::terminate)
+    std::thread srv([&] {
+      try {
+        server.serve(1 + 2 * (K + 1));
+      } catch (const std::exception& e) {
+        srv_err = e.what();
+      }
+    });
     MiddlewareClient::init(port, (int32_t)M, "/ip4/127.0.0.1/tcp/5001", "bench");
     g[0] = client_round(port, K, ups, reply);
     st0 = server.stats();
     g[1] = client_round(port, K, ups, reply);
     st1 = server.stats();
     srv.join();
+    if (!srv_err.empty()) {
+      std::fprintf(stderr, "server: %s\n", srv_err.c_str());
+      return 6;
+    }
   }
   // the averaged model's checksum (oracle.checksum's definition) over the reply
   uint64_t sum = 0;
