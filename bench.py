@@ -1715,22 +1715,26 @@ def main():
         step()
     agg.sync()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # HIP events at the two ends of the K back-to-back launches on the handle's
+    # stream: kern_ms = their span / K, the launch's average duration (plus the
+    # ~1.6 us in-order boundary to the next launch).  An event packet around
+    # every launch added ~4.6 us each to the timed region (tools/b_gap_probe.py,
+    # profiles/r05/b_gap/), so none sits between the launches.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        evs[i][0].record(stream)
         step()
-        evs[i][1].record(stream)
+    ev1.record(stream)
     agg.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     t = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
