@@ -11,11 +11,16 @@ buckets (16 partitions x 1,048,576 doubles x 8 peers, 1.21 GB per launch):
   out_ends      as events_ends, but reduce_batch_out into caller buffers
                 (what bench.py's config_leg launches)
 
+`IPLS_PROBE_CONFIG=C` runs the headline shape instead (16 x 4,194,304 x 32,
+17.7 GB per launch): whether an event packet between launches changes the
+kernel's own duration, not only the gap.
+
 Run it under `rocprofv3 --kernel-trace` and feed the trace to
 tools/gap_split.py for the kernel-only time and the gap between launches.
 Prints one JSON line.
 """
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -27,8 +32,9 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "ipls-java-api_amd"))
 import ipls  # noqa: E402
 
-P, L, K = 16, 1048576, 8
-N, ROUNDS = 50, 6
+CFG = os.environ.get("IPLS_PROBE_CONFIG", "B")
+P, L, K = {"B": (16, 1048576, 8), "C": (16, 4194304, 32)}[CFG]
+N, ROUNDS = (50, 6) if CFG == "B" else (20, 3)
 
 
 def main():
@@ -84,7 +90,7 @@ def main():
         agg.sync()
         outs.append(a.elapsed_time(b) / N)
     me, mn = float(np.median(each)), float(np.median(ends))
-    out = {"workload": f"B: {P} x {L} x {K}, {nbytes} B per launch", "launches_per_round": N, "rounds": ROUNDS,
+    out = {"workload": f"{CFG}: {P} x {L} x {K}, {nbytes} B per launch", "launches_per_round": N, "rounds": ROUNDS,
            "events_each_ms": round(me, 5), "events_each_frac": round(nbytes / me / 8e9, 4),
            "events_ends_ms": round(mn, 5), "events_ends_frac": round(nbytes / mn / 8e9, 4),
            "out_ends_ms": round(float(np.median(outs)), 5),
