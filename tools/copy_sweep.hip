@@ -37,7 +37,13 @@ namespace ipls {
 // SWZ (round 5): blocks that share an XCD (b % 8) take a contiguous run of
 // tiles (the guide's bijective T1 remap), so the W line a tile boundary splits
 // is read by two blocks on one L2 instead of two L2s.
-template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV, bool ALIGNED = false, bool SWZ = false>
+// WC (round 5): wave-contiguous steps -- a wave's V steps cover V adjacent
+// KiB of the output instead of every wave of the block taking one KiB per
+// step -- so that, with ALIGNED, the last lane's w[i+1] is lane 0's low half
+// of the wave's NEXT step (a broadcast shuffle), and only the wave's last step
+// reads one extra double: one shared line per V KiB instead of one per KiB.
+template <bool OUT_BE, bool SECURE, int BS = kBlock, int V = kDivV, bool ALIGNED = false, bool SWZ = false,
+          bool WC = false>
 __global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ parts,
                                                const double* __restrict__ arena,
                                                unsigned long long* __restrict__ out,
@@ -86,9 +92,44 @@ __global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ pa
   if (t == 0 && threadIdx.x < head) o[threadIdx.x] = f(w[threadIdx.x]);
   const int64_t base = (int64_t)t * kTile + head;
   if (base >= n) return;
+  // element index of lane threadIdx.x's pair at step v
+  const int64_t wave_base = base + (int64_t)(threadIdx.x >> 6) * 128 * kV + 2 * (threadIdx.x & 63);
+  auto idx = [&](int v) -> int64_t {
+    if constexpr (WC) return wave_base + (int64_t)v * 128;
+    return base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+  };
   if (base + kTile <= n) {
     double x[kV][2];
-    if constexpr (ALIGNED) {
+    if constexpr (ALIGNED && WC) {
+      if ((((uintptr_t)(w + base)) & 15) == 0) {   // uniform per block
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+          const d2 a = __builtin_bit_cast(d2, __builtin_nontemporal_load((gcu2)(w + idx(v))));
+          x[v][0] = a.x;
+          x[v][1] = a.y;
+        }
+      } else {
+        u2 a[kV];
+#pragma unroll
+        for (int v = 0; v < kV; ++v) a[v] = __builtin_nontemporal_load((gcu2)(w + idx(v) - 1));   // [i-1, i]
+        const bool last = (threadIdx.x & 63) == 63;
+        unsigned long long tail = 0;
+        if (last) tail = __builtin_nontemporal_load((const __attribute__((address_space(1))) unsigned long long*)(w + idx(kV - 1) + 1));
+#pragma unroll
+        for (int v = 0; v < kV; ++v) {
+          const unsigned long long lo = a[v].x;
+          unsigned long long nx = __shfl_down(lo, 1, 64);          // w[i+1] = next lane's low half
+          if (v + 1 < kV) {
+            const unsigned long long first = __shfl((unsigned long long)a[v + 1].x, 0, 64);   // next step's lane 0
+            if (last) nx = first;
+          } else if (last) {
+            nx = tail;
+          }
+          x[v][0] = __builtin_bit_cast(double, (unsigned long long)a[v].y);
+          x[v][1] = __builtin_bit_cast(double, nx);
+        }
+      }
+    } else if constexpr (ALIGNED) {
       if ((((uintptr_t)(w + base)) & 15) == 0) {   // uniform per block
 #pragma unroll
         for (int v = 0; v < kV; ++v) {
@@ -118,14 +159,14 @@ __global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ pa
     } else {
 #pragma unroll
       for (int v = 0; v < kV; ++v) {
-        const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+        const int64_t i = idx(v);
         x[v][0] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i));
         x[v][1] = __builtin_nontemporal_load((const __attribute__((address_space(1))) double*)(w + i + 1));
       }
     }
 #pragma unroll
     for (int v = 0; v < kV; ++v) {
-      const int64_t i = base + 2 * ((int64_t)v * kBlock + threadIdx.x);
+      const int64_t i = idx(v);
       u2 v2;
       v2.x = f(x[v][0]);
       v2.y = f(x[v][1]);
@@ -134,6 +175,38 @@ __global__ __launch_bounds__(BS) void k_divide_ab(const DivDesc* __restrict__ pa
     return;
   }
   for (int64_t i = base + threadIdx.x; i < n; i += kBlock) o[i] = f(w[i]);
+}
+
+// k_finalize with wave-contiguous steps (round 5 A/B; REP logically zero, no
+// accumulator zeroing: the sweep's shape of the shipped k_finalize<true, false>)
+template <int BS = kBlock, int V = kFinV>
+__global__ __launch_bounds__(BS) void k_finalize_wc(const FinDesc* __restrict__ parts, double* __restrict__ arena,
+                                                    int tiles_per_part) {
+  constexpr int64_t kTile = (int64_t)BS * 2 * V;
+  const int q = blockIdx.x / tiles_per_part;
+  const int t = blockIdx.x - q * tiles_per_part;
+  const FinDesc d = parts[q];
+  const int64_t base = (int64_t)t * kTile;
+  if (base >= d.len) return;
+  const int64_t end = (base + kTile < d.len) ? base + kTile : d.len;
+  const double* agg = arena + d.agg_off;
+  double* w = arena + d.w_off;
+  if (end - base == kTile) {
+    const int64_t wave_base = base + (int64_t)(threadIdx.x >> 6) * 128 * V + 2 * (threadIdx.x & 63);
+    u2 a[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) a[v] = __builtin_nontemporal_load((gcu2)(agg + wave_base + (int64_t)v * 128));
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const d2 x = __builtin_bit_cast(d2, a[v]);
+      d2 o;
+      o.x = x.x + 0.0;
+      o.y = x.y + 0.0;
+      __builtin_nontemporal_store(__builtin_bit_cast(u2, o), (gu2)(w + wave_base + (int64_t)v * 128));
+    }
+    return;
+  }
+  for (int64_t i = base + threadIdx.x; i < end; i += BS) w[i] = agg[i] + 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -184,26 +257,37 @@ int main(int argc, char** argv) {
                     hipLaunchKernelGGL((k_finalize<true, false, BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_fd, arena, tpp);                                                    \
                   }})
-#define DIVX(BS, V, AL, SW, TAG)                                                                            \
+#define DIVX(BS, V, AL, SW, TAG) DIVW(BS, V, AL, SW, false, TAG)
+#define DIVW(BS, V, AL, SW, WC, TAG)                                                                            \
   vars.push_back({"divide   BS=" #BS " V=" #V TAG, div_bytes, [=](hipStream_t s) {                          \
                     const int64_t tile = (int64_t)BS * 2 * V;                                                \
                     const int tpp = (int)((L - 1 + tile - 1) / tile);                                        \
-                    hipLaunchKernelGGL((k_divide_ab<false, false, BS, V, AL, SW>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
+                    hipLaunchKernelGGL((k_divide_ab<false, false, BS, V, AL, SW, WC>), dim3((unsigned)tpp * P), dim3(BS), 0, s, \
                                        d_dd, (const double*)arena, model, tpp);                              \
                   }})
 #define DIV(BS, V) DIVX(BS, V, false, false, "")
   FIN(256, 8);   // shipped (kFinV = 8)
   FIN(256, 4);
-  DIVX(256, 4, false, false, " 8B");   // shipped: two 8-B loads per lane
-  DIVX(256, 4, false, true, " 8B xcd");   // round 5: the XCD-contiguous tile order
-  DIVX(256, 8, false, true, " 8B xcd");
+#define FINW(BS, V)                                                                                         \
+  vars.push_back({"finalize BS=" #BS " V=" #V " wc", fin_bytes, [=](hipStream_t s) {                         \
+                    const int64_t tile = (int64_t)BS * 2 * V;                                                \
+                    const int tpp = (int)((L + tile - 1) / tile);                                            \
+                    hipLaunchKernelGGL((k_finalize_wc<BS, V>), dim3((unsigned)tpp * P), dim3(BS), 0, s,     \
+                                       d_fd, arena, tpp);                                                    \
+                  }})
+  FINW(256, 8);
+  FINW(256, 4);
+#undef FINW
+  DIVX(256, 4, false, false, " 8B");   // round 4's shipped form: two 8-B loads per lane
   DIVX(256, 4, true, false, " 16B");   // round-4 A/B: 16-B loads whatever the alignment
-  DIVX(256, 4, true, true, " 16B xcd");
-  DIV(256, 8);
-  DIV(512, 8);
+  DIVW(256, 4, false, false, true, " 8B wc");    // shipped since round 5: wave-contiguous steps
+  DIVW(256, 4, true, false, true, " 16B wc");
+  DIVW(256, 8, true, false, true, " 16B wc");
+  DIVW(256, 16, true, false, true, " 16B wc");
 #undef FIN
 #undef DIV
 #undef DIVX
+#undef DIVW
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t a, b;
