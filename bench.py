@@ -330,7 +330,7 @@ def f_stream_leg(ipls, torch, device: int, P: int = 16, L: int = 8388608, K: int
 
 
 def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 4194303, K: int = 32, D: int = 4,
-                          verify: bool = True) -> dict:
+                          verify: bool = True, warm_rounds: int = 3) -> dict:
     """The north_star's host boundary at model scale: the Middleware loopback
     socket (Middleware.java:212-268) carrying K task-2 updates of M = P x Lv
     doubles (Deserialize, :156-160, 537 MB each) and one task-3 reply
@@ -351,8 +351,10 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
 
     Ceiling: the same client against a server that receives each payload into
     one pinned buffer and answers task 3 from it, with no aggregator --
-    the loopback socket alone, measured in the same process.  Two rounds:
-    the first (cold: first-use allocations) is reported beside the second.
+    the loopback socket alone, measured in the same process and listening at
+    the same time.  One cold round of each (first-use allocations), then
+    `warm_rounds` rounds alternating ceiling / aggregator: the box's CPU share
+    moves between rounds, and a pair sees the same conditions.
     The reply is checked byte for byte against the oracle's writeDouble
     stream of the fixed-order average ((((+0.0 + u_0) + u_1) ...) + 0.0) / K."""
     import socket
@@ -411,7 +413,8 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
     staging = ipls.PinnedBuffer(nbytes)
     staging.view()[::4096] = 0
     srv = listener()
-    port = srv.getsockname()[1]
+    ceil_port = srv.getsockname()[1]
+    n_rounds = 1 + warm_rounds
 
     def null_server(n_conn):
         for _ in range(n_conn):
@@ -423,34 +426,37 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
                     conn.sendall(MW.ACK)
                 elif t == 3:
                     conn.sendall(memoryview(staging.view())[:nbytes])
-    th = threading.Thread(target=null_server, args=(2 * (K + 1),), daemon=True)
-    th.start()
-    ceil = [one_round(port) for _ in range(2)]
-    th.join(60)
-    srv.close()
-    staging.close()
-    progress("middleware leg: socket ceiling done")
+    th_ceil = threading.Thread(target=null_server, args=(n_rounds * (K + 1),), daemon=True)
+    th_ceil.start()
 
-    # --- the aggregator behind the same socket
+    # --- the aggregator behind the same socket, listening at the same time
     opts = MW.parse_arguments(f"-p 0 -pa {P} -mp 1 -n {K} -i 0 -training 0 -aggr 0".split())
     got_port, daemons = [], []
     ready = threading.Event()
-    th = threading.Thread(target=MW.serve, kwargs=dict(opts=opts, max_connections=1 + 2 * (K + 1), device=device,
-                                                       ready=ready, on_listen=got_port.append,
+    th = threading.Thread(target=MW.serve, kwargs=dict(opts=opts, max_connections=1 + n_rounds * (K + 1),
+                                                       device=device, ready=ready, on_listen=got_port.append,
                                                        on_daemon=daemons.append), daemon=True)
     th.start()
     if not ready.wait(60):
         return {"error": "the middleware server did not start"}
     port = got_port[0]
     assert bytes(task(port, MW.encode_init(False, [], "/ip4/127.0.0.1/tcp/5001", "bench", M), None, 2)) == MW.ACK
-    runs = []
-    for r in range(2):
+    # rounds alternate ceiling / aggregator, so that each pair sees the same
+    # host conditions (the box's CPU share is shared); the last round is the
+    # aggregator's, whose reply is verified
+    ceil, runs = [], []
+    for r in range(n_rounds):
+        ceil.append(one_round(ceil_port))
         st0 = dict(daemons[0].stats)
         dt, t2, t3 = one_round(port)
         st1 = daemons[0].stats
         runs.append((dt, t2, t3, {"update_s": st1["update_s"] - st0["update_s"],
                                   "reply_s": st1["reply_s"] - st0["reply_s"]}))
     th.join(120)
+    th_ceil.join(60)
+    srv.close()
+    staging.close()
+    progress("middleware leg: socket ceiling and aggregator done")
     ok = None
     want_sum = None
     if verify:
@@ -464,11 +470,16 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
         ok = bool(reply.tobytes() == want)
         want_sum = O.checksum(avg)
         del vals, acc, want, avg
-    cold, warm = summary(*ceil[0]), summary(*ceil[1])
-    g_cold, g_warm = summary(*runs[0][:3]), summary(*runs[1][:3])
-    for g, rr in ((g_cold, runs[0]), (g_warm, runs[1])):
+    ceil_s = [summary(*c) for c in ceil]
+    agg_s = [summary(*rr[:3]) for rr in runs]
+    for g, rr in zip(agg_s, runs):
         g["server_ms_per_task2"] = round(1e3 * rr[3]["update_s"] / K, 2)
         g["server_ms_task3"] = round(1e3 * rr[3]["reply_s"], 2)
+    cold, g_cold = ceil_s[0], agg_s[0]
+    # the warm rounds' median pair (by the aggregator's rate), and each pair's ratio
+    ratios = [a["GBps"] / c["GBps"] for a, c in zip(agg_s[1:], ceil_s[1:])]
+    mid = sorted(range(warm_rounds), key=lambda i: agg_s[1 + i]["GBps"])[warm_rounds // 2]
+    g_warm, warm = agg_s[1 + mid], ceil_s[1 + mid]
     del ups, reply
     # the same traffic through the native server (host/ipls_middleware.hpp, Middleware.main in C++ over the
     # C-ABI) and a native client: tools/middleware_e2e.cpp, a child process, the same update vectors
@@ -490,6 +501,8 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
     return {"workload": f"Middleware over TCP loopback: -pa {P} -n {K}, model {M} doubles ({nbytes / 1e6:.0f} MB per "
                         f"task): {K} task-2 updates + 1 task-3 reply per round, one connection per task",
             "GBps": g_warm["GBps"], "ceiling_GBps": warm["GBps"], "frac_of_ceiling": round(g_warm["GBps"] / warm["GBps"], 4),
+            "frac_of_ceiling_per_round": [round(x, 4) for x in ratios],
+            "GBps_per_round": [a["GBps"] for a in agg_s[1:]], "ceiling_GBps_per_round": [c["GBps"] for c in ceil_s[1:]],
             "aggregator": g_warm, "aggregator_cold_round": g_cold, "socket_ceiling": warm,
             "socket_ceiling_cold_round": cold, "verified_task3_bytes": ok, "prep_s": round(prep_s, 1),
             "native": native,
@@ -500,6 +513,8 @@ def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 41943
                     "sent chunk by chunk from the pinned ring (ipls_agg_get_partitions_wire_chunked).  "
                     "server_ms_*: time inside the aggregator's socket handlers (socket reads/writes included).  "
                     "Ceiling = the same socket traffic into / out of one pinned buffer with no aggregator.  "
+                    f"One cold round of each, then {warm_rounds} warm rounds alternating ceiling / aggregator; "
+                    "the headline pair is the warm round with the median aggregator rate.  "
                     "Python server and client threads in one process"}
 
 
