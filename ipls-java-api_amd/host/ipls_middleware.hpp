@@ -137,6 +137,8 @@ class MiddlewareServer {
   // max_connections (< 0: never).  A task that fails (a short read, a library
   // error) throws, as the reference's main ends on its first exception
   // (Middleware.java:262-265); a caller running it on a thread catches there.
+  // A task-2 connection that ends mid-update leaves the partitions received
+  // before it folded (each partition is one call; the one cut short is not).
   void serve(int max_connections = -1) {
     for (int served = 0; max_connections < 0 || served < max_connections; ++served) {
       const int fd = ::accept(lfd_, nullptr, nullptr);
