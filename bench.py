@@ -897,9 +897,13 @@ def config_leg(ipls, torch, name: str, be: bool, device: int, steps: int = 5, ve
     # packet after every launch added 4.6 us to each 0.18 ms B launch (2.5 % of
     # the line, tools/b_gap_probe.py, profiles/r05/b_gap/); what remains
     # between launches is the in-order dependent-launch boundary (~1.6 us)
+    # and one untimed launch before the first event keeps the GPU busy while the
+    # timed ones are issued, so the first launch's host latency (~55 us per
+    # call here) is not in the span
     per_round = []
     for _ in range(rounds):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        step()
         ev0.record(stream)
         for i in range(steps):
             step()
@@ -1018,6 +1022,7 @@ def few_partitions_leg(ipls, torch, device: int, P: int = 3, L: int = 4194304, K
         fn()
         agg.sync()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()   # untimed, in flight while the timed launches are issued
         e0.record(stream)
         for _ in range(steps):
             fn()
@@ -1220,6 +1225,7 @@ def round_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, kern_ms: f
     # config legs), the steady-state per-launch time
     agg.sync()
     d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    agg.GetPartitions(out=fb)   # untimed, in flight while the timed launches are issued (no launch latency in d0..d1)
     d0.record(stream)
     for _ in range(20):
         agg.GetPartitions(out=fb)
