@@ -49,6 +49,71 @@ CONFIGS = {
 }
 
 
+# The 1-GPU numbers the multi-GPU prediction starts from:
+# config C's k_reduce on the round-5 library over the round's boxes
+# (profiles/r05/q, r05/t and the driver's BENCH_r05: 2.4814-2.5193 ms).
+ONE_GPU_C_MS = (2.48, 2.54)
+
+
+def spread_sources(owner: int, world: int, P: int) -> dict:
+    """ReplicaPlan.spread (ipls.distributed) / c_abi_multi_gpu's slot map:
+    the q-th partition of `owner` has its replica partial on GPU
+    (owner + 1 + q mod (G-1)) mod G.  Returns {source GPU: partials}."""
+    cnt = {}
+    for q in range(P):
+        s = (owner + 1 + q % (world - 1)) % world
+        cnt[s] = cnt.get(s, 0) + 1
+    return cnt
+
+
+def scaling_prediction(world: int, P: int = 16, L: int = 4194304, K: int = 32) -> dict:
+    """What an N-GPU run of this bench should read, written before any such
+    run (the table of DESIGN.md §6.1 is this function's
+    output).  Weak scaling: every GPU folds its own config-C slice from its
+    own HBM, so the fold time stays the 1-GPU one and the line's value is
+    N x the per-GPU rate over the slowest rank's time.  The exchange legs are
+    bounded by xGMI: one link per GPU pair, XGMI_LINK_GBS per direction, and
+    the spread schedule pulls each owner's P partials (L doubles each) from
+    its G-1 peers -- ceil(P / (G-1)) over the busiest link."""
+    fold_bytes = P * (K + 1) * L * 8
+    lo, hi = ONE_GPU_C_MS
+    pred = {"link_GBps": XGMI_LINK_GBS, "fold_ms_per_gpu": [lo, hi],
+            "value_GBps": [round(world * fold_bytes / hi / 1e6, 0), round(world * fold_bytes / lo / 1e6, 0)]}
+    if world > 1:
+        part = L * 8
+        busiest = max(spread_sources(0, world, P).values())
+        links = min(world - 1, P)
+        pred.update({
+            "partials_per_owner": P, "partial_bytes": part, "links_per_owner": links,
+            "busiest_link_partials": busiest,
+            # c_abi_multi_gpu's combine and replica_exchange's RCCL exchange move the same bytes
+            "combine_ms_at_link_peak": round(busiest * part / (XGMI_LINK_GBS * 1e9) * 1e3, 3),
+            "combine_ms_even_links": round(P * part / (links * XGMI_LINK_GBS * 1e9) * 1e3, 3),
+            "frac_of_xgmi_if_busiest_link_saturated": round(P / (links * busiest), 4),
+            "e2e_GBps_per_gpu_pcie_bound": PCIE_GBS,
+        })
+    return pred
+
+
+def scaling_check(world: int, out: dict) -> dict:
+    """The N > 1 line's prediction next to what this run measured, compact
+    and near the end of the line (the driver keeps its stdout tail)."""
+    m = {"value_GBps": out.get("value"), "ms_per_step": out.get("ms_per_step")}
+    ml = out.get("c_abi_multi_gpu") or {}
+    cb = ml.get("combine") or {}
+    for k in ("owner_kernel_ms", "frac_of_xgmi", "frac_of_xgmi_min", "xgmi_link_GBps", "status"):
+        if k in cb:
+            m[f"combine_{k}" if not k.startswith("combine") else k] = cb[k]
+    rx = out.get("replica_exchange") or {}
+    for k in ("exchange_ms", "exchange_GBps_per_rank_each_way"):
+        if k in rx:
+            m[f"replica_{k}"] = rx[k]
+    e2e = out.get("host_inclusive_multi") or {}
+    if "GBps_per_gpu_min" in e2e:
+        m["e2e_GBps_per_gpu_min"] = e2e["GBps_per_gpu_min"]
+    return {"predicted": scaling_prediction(world), "measured": m, "source": "DESIGN.md §6.1"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1546,7 +1611,7 @@ def claim_stdout() -> None:
         os.dup2(2, 1)
 
 
-TAIL_KEYS = ("verified", "verified_partitions", "build")
+TAIL_KEYS = ("scaling_check", "verified", "verified_partitions", "build")
 BUILD_TAIL = ("so_sha256", "device_code_sha256", "built_utc", "stamp_matches_so", "sources_match")
 
 
@@ -1654,8 +1719,11 @@ def plumbing_selftest(args) -> None:
     ranks = [None] * dist.get_world_size()
     dist.all_gather_object(ranks, me)
     if rank == 0:
-        emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "selftest": "plumbing",
-              "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks}})
+        line = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "selftest": "plumbing",
+                "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "ranks": ranks}}
+        if world > 1:
+            line["scaling_check"] = scaling_check(world, line)
+        emit(line)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -1966,6 +2034,8 @@ def main():
     if dog is not None:
         dog.cancel()          # every leg finished: the line is printed once, here
                               # (if the dog fired first, it printed and exits)
+    if out is not None and world > 1:
+        out["scaling_check"] = scaling_check(world, out)
     if out is not None:
         emit(out)
     agg.close()

@@ -32,6 +32,13 @@
  *    bucket (ipls_agg_accumulate, or ipls_agg_accumulate_chunked for a
  *    caller that produces the bucket chunk by chunk), AggregatePartition plus
  *    its commit_update bytes (ipls_agg_finalize, ipls_agg_finalize_chunked).
+ *    A chunked call takes effect, as one unit, at one instant: an
+ *    accumulate_chunked when its last chunk has landed on the GPU (as
+ *    Middleware's Deserialize reads the whole stream before UpdateModel takes
+ *    PeerData.mtx, Middleware.java:224, 246), a finalize_chunked /
+ *    get_partitions(_wire)_chunked when it takes its snapshot, before the
+ *    first chunk is delivered.  No shard lock is held while the caller's
+ *    source or sink runs, so a blocking one (a socket) holds up nobody else.
  *    ipls_agg_accumulate_range / ipls_agg_read_range are single calls too:
  *    a caller that splits one arrival into ranges holds its own lock across
  *    them (PeerData.mtx, Updater.java:72-149) or gets a mixed order.
@@ -126,8 +133,9 @@ typedef struct ipls_agg_cfg {
 
 /* Caller callbacks of the chunked calls (ipls_agg_get_partitions_chunked,
  * ipls_agg_finalize_chunked: sink; ipls_agg_accumulate_chunked: source).
- * They run on the calling thread, inside the call, and must not call into
- * the same handle. */
+ * They run on the calling thread, inside the call, with no library lock held:
+ * they may block (a socket recv/send -- bound it with a timeout, the call
+ * waits for its callback) and may call into the same handle. */
 typedef int (*ipls_chunk_sink)(void *ctx, const double *values, int64_t offset, int64_t n);
 typedef int (*ipls_chunk_source)(void *ctx, void *dst, int64_t offset, int64_t n);
 
@@ -230,11 +238,15 @@ int ipls_agg_accumulate_range(ipls_agg *h, int p, int target, const void *src, i
  *    values past L_p are never asked for.
  *  - All or nothing: a non-zero source return stops the call with
  *    IPLS_E_INVAL and nothing folded.
- *  - The shard's lock is held from the first source call to the fold's
- *    launch, so no other caller's call on this GPU shard lands in between:
- *    the bits are those of ipls_agg_accumulate on the whole bucket, in call
- *    order.  The source must not call into this handle.
- * The JNI shim's accumulate(double[]) source is GetDoubleArrayRegion. */
+ *  - The chunks land in staging of this call's own, with no lock held; the
+ *    shard's lock is taken once every chunk has landed, for the fold alone.
+ *    So the bucket takes effect as one unit at that instant (a fold another
+ *    thread makes into the same target while the source is still producing
+ *    lands before it): the bits are those of ipls_agg_accumulate on the whole
+ *    bucket at that point of the call order.  A slow source holds up no other
+ *    caller of the shard.
+ * The JNI shim's accumulate(double[]) source is GetDoubleArrayRegion; the
+ * Middleware servers' is a socket recv. */
 int ipls_agg_accumulate_chunked(ipls_agg *h, int p, int target, int64_t n, int src_kind, int64_t chunk,
                                 ipls_chunk_source source, void *ctx);
 
@@ -412,12 +424,15 @@ int ipls_agg_finalize(ipls_agg *h, int p, void *sum_out, int sum_kind, double *a
  * consecutive ranges of [0, L_p), so the sink's copy of one chunk overlaps
  * the transfer of the next.  values: n 8-byte values, doubles (HOST_F64) or
  * the commit_update file bytes (HOST_BE, update_file's putDouble order,
- * MyIPFSClass.java:105-116), valid during the sink call only.  The shard's
- * lock is held throughout, so no set_weights, fold or finalize of another
- * thread tears the bytes.  A non-zero sink return stops the delivery with
+ * MyIPFSClass.java:105-116), valid during the sink call only.  Under the
+ * shard's lock the call runs AggregatePartition and snapshots W (or its
+ * bytes) into staging of its own; the lock is released before the first sink
+ * call.  So the bytes are this call's W whatever set_weights, fold or
+ * finalize another thread makes meanwhile (never torn), and a slow sink
+ * holds up nobody.  A non-zero sink return stops the delivery with
  * IPLS_E_INVAL; the round is consumed either way (W is written, AGG = REP =
- * 0), as after a failed update_file.  The sink must not call into this
- * handle.  The JNI shim's finalizePartition(byte[]) sink is SetByteArrayRegion. */
+ * 0), as after a failed update_file.  The JNI shim's finalizePartition(byte[])
+ * sink is SetByteArrayRegion. */
 int ipls_agg_finalize_chunked(ipls_agg *h, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void *ctx);
 
 /* A whole aggregation round for partitions [p_first, p_first+n_parts) in ONE
@@ -450,13 +465,16 @@ int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
 
 /* GetPartitions (IPLS.java:1159-1174) delivered in chunks of `chunk` doubles
  * (even, >= 2) to sink(ctx, values, offset, n) on the calling thread, in
- * model order: the divide runs once on the GPU, then each chunk comes back
- * through a pinned two-slot ring, so the sink's copy of chunk k overlaps the
- * transfer of chunk k + 1 (the JNI getPartitions(double[]) copies each chunk
- * into the Java array with SetDoubleArrayRegion).  `values` is valid only
- * during the sink call.  A non-zero sink return stops the transfer: the call
- * returns IPLS_E_INVAL and no further chunk is delivered.  The sink must not
- * call into this handle.  Replaces the same loop as ipls_agg_get_partitions. */
+ * model order: the divide runs once on the GPU into staging of this call's
+ * own -- every shard's, each under its shard lock for that launch only,
+ * before any chunk is delivered, so the whole model is one snapshot -- then
+ * each chunk comes back through a pinned two-slot ring with no lock held, so
+ * the sink's copy of chunk k overlaps the transfer of chunk k + 1 (the JNI
+ * getPartitions(double[]) copies each chunk into the Java array with
+ * SetDoubleArrayRegion).  `values` is valid only during the sink call.  A
+ * non-zero sink return stops the transfer: the call returns IPLS_E_INVAL and
+ * no further chunk is delivered.  Replaces the same loop as
+ * ipls_agg_get_partitions. */
 int ipls_agg_get_partitions_chunked(ipls_agg *h, int64_t chunk, ipls_chunk_sink sink, void *ctx);
 
 /* The same delivery as Middleware task 3's reply (Serialize, Middleware.java:

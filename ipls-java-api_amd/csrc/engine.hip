@@ -55,6 +55,26 @@ struct PinnedSlot {
 
 }  // namespace
 
+// The staging of one chunked call (accumulate / finalize / get_partitions
+// _chunked), owned by that call alone from acquire to release, so the
+// caller's source or sink -- a socket recv/send, a JNI array copy -- runs
+// with no engine lock held.  A pinned two-slot host ring,
+// a device buffer for the whole bucket (or snapshot) and a copy stream of its
+// own.  Stages are pooled per shard and freed only at close.
+// Invariants at release: every pinned slot whose copy may still be in flight
+// is `pending` (its event recorded after that copy); `free_pending` says a
+// kernel on the shard stream may still read `d` (recorded after it).
+struct ipls_stage {
+  hipStream_t copy = nullptr;
+  PinnedSlot slot[2];
+  void* d = nullptr;
+  size_t d_cap = 0;
+  hipEvent_t landed = nullptr;    // copy stream -> shard stream: every chunk is in `d`
+  hipEvent_t ready = nullptr;     // shard stream -> copy stream: the snapshot is in `d`
+  hipEvent_t free_ev = nullptr;   // shard stream: the fold that read `d` has run
+  bool free_pending = false;
+};
+
 struct ipls_dev {
   std::mutex mu;
   std::string err;
@@ -85,11 +105,11 @@ struct ipls_dev {
   std::vector<unsigned char> last_table;  // cache of the last uploaded table
   int last_slot = -1;
 
-  // pinned two-slot rings of the chunked calls (lazily, freed at close):
-  // device -> host (get_partitions_chunked, finalize_chunked) and host ->
-  // device (accumulate_chunked)
-  PinnedSlot out_ring[2];
-  PinnedSlot in_ring[2];
+  // staging of the chunked calls: one per concurrent call, pooled (lazily,
+  // freed at close); stage_mu guards the pool only, never taken with mu held
+  // for longer than a push
+  std::mutex stage_mu;
+  std::vector<ipls_stage*> stage_all, stage_idle;
   // staging
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -240,6 +260,116 @@ int ensure_pinned(ipls_dev* h, PinnedSlot& s, size_t bytes) {
     s.cap = cap;
   }
   if (!s.ev) HIP_TRY(h, hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+  return IPLS_OK;
+}
+
+// ---- chunked-call staging (ipls_stage) ----
+// A failure outside the engine lock: the calling thread's message, and the
+// handle's under its lock (h->err is shared with the locked paths).
+int fail_nl(ipls_dev* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_tls_err = buf;
+  if (h) {
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->err = buf;
+  }
+  return code;
+}
+
+#define HIP_TRY_NL(h, expr)                                                             \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      (void)hipGetLastError();                                                          \
+      return fail_nl((h), e_ == hipErrorOutOfMemory ? IPLS_E_NOMEM : IPLS_E_DEVICE,     \
+                     "%s failed: %s", #expr, hipGetErrorString(e_));                    \
+    }                                                                                   \
+  } while (0)
+
+// Take an idle stage of the pool (or make one) and size it: `dev_bytes` of
+// device buffer, two pinned slots of `slot_bytes`.  Called with the engine
+// lock NOT held, on the shard's device.  Regrowing frees only memory this
+// call owns, after the copies and the kernel that last used it are done.
+int stage_acquire(ipls_dev* h, size_t dev_bytes, size_t slot_bytes, ipls_stage** out) {
+  *out = nullptr;
+  ipls_stage* st = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(h->stage_mu);
+    if (!h->stage_idle.empty()) {
+      st = h->stage_idle.back();
+      h->stage_idle.pop_back();
+    } else {
+      st = new ipls_stage();
+      h->stage_all.push_back(st);
+    }
+  }
+  auto give_back = [&](int rc) {
+    std::lock_guard<std::mutex> lk(h->stage_mu);
+    h->stage_idle.push_back(st);
+    return rc;
+  };
+  auto try_hip = [&](hipError_t e, const char* what) -> int {
+    if (e == hipSuccess) return IPLS_OK;
+    (void)hipGetLastError();
+    return fail_nl(h, e == hipErrorOutOfMemory ? IPLS_E_NOMEM : IPLS_E_DEVICE, "%s failed: %s", what,
+                   hipGetErrorString(e));
+  };
+  int rc = IPLS_OK;
+  if (!st->copy) rc = try_hip(hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking), "hipStreamCreate");
+  for (hipEvent_t* e : {&st->landed, &st->ready, &st->free_ev})
+    if (!rc && !*e) rc = try_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+  if (!rc && st->d_cap < dev_bytes) {
+    if (st->d) {
+      if (st->free_pending) rc = try_hip(hipEventSynchronize(st->free_ev), "hipEventSynchronize");
+      if (!rc) rc = try_hip(hipStreamSynchronize(st->copy), "hipStreamSynchronize");
+      if (!rc) rc = try_hip(hipFree(st->d), "hipFree");
+      if (!rc) {
+        st->d = nullptr;
+        st->d_cap = 0;
+        st->free_pending = false;
+      }
+    }
+    const size_t cap = (size_t)align_up((int64_t)dev_bytes, 1 << 20);
+    if (!rc) rc = try_hip(hipMalloc(&st->d, cap), "hipMalloc");
+    if (!rc) st->d_cap = cap;
+  }
+  for (auto& s : st->slot) {
+    if (rc) break;
+    if (s.cap < slot_bytes) {
+      if (s.pending) rc = try_hip(hipEventSynchronize(s.ev), "hipEventSynchronize");
+      if (!rc) s.pending = false;
+      if (!rc && s.host) rc = try_hip(hipHostFree(s.host), "hipHostFree");
+      if (!rc) {
+        s.host = nullptr;
+        s.cap = 0;
+        const size_t cap = std::max<size_t>(slot_bytes, 64 << 10);
+        rc = try_hip(hipHostMalloc(&s.host, cap, hipHostMallocDefault), "hipHostMalloc");
+        if (!rc) s.cap = cap;
+      }
+    }
+    if (!rc && !s.ev) rc = try_hip(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate");
+  }
+  if (rc) return give_back(rc);
+  *out = st;
+  return IPLS_OK;
+}
+
+void stage_release(ipls_dev* h, ipls_stage* st) {
+  if (!st) return;
+  std::lock_guard<std::mutex> lk(h->stage_mu);
+  h->stage_idle.push_back(st);
+}
+
+// The host may write pinned slot k & 1 again: the copy that last read it is done.
+int stage_slot_free(ipls_dev* h, PinnedSlot& sl) {
+  if (sl.pending) {
+    HIP_TRY_NL(h, hipEventSynchronize(sl.ev));
+    sl.pending = false;
+  }
   return IPLS_OK;
 }
 
@@ -963,13 +1093,19 @@ int dev_close(ipls_dev* h) {
     if (s.host) hipHostFree(s.host);
     if (s.ev) hipEventDestroy(s.ev);
   }
-  for (auto& s : h->out_ring) {
-    if (s.host) hipHostFree(s.host);
-    if (s.ev) hipEventDestroy(s.ev);
-  }
-  for (auto& s : h->in_ring) {
-    if (s.host) hipHostFree(s.host);
-    if (s.ev) hipEventDestroy(s.ev);
+  for (ipls_stage* st : h->stage_all) {
+    if (st->copy) {
+      hipStreamSynchronize(st->copy);
+      hipStreamDestroy(st->copy);
+    }
+    for (auto& s : st->slot) {
+      if (s.host) hipHostFree(s.host);
+      if (s.ev) hipEventDestroy(s.ev);
+    }
+    if (st->d) hipFree(st->d);
+    for (hipEvent_t e : {st->landed, st->ready, st->free_ev})
+      if (e) hipEventDestroy(e);
+    delete st;
   }
   if (h->copy_ev) hipEventDestroy(h->copy_ev);
   for (hipStream_t cs : h->copy_stream)
@@ -1307,46 +1443,139 @@ int dev_accumulate_range(ipls_dev* h, int p, int target, const void* src, int64_
 }
 
 // One arrival produced by the caller chunk by chunk, as one call (Updater's
-// whole-bucket fold under PeerData.mtx, Updater.java:72-149, 115-117).  The
-// engine lock is held from the first source call to the fold's launch, so no
-// other caller's call on this shard lands inside the arrival -- the ordering
-// that per-range calls (dev_accumulate_range) cannot give.  Chunk k is filled
-// by source() into pinned slot k % 2 and sent to the device scratch by the
-// copy engine while the source fills chunk k + 1; the fold of the whole
-// bucket runs once every chunk has landed (one launch from HBM, 24 B per
-// element), so a source that stops leaves the target untouched.
+// whole-bucket fold under PeerData.mtx, Updater.java:72-149, 115-117).
+// Chunk k is filled by source() into pinned slot k % 2 of a staging of this
+// call's own and sent to its device buffer on the stage's copy stream while
+// the source fills chunk k + 1 -- all with NO engine lock held, so a source
+// that blocks (a socket recv) stalls only this call.  Once every chunk has
+// landed, the lock is taken for the fold alone: the shard stream waits for
+// the copies (an event, no host wait) and folds the whole bucket in one launch
+// (24 B per element).  So the arrival takes effect, as one unit, when its last
+// chunk has landed -- the reference's order: Middleware's Deserialize reads
+// the whole stream before UpdateModel takes PeerData.mtx (Middleware.java:224,
+// 246).  A source that stops leaves the target untouched.
 int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_kind, int64_t chunk,
                            ipls_chunk_source source, void* ctx) {
-  if (!h || !source) return fail(h, IPLS_E_INVAL, "null argument");
-  if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
-  IPLS_LOCK(h);   // earlier queued device buckets fold first
-  if (int rc = check_part(h, p)) return rc;
-  if (target_off(h, p, target) < 0) return fail(h, IPLS_E_INVAL, "bad target %d", target);
+  if (!h || !source) return fail_nl(h, IPLS_E_INVAL, "null argument");
+  if (chunk < 2 || (chunk & 1))
+    return fail_nl(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
+  // geometry is fixed at open: validated without the lock
+  if (p < 0 || p >= h->P) return fail_nl(h, IPLS_E_RANGE, "partition %d out of range [0,%d)", p, h->P);
+  if (target_off(h, p, target) < 0) return fail_nl(h, IPLS_E_INVAL, "bad target %d", target);
   if (src_kind != IPLS_HOST_F64 && src_kind != IPLS_HOST_BE)
-    return fail(h, IPLS_E_INVAL, "a chunked fold takes HOST_F64 or HOST_BE values, not kind %d", src_kind);
+    return fail_nl(h, IPLS_E_INVAL, "a chunked fold takes HOST_F64 or HOST_BE values, not kind %d", src_kind);
   const int64_t L = h->len[p];
-  if (int rc = host_decode_count(src_kind, n, L, h)) return rc;   // before any source call
-  HIP_TRY(h, dev_use(h->device));
-  if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+  if (n < L)   // before any source call (Updater.java:115)
+    return fail_nl(h, IPLS_E_RANGE, "bucket of %lld doubles shorter than partition length %lld", (long long)n,
+                   (long long)L);
+  HIP_TRY_NL(h, dev_use(h->device));
   const int64_t c = std::min(chunk, L);
-  for (auto& sl : h->in_ring)
-    if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;
-  unsigned long long* d_in = (unsigned long long*)h->d_scratch;
-  for (int64_t k = 0, off = 0; off < L; ++k, off += c) {
-    PinnedSlot& sl = h->in_ring[k & 1];
-    if (sl.pending) {   // the copy of chunk k - 2 still reads this slot
-      HIP_TRY(h, hipEventSynchronize(sl.ev));
-      sl.pending = false;
+  ipls_stage* st = nullptr;
+  if (int rc = stage_acquire(h, (size_t)L * 8, (size_t)c * 8, &st)) return rc;
+  unsigned long long* d_in = (unsigned long long*)st->d;
+  int rc = IPLS_OK;
+  auto try_hip = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && !rc) {
+      (void)hipGetLastError();
+      rc = fail_nl(h, IPLS_E_DEVICE, "%s failed: %s", what, hipGetErrorString(e));
     }
+  };
+  // the fold that last read the device buffer runs before these copies overwrite it
+  if (st->free_pending) try_hip(hipStreamWaitEvent(st->copy, st->free_ev, 0), "hipStreamWaitEvent");
+  for (int64_t k = 0, off = 0; off < L && !rc; ++k, off += c) {
+    PinnedSlot& sl = st->slot[k & 1];
+    if ((rc = stage_slot_free(h, sl))) break;   // the copy of chunk k - 2 still reads this slot
     const int64_t len = std::min(c, L - off);
-    if (source(ctx, sl.host, off, len) != 0)
-      return fail(h, IPLS_E_INVAL, "the chunk source stopped at offset %lld: nothing folded", (long long)off);
-    HIP_TRY(h, hipMemcpyAsync(d_in + off, sl.host, (size_t)len * 8, hipMemcpyHostToDevice, h->stream));
-    HIP_TRY(h, hipEventRecord(sl.ev, h->stream));
-    sl.pending = true;
+    if (source(ctx, sl.host, off, len) != 0) {
+      rc = fail_nl(h, IPLS_E_INVAL, "the chunk source stopped at offset %lld: nothing folded", (long long)off);
+      break;
+    }
+    try_hip(hipMemcpyAsync(d_in + off, sl.host, (size_t)len * 8, hipMemcpyHostToDevice, st->copy), "hipMemcpyAsync");
+    try_hip(hipEventRecord(sl.ev, st->copy), "hipEventRecord");
+    if (!rc) sl.pending = true;
   }
-  const void* bl[1] = {d_in};
-  return reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target);
+  if (!rc) try_hip(hipEventRecord(st->landed, st->copy), "hipEventRecord");
+  if (rc) {
+    // nothing folded; the copies already queued finish before the stage is reused
+    (void)hipStreamSynchronize(st->copy);
+    (void)hipGetLastError();
+    for (auto& sl : st->slot) sl.pending = false;
+    stage_release(h, st);
+    return rc;
+  }
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    rc = flush_pending(h);   // earlier queued device buckets fold first
+    if (!rc) {
+      const hipError_t e = hipStreamWaitEvent(h->stream, st->landed, 0);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        rc = fail(h, IPLS_E_DEVICE, "hipStreamWaitEvent failed: %s", hipGetErrorString(e));
+      }
+    }
+    const void* bl[1] = {d_in};
+    if (!rc) rc = reduce_dev(h, p, 1, bl, 1, src_kind == IPLS_HOST_BE, IPLS_START_ACCUM, target);
+    // whatever ran, nothing queued on the shard stream after this point reads `d`
+    if (hipEventRecord(st->free_ev, h->stream) == hipSuccess) {
+      st->free_pending = true;
+    } else {
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(h->stream);
+      st->free_pending = false;
+    }
+  }
+  if (rc) {   // the shard stream may not have waited for the copies: drain them
+    (void)hipStreamSynchronize(st->copy);
+    (void)hipGetLastError();
+  }
+  stage_release(h, st);
+  return rc;
+}
+
+// Hand n values of a stage's device snapshot (complete once st->ready fires)
+// to the sink in chunks of c, with no engine lock held: chunk k + 1 crosses
+// PCIe into one pinned slot on the stage's copy stream while sink() consumes
+// chunk k from the other.  `base` is added to the offsets the sink sees.
+// Releases the stage.
+static int stage_deliver(ipls_dev* h, ipls_stage* st, int64_t n, int64_t c, int64_t base, ipls_chunk_sink sink, void* ctx,
+                  const char* stopped_note) {
+  const double* d = (const double*)st->d;
+  int rc = IPLS_OK;
+  auto try_hip = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && !rc) {
+      (void)hipGetLastError();
+      rc = fail_nl(h, IPLS_E_DEVICE, "%s failed: %s", what, hipGetErrorString(e));
+    }
+  };
+  try_hip(hipStreamWaitEvent(st->copy, st->ready, 0), "hipStreamWaitEvent");
+  const int64_t K = n > 0 ? (n + c - 1) / c : 0;
+  auto issue = [&](int64_t k) {
+    PinnedSlot& sl = st->slot[k & 1];
+    const int64_t off = k * c, len = std::min(c, n - off);
+    try_hip(hipMemcpyAsync(sl.host, d + off, (size_t)len * 8, hipMemcpyDeviceToHost, st->copy), "hipMemcpyAsync");
+    try_hip(hipEventRecord(sl.ev, st->copy), "hipEventRecord");
+  };
+  if (K > 0) issue(0);
+  for (int64_t k = 0; k < K && !rc; ++k) {
+    if (k + 1 < K) issue(k + 1);   // into the slot chunk k - 1 used, whose sink has returned
+    if (rc) break;
+    PinnedSlot& sl = st->slot[k & 1];
+    try_hip(hipEventSynchronize(sl.ev), "hipEventSynchronize");
+    if (rc) break;
+    const int64_t off = k * c, len = std::min(c, n - off);
+    if (sink(ctx, (const double*)sl.host, base + off, len) != 0)
+      rc = fail_nl(h, IPLS_E_INVAL, "the chunk sink stopped the transfer at offset %lld%s", (long long)(base + off),
+                   stopped_note);
+  }
+  // every copy of this call is done before the stage can be reused (on the
+  // success path they already are: each chunk's event was waited for)
+  if (rc) {
+    (void)hipStreamSynchronize(st->copy);
+    (void)hipGetLastError();
+  }
+  for (auto& sl : st->slot) sl.pending = false;
+  stage_release(h, st);
+  return rc;
 }
 
 // The reverse: target[off..off+n) of partition p into pinned host memory,
@@ -1652,55 +1881,57 @@ int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_ou
 }
 
 // AggregatePartition of one partition with the commit_update bytes (or the
-// sum as doubles) handed to a sink chunk by chunk, as one call: W = AGG + REP,
-// then W comes back through the pinned two-slot ring, chunk k + 1 in flight
-// while sink() copies chunk k.  The engine lock spans the whole sequence, so
-// no set_weights / fold / finalize of another caller tears the bytes (the
-// per-range reads of dev_read_range cannot promise that).
+// sum as doubles) handed to a sink chunk by chunk, as one call.  Under the
+// engine lock: W = AGG + REP and a snapshot of W (or of its big-endian bytes)
+// into this call's own staging -- one kernel or copy on the shard stream.
+// The lock is then released and the snapshot goes to the sink through the
+// pinned two-slot ring, chunk k + 1 in flight while sink() copies chunk k.
+// The bytes are the W of this call's AggregatePartition whatever another
+// caller's set_weights / fold / finalize does meanwhile (the per-range reads
+// of dev_read_range cannot promise that), and a slow sink (a socket send)
+// holds nothing: the reference writes after Get_Partitions has returned
+// (Middleware.java:254).
 int dev_finalize_chunked(ipls_dev* h, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
-  if (!h || !sink) return fail(h, IPLS_E_INVAL, "null argument");
-  if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
-  IPLS_LOCK(h);
-  if (int rc = check_part(h, p)) return rc;
+  if (!h || !sink) return fail_nl(h, IPLS_E_INVAL, "null argument");
+  if (chunk < 2 || (chunk & 1))
+    return fail_nl(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
+  if (p < 0 || p >= h->P) return fail_nl(h, IPLS_E_RANGE, "partition %d out of range [0,%d)", p, h->P);
   if (sum_kind != IPLS_HOST_F64 && sum_kind != IPLS_HOST_BE)
-    return fail(h, IPLS_E_INVAL, "sum_kind must be HOST_F64 or HOST_BE");
+    return fail_nl(h, IPLS_E_INVAL, "sum_kind must be HOST_F64 or HOST_BE");
   const int64_t L = h->len[p];
-  HIP_TRY(h, dev_use(h->device));
-  // every buffer first: a failure here leaves the round in place
-  if (sum_kind == IPLS_HOST_BE)
-    if (int rc = ensure_scratch(h, (size_t)L * 8)) return rc;
+  HIP_TRY_NL(h, dev_use(h->device));
   const int64_t c = std::min(chunk, L);
-  for (auto& sl : h->out_ring)
-    if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;
-  if (int rc = finalize_range(h, p, 1)) return rc;
-  const unsigned long long* w = (const unsigned long long*)(h->arena + h->w_off[p]);
-  if (sum_kind == IPLS_HOST_BE) {
-    launch_bswap(h->stream, w, (unsigned long long*)h->d_scratch, L);
-    HIP_TRY(h, hipGetLastError());
-    w = (const unsigned long long*)h->d_scratch;
-  }
-  const int64_t K = (L + c - 1) / c;
-  auto issue = [&](int64_t k) -> int {
-    PinnedSlot& sl = h->out_ring[k & 1];
-    const int64_t off = k * c, len = std::min(c, L - off);
-    HIP_TRY(h, hipMemcpyAsync(sl.host, w + off, (size_t)len * 8, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipEventRecord(sl.ev, h->stream));
-    return IPLS_OK;
-  };
-  if (int rc = issue(0)) return rc;
-  for (int64_t k = 0; k < K; ++k) {
-    if (k + 1 < K)   // into the slot chunk k - 1 used, whose sink has returned
-      if (int rc = issue(k + 1)) return rc;
-    PinnedSlot& sl = h->out_ring[k & 1];
-    HIP_TRY(h, hipEventSynchronize(sl.ev));
-    const int64_t off = k * c, len = std::min(c, L - off);
-    if (sink(ctx, (const double*)sl.host, off, len) != 0) {
-      HIP_TRY(h, hipStreamSynchronize(h->stream));   // the copy still writing the other slot
-      return fail(h, IPLS_E_INVAL, "the chunk sink stopped the transfer at offset %lld (the round is consumed)",
-                  (long long)off);
+  // every buffer first: a failure here leaves the round in place
+  ipls_stage* st = nullptr;
+  if (int rc = stage_acquire(h, (size_t)L * 8, (size_t)c * 8, &st)) return rc;
+  int rc = IPLS_OK;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    rc = flush_pending(h);
+    if (!rc) rc = finalize_range(h, p, 1);
+    if (!rc) {
+      const unsigned long long* w = (const unsigned long long*)(h->arena + h->w_off[p]);
+      hipError_t e;
+      if (sum_kind == IPLS_HOST_BE) {
+        launch_bswap(h->stream, w, (unsigned long long*)st->d, L);
+        e = hipGetLastError();
+      } else {
+        e = hipMemcpyAsync(st->d, w, (size_t)L * 8, hipMemcpyDeviceToDevice, h->stream);
+      }
+      if (e == hipSuccess) e = hipEventRecord(st->ready, h->stream);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        rc = fail(h, IPLS_E_DEVICE, "W snapshot: %s", hipGetErrorString(e));
+      }
     }
   }
-  return IPLS_OK;
+  if (rc) {   // a kernel of this call may have been queued before the failure
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipGetLastError();
+    stage_release(h, st);
+    return rc;
+  }
+  return stage_deliver(h, st, L, c, 0, sink, ctx, " (the round is consumed)");
 }
 
 int dev_set_weights(ipls_dev* h, int p, const void* src, int64_t n, int src_kind) {
@@ -2072,52 +2303,73 @@ int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind) {
   return d2h(h, out, d_out, (size_t)M * 8);
 }
 
-// GetPartitions (IPLS.java:1159-1174) handed to the caller chunk by chunk:
-// the divide runs once into the device scratch, then chunk k + 1 is copied
-// into one slot of a pinned two-slot ring while sink() consumes chunk k from
-// the other, on the calling thread (the JNI shim's sink is
-// SetDoubleArrayRegion, so the heap copy overlaps the transfer).  sink gets
-// flat model offsets (this engine's segment starts at flat_base); a non-zero
-// return stops the transfer
-// (IPLS_E_INVAL, nothing further is delivered).  The sink must not call
-// into this handle.
-// wire: the same chunks as Middleware's task-3 writeDouble stream (big-endian,
-// NaN canonical: k_divide's OUT_BE form), e.g. for a socket sink.
-int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire) {
-  if (!h || !sink) return fail(h, IPLS_E_INVAL, "null argument");
-  if (chunk < 2 || (chunk & 1)) return fail(h, IPLS_E_INVAL, "chunk of %lld doubles: even and >= 2", (long long)chunk);
-  IPLS_LOCK(h);
+// GetPartitions (IPLS.java:1159-1174) handed to the caller chunk by chunk,
+// in two phases so that a multi-shard handle snapshots every shard before it
+// delivers any byte (ipls_agg.cpp):
+//  * snapshot, under the engine lock: the divide runs once into this call's
+//    own staging (wire: the same values as Middleware's task-3 writeDouble
+//    stream -- big-endian, NaN canonical: k_divide's OUT_BE form);
+//  * deliver, with no lock held: chunk k + 1 is copied into one slot of the
+//    stage's pinned two-slot ring while sink() consumes chunk k from the other,
+//    on the calling thread (the JNI shim's sink is SetDoubleArrayRegion, the
+//    Middleware's a socket send).  sink gets flat model offsets (this engine's
+//    segment starts at flat_base); a non-zero return stops the transfer
+//    (IPLS_E_INVAL, nothing further is delivered).
+// *st is null when the engine's segment is empty.
+int dev_get_partitions_snapshot(ipls_dev* h, int64_t chunk, bool wire, ipls_stage** st_out) {
+  *st_out = nullptr;
+  if (!h) return fail_nl(h, IPLS_E_INVAL, "null argument");
+  if (chunk < 2 || (chunk & 1))
+    return fail_nl(h, IPLS_E_INVAL, "chunk of %lld doubles: even and >= 2", (long long)chunk);
   const int64_t M = h->flat_total - h->flat_base;
   if (M <= 0) return IPLS_OK;
-  HIP_TRY(h, dev_use(h->device));
-  if (int rc = ensure_scratch(h, (size_t)M * 8)) return rc;
-  const double* d_out = (const double*)h->d_scratch;
-  if (int rc = divide_range(h, 0, h->P, (unsigned long long*)h->d_scratch, wire)) return rc;
-  const int64_t c = std::min(chunk, M);
-  for (auto& sl : h->out_ring)
-    if (int rc = ensure_pinned(h, sl, (size_t)c * 8)) return rc;
-  const int64_t K = (M + c - 1) / c;
-  auto issue = [&](int64_t k) -> int {
-    PinnedSlot& sl = h->out_ring[k & 1];
-    const int64_t off = k * c, len = std::min(c, M - off);
-    HIP_TRY(h, hipMemcpyAsync(sl.host, d_out + off, (size_t)len * 8, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipEventRecord(sl.ev, h->stream));
-    return IPLS_OK;
-  };
-  if (int rc = issue(0)) return rc;
-  for (int64_t k = 0; k < K; ++k) {
-    // chunk k + 1 goes into the slot chunk k - 1 used, whose sink has returned
-    if (k + 1 < K)
-      if (int rc = issue(k + 1)) return rc;
-    PinnedSlot& sl = h->out_ring[k & 1];
-    HIP_TRY(h, hipEventSynchronize(sl.ev));
-    const int64_t off = k * c, len = std::min(c, M - off);
-    if (sink(ctx, (const double*)sl.host, h->flat_base + off, len) != 0) {
-      HIP_TRY(h, hipStreamSynchronize(h->stream));   // the copy still writing the other slot
-      return fail(h, IPLS_E_INVAL, "the chunk sink stopped the transfer at offset %lld", (long long)(h->flat_base + off));
+  HIP_TRY_NL(h, dev_use(h->device));
+  ipls_stage* st = nullptr;
+  if (int rc = stage_acquire(h, (size_t)M * 8, (size_t)std::min(chunk, M) * 8, &st)) return rc;
+  int rc = IPLS_OK;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    rc = flush_pending(h);
+    if (!rc) rc = divide_range(h, 0, h->P, (unsigned long long*)st->d, wire);
+    if (!rc) {
+      const hipError_t e = hipEventRecord(st->ready, h->stream);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        rc = fail(h, IPLS_E_DEVICE, "hipEventRecord failed: %s", hipGetErrorString(e));
+      }
     }
   }
+  if (rc) {   // a kernel of this call may have been queued before the failure
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipGetLastError();
+    stage_release(h, st);
+    return rc;
+  }
+  *st_out = st;
   return IPLS_OK;
+}
+
+int dev_get_partitions_deliver(ipls_dev* h, ipls_stage* st, int64_t chunk, ipls_chunk_sink sink, void* ctx) {
+  if (!st) return IPLS_OK;
+  const int64_t M = h->flat_total - h->flat_base;
+  HIP_TRY_NL(h, dev_use(h->device));
+  return stage_deliver(h, st, M, std::min(chunk, M), h->flat_base, sink, ctx, "");
+}
+
+// A snapshot that is not delivered (another shard failed first): the divide
+// that writes it finishes before the stage can be reused.
+void dev_stage_release(ipls_dev* h, ipls_stage* st) {
+  if (!st) return;
+  (void)dev_use(h->device);
+  if (hipEventSynchronize(st->ready) != hipSuccess) (void)hipGetLastError();
+  stage_release(h, st);
+}
+
+int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire) {
+  if (!h || !sink) return fail_nl(h, IPLS_E_INVAL, "null argument");
+  ipls_stage* st = nullptr;
+  if (int rc = dev_get_partitions_snapshot(h, chunk, wire, &st)) return rc;
+  return dev_get_partitions_deliver(h, st, chunk, sink, ctx);
 }
 
 // ---- device utilities ----

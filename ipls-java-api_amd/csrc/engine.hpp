@@ -16,6 +16,7 @@
 #include "../../include/ipls_agg.h"
 
 struct ipls_dev;
+struct ipls_stage;   // the staging one chunked call owns (engine.hip)
 
 const char* dev_last_error(const ipls_dev* h);
 void dev_set_thread_error(const char* msg);
@@ -52,6 +53,12 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
                            ipls_chunk_source source, void* ctx);
 int dev_finalize_chunked(ipls_dev* h, int p, int sum_kind, int64_t chunk, ipls_chunk_sink sink, void* ctx);
 int dev_get_partitions_chunked(ipls_dev* h, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire);
+// the two phases of dev_get_partitions_chunked: the snapshot under the
+// engine lock (into a stage the call owns; null for an empty segment), then
+// the delivery to the sink with no lock held, which releases the stage
+int dev_get_partitions_snapshot(ipls_dev* h, int64_t chunk, bool wire, ipls_stage** st);
+int dev_get_partitions_deliver(ipls_dev* h, ipls_stage* st, int64_t chunk, ipls_chunk_sink sink, void* ctx);
+void dev_stage_release(ipls_dev* h, ipls_stage* st);
 int dev_update_indirect(ipls_dev* h, int p, int target, const void* bytes, int64_t n_bytes);
 int dev_gbuf_load(ipls_dev* h, const void* bytes, int64_t n_bytes, const void** gbuf, int64_t* glen);
 int dev_other_replica(ipls_dev* h, int p, int32_t aggregator, const void* src, int64_t n, int src_kind);

@@ -1028,11 +1028,24 @@ namespace {
 int get_partitions_chunked(ipls_agg* H, int64_t chunk, ipls_chunk_sink sink, void* ctx, bool wire) {
   KeepDevice keep_device;
   if (!H || !sink) return ferr(H, IPLS_E_INVAL, "null argument");
-  // shard by shard on the calling thread, in model order: the sink runs
-  // where the caller is (a JNIEnv belongs to its thread)
-  for (int s : nonempty_shards(H))
-    if (int rc = fwd(H, s, dev_get_partitions_chunked(H->sh[s], chunk, sink, ctx, wire))) return rc;
-  return IPLS_OK;
+  // Every shard's divide into a staging of this call first, each under its
+  // own shard lock for that launch only; then the snapshots go to the sink
+  // shard by shard in model order with no lock held, on the calling thread
+  // (a JNIEnv belongs to its thread).  So the whole model is one snapshot,
+  // and a slow sink holds no shard.
+  const std::vector<int> ss = nonempty_shards(H);
+  std::vector<ipls_stage*> st(ss.size(), nullptr);
+  int rc = IPLS_OK;
+  size_t i = 0;
+  for (; i < ss.size() && !rc; ++i) rc = fwd(H, ss[i], dev_get_partitions_snapshot(H->sh[ss[i]], chunk, wire, &st[i]));
+  for (size_t j = 0; j < ss.size(); ++j) {
+    if (!rc && j < i) {
+      rc = fwd(H, ss[j], dev_get_partitions_deliver(H->sh[ss[j]], st[j], chunk, sink, ctx));
+    } else if (st[j]) {
+      dev_stage_release(H->sh[ss[j]], st[j]);   // after a failure: nothing more is delivered
+    }
+  }
+  return rc;
 }
 }  // namespace
 

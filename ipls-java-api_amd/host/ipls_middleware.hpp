@@ -32,6 +32,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -93,6 +94,17 @@ inline void big_socket_buffers(int fd, int bytes = 8 << 20) {
   setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &bytes, sizeof bytes);
   setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &bytes, sizeof bytes);
 }
+// A bound on every blocking recv/send of a connection: a peer that stalls
+// mid-task makes that recv/send fail (EAGAIN -> recv_exact / send_all false)
+// instead of holding the task forever.  ms <= 0: no bound.
+inline void io_timeout(int fd, int ms) {
+  if (ms <= 0) return;
+  timeval tv{};
+  tv.tv_sec = ms / 1000;
+  tv.tv_usec = (ms % 1000) * 1000;
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+}
 
 // ---- the server ----------------------------------------------------------------
 class MiddlewareServer {
@@ -108,8 +120,10 @@ class MiddlewareServer {
     double update_s = 0, reply_s = 0;   // inside the task handlers, socket reads/writes included
   };
 
-  // opts: Middleware.parse_arguments' PeerData (-pa, -n, device ...)
-  explicit MiddlewareServer(PeerData opts, int64_t chunk = 1 << 19) : opts_(std::move(opts)), chunk_(chunk) {}
+  // opts: Middleware.parse_arguments' PeerData (-pa, -n, device ...);
+  // io_timeout_ms bounds each blocking socket read/write of a connection
+  explicit MiddlewareServer(PeerData opts, int64_t chunk = 1 << 19, int io_timeout_ms = 60000)
+      : opts_(std::move(opts)), chunk_(chunk), io_timeout_ms_(io_timeout_ms) {}
   ~MiddlewareServer() {
     if (lfd_ >= 0) ::close(lfd_);
   }
@@ -139,6 +153,10 @@ class MiddlewareServer {
   // (Middleware.java:262-265); a caller running it on a thread catches there.
   // A task-2 connection that ends mid-update leaves the partitions received
   // before it folded (each partition is one call; the one cut short is not).
+  // A client that stalls fails its task after io_timeout_ms, the same way.
+  // The library holds no shard lock while a task's socket is read or
+  // written (the chunked calls lock for the fold / the snapshot only), so
+  // other threads' calls on the same IPLS instance never wait for a client.
   void serve(int max_connections = -1) {
     for (int served = 0; max_connections < 0 || served < max_connections; ++served) {
       const int fd = ::accept(lfd_, nullptr, nullptr);
@@ -148,6 +166,7 @@ class MiddlewareServer {
       }
       struct Closer { int fd; ~Closer() { ::close(fd); } } closer{fd};
       big_socket_buffers(fd);
+      io_timeout(fd, io_timeout_ms_);
       int16_t task = 0;
       if (!read_i16(fd, &task)) throw BufferUnderflowException(IPLS_E_FORMAT, "EOFException: no task");
       if (task == 1) task1(fd);
@@ -241,6 +260,7 @@ class MiddlewareServer {
 
   PeerData opts_;
   int64_t chunk_;
+  int io_timeout_ms_;
   int lfd_ = -1;
   std::unique_ptr<IPLS> ipls_;
   Init init_;

@@ -108,6 +108,25 @@ def _operand(x, big_endian: bool = False):
     return _host_operand(x, big_endian)
 
 
+def _callback(caught: list, fn, *args) -> int:
+    """Body of a chunk source/sink called from C: 0 to go on, 1 to stop.  No
+    exception may unwind through the library, so any -- a socket's EOFError
+    or timeout, a KeyboardInterrupt -- is kept and stops the call; the Python
+    caller re-raises it (_reraise) once the library has returned."""
+    if caught:
+        return 1
+    try:
+        return 0 if fn(*args) else 1
+    except BaseException as e:   # noqa: BLE001 -- re-raised after the library call
+        caught.append(e)
+        return 1
+
+
+def _reraise(caught: list) -> None:
+    if caught:
+        raise caught[0]
+
+
 class Aggregator:
     """One aggregator's partition accumulators on one MI355X.
 
@@ -294,15 +313,15 @@ class Aggregator:
         (shorter than the partition: ArrayIndexOutOfBounds, before any
         source call)."""
         target = N.TGT_AGG if from_clients else N.TGT_REP
+        caught = []
 
         @N.CHUNK_SOURCE
         def cb(ctx, dst, off, cnt):
-            try:
-                return 0 if source(dst, off, cnt) else 1
-            except Exception:   # noqa: BLE001 -- an exception must not unwind through C
-                return 1
-        self._chk(self._lib.ipls_agg_accumulate_chunked(self._h, partition, target, n,
-                                                        N.HOST_BE if big_endian else N.HOST_F64, chunk, cb, None))
+            return _callback(caught, source, dst, off, cnt)
+        rc = self._lib.ipls_agg_accumulate_chunked(self._h, partition, target, n,
+                                                   N.HOST_BE if big_endian else N.HOST_F64, chunk, cb, None)
+        _reraise(caught)
+        self._chk(rc)
 
     def GetPartitionsChunked(self, sink, *, wire: bool = False, chunk: int = 1 << 19):
         """GetPartitions (IPLS.java:1159-1174) handed to ``sink(ptr, offset,
@@ -311,27 +330,29 @@ class Aggregator:
         ipls_agg_get_partitions_wire_chunked): 8*count bytes at ``ptr`` in
         the library's pinned ring, valid during the call; the sink returns
         True to go on."""
+        caught = []
+
         @N.CHUNK_SINK
         def cb(ctx, vals, off, cnt):
-            try:
-                return 0 if sink(ctypes.cast(vals, ctypes.c_void_p).value, off, cnt) else 1
-            except Exception:   # noqa: BLE001
-                return 1
+            return _callback(caught, sink, ctypes.cast(vals, ctypes.c_void_p).value, off, cnt)
         fn = self._lib.ipls_agg_get_partitions_wire_chunked if wire else self._lib.ipls_agg_get_partitions_chunked
-        self._chk(fn(self._h, chunk, cb, None))
+        rc = fn(self._h, chunk, cb, None)
+        _reraise(caught)
+        self._chk(rc)
 
     def AggregatePartitionChunked(self, partition: int, sink, *, big_endian: bool = True, chunk: int = 1 << 19):
         """AggregatePartition with the committed sum handed to ``sink(ptr,
         offset, count)`` chunk by chunk, as one call (ipls_agg_finalize_chunked:
         no other caller's call lands between the sum and its bytes)."""
+        caught = []
+
         @N.CHUNK_SINK
         def cb(ctx, vals, off, cnt):
-            try:
-                return 0 if sink(ctypes.cast(vals, ctypes.c_void_p).value, off, cnt) else 1
-            except Exception:   # noqa: BLE001
-                return 1
-        self._chk(self._lib.ipls_agg_finalize_chunked(self._h, partition, N.HOST_BE if big_endian else N.HOST_F64,
-                                                      chunk, cb, None))
+            return _callback(caught, sink, ctypes.cast(vals, ctypes.c_void_p).value, off, cnt)
+        rc = self._lib.ipls_agg_finalize_chunked(self._h, partition, N.HOST_BE if big_endian else N.HOST_F64,
+                                                 chunk, cb, None)
+        _reraise(caught)
+        self._chk(rc)
 
     def flush(self):
         """Launch the folds of every queued device bucket now (no wait)."""

@@ -9,12 +9,13 @@ Wire format (Java DataInput/OutputStream, big-endian):
   ack     writeChar('A') = 00 41                                (:188-194)
 
 MI355X path. Java reads task 2 one ``readDouble`` at a time and writes task 3
-one ``writeDouble`` at a time on an unbuffered stream. Here the M doubles of
-task 2 are received as one byte buffer (pinned, when a PinnedBuffer is
-supplied) and handed to the GPU still big-endian: the fold kernel does the
-byte swap. The task-3 reply is one ``sendall`` of the bytes produced on the
-GPU by ``GetPartitions(wire=True)``, with NaN canonicalised as
-``writeDouble`` does.
+one ``writeDouble`` at a time on an unbuffered stream. Here each partition's
+slice of task 2 is received chunk by chunk straight into the library's pinned
+staging and handed to the GPU still big-endian (the fold kernel does the byte
+swap; ``update_from_socket``). The task-3 reply is the bytes produced on the
+GPU by the divide kernel, NaN canonicalised as ``writeDouble`` does, sent
+chunk by chunk (``reply_to_socket``). Neither holds a library lock while the
+socket is read or written, and every connection has a timeout (``serve``).
 
 ``LoopbackAggregator`` plays the aggregator of BASELINE configs[0] ("-pa 3
 -n 3 loopback: the aggregator averages 3 peers' List<Double>"). Each task 2 is
@@ -33,6 +34,8 @@ import time
 from dataclasses import dataclass, field
 
 import numpy as np
+
+from ._native import IplsError
 
 
 class MissingOptionError(SystemExit):
@@ -213,7 +216,10 @@ class LoopbackAggregator:
         ipls_agg_accumulate_chunked call whose source receives each chunk
         straight into the library's pinned ring; the copy engine sends it to
         the GPU while the next chunk is received, and the partition is folded
-        once its slice has landed.  Same bits as update_model on the whole
+        once its slice has landed.  The library takes its shard lock for that
+        fold only, never across the recv, so the other callers of the
+        aggregator are not held by a slow client (``self.lock`` orders this
+        server's own tasks and round count only).  Same bits as update_model on the whole
         payload.  A connection that ends mid-update raises (Java's
         EOFException ends the Middleware, Middleware.java:262-265), with the
         partitions received before it already folded."""
@@ -270,10 +276,25 @@ class LoopbackAggregator:
 
 
 def serve(opts: Options, max_connections: int | None = None, device: int = 0, initial_model=None,
-          ready: threading.Event | None = None, host: str = "127.0.0.1", on_listen=None, on_daemon=None):
+          ready: threading.Event | None = None, host: str = "127.0.0.1", on_listen=None, on_daemon=None,
+          io_timeout: float | None = 60.0, on_error=None):
     """Middleware.main (Middleware.java:212-268): one connection per task.
     ``opts.port`` 0 binds a free port; ``on_listen(port)`` is told which, and
-    ``on_daemon(aggregator)`` gets the LoopbackAggregator task 1 creates."""
+    ``on_daemon(aggregator)`` gets the LoopbackAggregator task 1 creates.
+
+    Every accepted connection gets ``io_timeout`` seconds per blocking socket
+    operation: a client that stalls mid-task fails that task (socket.timeout)
+    instead of holding the server.  The library holds no shard lock while the
+    socket is read or written (ipls_agg_accumulate_chunked /
+    get_partitions_wire_chunked), so other callers of the same aggregator --
+    the Updater's folds -- go on meanwhile either way.  A task that fails
+    (timeout, connection closed mid-message, a library error) ends that
+    connection only; ``on_error(task, exc)`` is told, and the server goes on
+    with the next connection.  Java's Middleware exits on any exception
+    (:262-265); a server of many peers should not be ended by one bad one.
+    A task 2 that fails mid-stream leaves the partitions whose slices fully
+    arrived folded, the rest untouched (each partition is one
+    all-or-nothing call)."""
     srv = socket.socket()
     srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     srv.bind((host, opts.port))
@@ -288,19 +309,27 @@ def serve(opts: Options, max_connections: int | None = None, device: int = 0, in
         while max_connections is None or served < max_connections:
             conn, _ = srv.accept()
             served += 1
+            task = None
             with conn:
-                (task,) = struct.unpack(">h", _recv_exact(conn, 2))
-                if task == 1:
-                    _, data = read_task(conn, 0, task=1)
-                    daemon = LoopbackAggregator(opts, data["model_size"], device, initial_model)
-                    if on_daemon is not None:
-                        on_daemon(daemon)
-                    conn.sendall(ACK)
-                elif task == 2:
-                    daemon.update_from_socket(conn)
-                    conn.sendall(ACK)
-                elif task == 3:
-                    daemon.reply_to_socket(conn)
+                conn.settimeout(io_timeout)
+                try:
+                    (task,) = struct.unpack(">h", _recv_exact(conn, 2))
+                    if task == 1:
+                        _, data = read_task(conn, 0, task=1)
+                        daemon = LoopbackAggregator(opts, data["model_size"], device, initial_model)
+                        if on_daemon is not None:
+                            on_daemon(daemon)
+                        conn.sendall(ACK)
+                    elif task == 2:
+                        daemon.update_from_socket(conn)
+                        conn.sendall(ACK)
+                    elif task == 3:
+                        daemon.reply_to_socket(conn)
+                except (OSError, EOFError, IplsError) as e:   # socket.timeout is an OSError
+                    if daemon is not None:
+                        daemon.stats["failed"] = daemon.stats.get("failed", 0) + 1
+                    if on_error is not None:
+                        on_error(task, e)
     finally:
         srv.close()
         if daemon is not None:

@@ -1181,11 +1181,15 @@ def test_chunked_calls_tiny_partitions_and_wire(ipls, O, devices):
 def test_accumulate_chunked_threads_serialise(ipls, O, devices):
     """Four threads fold four buckets into the same partition, each as one
     ipls_agg_accumulate_chunked call whose source sleeps between chunks (so
-    that, were the calls not units, they would interleave).  Each call holds
-    its shard's lock from its first source call to its fold, so the order in
-    which the threads made their first source call is the serial order, and
-    the target equals the oracle's fold in that order, bit for bit.  A fifth
-    thread keeps folding into another partition of the same shard meanwhile."""
+    that, were the calls not units, they would interleave).  Each call takes
+    effect as a whole when its last chunk has landed (the shard lock is held
+    for the fold only), so the target equals the oracle's fold of the four
+    whole buckets in ONE serial order, bit for bit -- normally the order in
+    which the sources delivered their last chunks; two calls whose last
+    chunks land within the same instant may take the lock in either order,
+    so every order is tried and exactly one must match.  A fifth thread keeps
+    folding into another partition of the same shard meanwhile."""
+    import itertools
     import threading
     import time
     from ipls import _native as N
@@ -1193,7 +1197,9 @@ def test_accumulate_chunked_threads_serialise(ipls, O, devices):
     agg = ipls.Aggregator(n_partitions=2, bucket_len=L, devices=devices)
     lib, h = agg._lib, agg._h
     gs = [O.synth_bucket(L, 1, 300 + i) * (1.0 + i) for i in range(4)]
-    order, lock = [], threading.Lock()
+    base = O.synth_bucket(L, 1, 299)   # a non-zero start: (0 + a) + b == (0 + b) + a would hide an order
+    agg.Update(base, 1)
+    last, lock = [], threading.Lock()
     errs = []
 
     def worker(i):
@@ -1201,11 +1207,12 @@ def test_accumulate_chunked_threads_serialise(ipls, O, devices):
 
         @N.CHUNK_SOURCE
         def src(ctx, dst, off, n):
-            if off == 0:
-                with lock:
-                    order.append(i)
             ctypes.memmove(dst, ctypes.c_char_p(raw[8 * off:8 * (off + n)]), 8 * n)
-            time.sleep(0.002)
+            if off + n == L:
+                with lock:
+                    last.append(i)
+            else:
+                time.sleep(0.002 * (1 + i))
             return 0
         rc = lib.ipls_agg_accumulate_chunked(h, 1, ipls.TGT_AGG, L, N.HOST_F64, 32768, src, None)
         if rc != 0:
@@ -1221,15 +1228,146 @@ def test_accumulate_chunked_threads_serialise(ipls, O, devices):
         t.start()
     for t in ths:
         t.join(60)
-    assert not errs and sorted(order) == [0, 1, 2, 3]
-    want = np.zeros(L)
-    for i in order:
-        want = O.fold(want, gs[i])
-    assert_bits_equal(agg.read(1, ipls.TGT_AGG), want, f"serial order {order}")
+    assert not errs and sorted(last) == [0, 1, 2, 3]
+    got = agg.read(1, ipls.TGT_AGG).view(np.uint64)
+
+    def serial(order):
+        want = O.fold(np.zeros(L), base)
+        for i in order:
+            want = O.fold(want, gs[i])
+        return want
+    matches = [o for o in itertools.permutations(range(4)) if np.array_equal(serial(o).view(np.uint64), got)]
+    assert len(matches) == 1, f"{len(matches)} serial orders match (last-chunk order {last})"
     side_want = np.zeros(L)
     for _ in range(20):
         side_want = O.fold(side_want, other)
     assert_bits_equal(agg.read(0, ipls.TGT_AGG), side_want, "the other partition")
+    agg.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_chunked_io_holds_no_shard_lock(ipls, O, devices):
+    """a chunked call's source or sink -- in the
+    Middleware servers a blocking socket recv/send -- runs with no shard lock
+    held, so a stalled peer freezes nothing else (the reference deserialises
+    the whole stream before UpdateModel takes PeerData.mtx, and writes the
+    reply after Get_Partitions returned, Middleware.java:224, 246, 254).
+
+    1. Thread A's accumulate_chunked into partition 1 blocks in its source
+       after the first chunk, for 500 ms.  Meanwhile a fold into partition 0
+       (same shard) and one into partition 1 itself both return, and so does
+       a GetPartitions.  A then completes; it takes effect when its last chunk
+       has landed: p1 = (base + B) + A and p0 = +0.0 + B0, bit for bit.
+    2. finalize_chunked of partition 1 whose sink blocks after the first
+       chunk: an Update into partition 1 and a set_weights of partition 1
+       return meanwhile.  The bytes delivered are the commit_update bytes of
+       this call's AggregatePartition (a snapshot: not torn), AGG then holds
+       the new arrival and W the new weights.
+    3. get_partitions_wire_chunked whose sink blocks: set_weights of every
+       partition returns meanwhile; the stream is the pre-call model's."""
+    import threading
+    import time
+    from ipls import _native as N
+    L = 300007
+    agg = ipls.Aggregator(n_partitions=4, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    a, b, b0, base = (O.synth_bucket(L, 1, 610 + i) * (1.0 + 2 * i) for i in range(4))
+    agg.Update(base, 1)   # a non-zero start, so that (base + B) + A and (base + A) + B differ
+    blocked, release = threading.Event(), threading.Event()
+    res = {}
+
+    def run_a():
+        raw = a.tobytes()
+
+        @N.CHUNK_SOURCE
+        def src(ctx, dst, off, n):
+            ctypes.memmove(dst, ctypes.c_char_p(raw[8 * off:8 * (off + n)]), 8 * n)
+            if off == 0:
+                blocked.set()
+                release.wait(10)
+            return 0
+        res["a"] = lib.ipls_agg_accumulate_chunked(h, 1, ipls.TGT_AGG, L, N.HOST_F64, 65536, src, None)
+    ta = threading.Thread(target=run_a)
+    ta.start()
+    assert blocked.wait(30)
+    t0 = time.perf_counter()
+    agg.Update(b0, 0)
+    agg.Update(b, 1)
+    whole = agg.GetPartitions(wire=True)
+    inside = time.perf_counter() - t0
+    time.sleep(max(0.0, 0.5 - inside))
+    assert not res, "A finished while its source was blocked"
+    release.set()
+    ta.join(30)
+    assert res["a"] == 0
+    assert inside < 0.5, f"the other calls waited {inside:.3f} s behind a blocked source"
+    assert len(whole) == 8 * 4 * (L - 1)
+    assert_bits_equal(agg.read(0, ipls.TGT_AGG), O.fold(np.zeros(L), b0), "p0")
+    p1 = O.fold(O.fold(O.fold(np.zeros(L), base), b), a)
+    assert not np.array_equal(p1.view(np.uint64), O.fold(O.fold(O.fold(np.zeros(L), base), a), b).view(np.uint64))
+    assert_bits_equal(agg.read(1, ipls.TGT_AGG), p1, "p1 = (base + B) + A")
+
+    # 2. a blocked finalize sink
+    r = O.synth_bucket(L, 1, 620) * 3.0
+    agg.Update(r, 1, from_clients=False)
+    w_round = p1 + O.fold(np.zeros(L), r)
+    nxt, w_new = O.synth_bucket(L, 1, 621), O.synth_bucket(L, 1, 622)
+    blocked.clear()
+    release.clear()
+    out = bytearray(8 * L)
+
+    def run_f():
+        @N.CHUNK_SINK
+        def sink(ctx, vals, off, n):
+            out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+            if off == 0:
+                blocked.set()
+                release.wait(10)
+            return 0
+        res["f"] = lib.ipls_agg_finalize_chunked(h, 1, N.HOST_BE, 65536, sink, None)
+    tf = threading.Thread(target=run_f)
+    tf.start()
+    assert blocked.wait(30)
+    t0 = time.perf_counter()
+    agg.Update(nxt, 1)
+    assert lib.ipls_agg_set_weights(h, 1, w_new.ctypes.data, L, N.HOST_F64) == 0
+    inside = time.perf_counter() - t0
+    assert "f" not in res
+    release.set()
+    tf.join(30)
+    assert res["f"] == 0 and inside < 0.5, inside
+    assert bytes(out) == O.be_encode(w_round), "commit_update bytes: this call's snapshot"
+    assert_bits_equal(agg.read(1, ipls.TGT_AGG), O.fold(np.zeros(L), nxt), "AGG: the arrival after the round")
+    assert_bits_equal(agg.read(1, ipls.TGT_WEIGHTS), w_new, "W: the later set_weights")
+
+    # 3. a blocked GetPartitions sink
+    ws = [agg.read(p, ipls.TGT_WEIGHTS) for p in range(4)]
+    want = O.be_encode_canonical(O.get_partitions(ws))
+    blocked.clear()
+    release.clear()
+    got = bytearray()
+
+    def run_g():
+        @N.CHUNK_SINK
+        def sink(ctx, vals, off, n):
+            got.extend(ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n))
+            if len(got) == 8 * n:
+                blocked.set()
+                release.wait(10)
+            return 0
+        res["g"] = lib.ipls_agg_get_partitions_wire_chunked(h, 65536, sink, None)
+    tg = threading.Thread(target=run_g)
+    tg.start()
+    assert blocked.wait(30)
+    t0 = time.perf_counter()
+    for p in range(4):
+        assert lib.ipls_agg_set_weights(h, p, w_new.ctypes.data, L, N.HOST_F64) == 0
+    inside = time.perf_counter() - t0
+    assert "g" not in res
+    release.set()
+    tg.join(30)
+    assert res["g"] == 0 and inside < 0.5, inside
+    assert bytes(got) == want, "the wire stream is the model at the call"
     agg.close()
 
 

@@ -323,24 +323,28 @@ def test_jni_heap_accumulate_pipelined(jvm, gpu, O):
 
 @pytest.mark.gpu
 def test_jni_heap_natives_are_one_ordered_unit(jvm, gpu, O):
-    """VERDICT r4 next 1 / ADVICE r4 (high, medium): a second thread's call on
-    the same partition, started in the middle of a heap-array native, lands
-    before or after the native's whole work, never inside it.
+    """a second thread's call on the same
+    partition, started in the middle of a heap-array native, lands before or
+    after the native's whole work, never inside it -- and it does not wait for
+    the native's Java-side copies (no shard lock is held across them).
 
     accumulate(double[]) of bucket A (3 chunks): the fake JVM starts a second
     thread's ipls_agg_accumulate of bucket B into the same (p, target) at the
     native's 2nd GetDoubleArrayRegion -- after chunk 0 was handed to the
-    library -- and gives it 300 ms.  It is still waiting when the window ends
-    (fj_inject_state 2), and the target holds one serial order, (acc + A) + B,
-    bit for bit against the oracle (Updater.java:72-149: whole-bucket folds
-    under PeerData.mtx).  The per-range library calls the round-4 shim used
-    do interleave under the same schedule (chunk 0 of A, then B, then the rest
+    library -- and gives it 300 ms.  It returns inside that window
+    (fj_inject_state 1), and the target holds one serial order, (acc + B) + A:
+    the native's bucket takes effect when its last chunk has landed, bit for
+    bit against the oracle (Updater.java:72-149: whole-bucket folds under
+    PeerData.mtx; Middleware.java:224, 246: the whole bucket is read before
+    the fold).  The per-range library calls the round-4 shim used do
+    interleave under the same schedule (chunk 0 of A, then B, then the rest
     of A), and those bits differ from every serial order: the check can tell.
 
     finalizePartition(byte[]): a second thread's set_weights on the same
     partition (Download_Scheduler.cache_partition) started at the native's 2nd
-    SetByteArrayRegion waits too; the bytes are exactly AGG + REP's, not torn,
-    and W holds the new weights after the join."""
+    SetByteArrayRegion returns inside the window too; the bytes are exactly
+    this call's AGG + REP (a snapshot, not torn), and W holds the new weights
+    after the join."""
     from ipls import _native as N
     lib = N.lib()
     M, P = 2 * 1048576 + 4099, 2
@@ -355,20 +359,20 @@ def test_jni_heap_natives_are_one_ordered_unit(jvm, gpu, O):
     jvm.L.fj_inject(0, 2, 300, h.value, 1, 0, b.ctypes.data, L)
     _, exc = jvm.call("accumulate", h, 1, 0, jvm.doubles(a))
     assert exc is None
-    assert jvm.L.fj_inject_state() == 2, "the second thread's fold ran inside accumulate(double[])"
+    assert jvm.L.fj_inject_state() == 1, "the second thread's fold waited for accumulate(double[])'s heap copies"
     assert jvm.L.fj_inject_join() == 0
-    serial = O.fold(O.fold(O.fold(np.zeros(L), base), a), b)
+    serial = O.fold(O.fold(O.fold(np.zeros(L), base), b), a)
     got = np.zeros(L)
     assert lib.ipls_agg_sync(ctypes.c_void_p(h.value)) == 0
     assert lib.ipls_agg_read(ctypes.c_void_p(h.value), 1, N.TGT_AGG, got.ctypes.data, L, N.HOST_F64) == 0
-    assert_bits_equal(got, serial, "one serial order: (base + A) + B")
+    assert_bits_equal(got, serial, "one serial order: (base + B) + A")
     # the round-4 pattern under the same schedule: per-range calls interleave
     c = 524288
     mixed = O.fold(np.zeros(L), base)
     mixed[:c] = mixed[:c] + a[:c]
     mixed = mixed + b
     mixed[c:] = mixed[c:] + a[c:]
-    other = O.fold(O.fold(O.fold(np.zeros(L), base), b), a)
+    other = O.fold(O.fold(O.fold(np.zeros(L), base), a), b)
     assert not np.array_equal(mixed.view(np.uint64), serial.view(np.uint64))
     assert not np.array_equal(mixed.view(np.uint64), other.view(np.uint64))
     hv = ctypes.c_void_p(h.value)
@@ -399,7 +403,7 @@ def test_jni_heap_natives_are_one_ordered_unit(jvm, gpu, O):
     out = jvm.bytes_(b"\0" * (8 * L))
     _, exc = jvm.call("finalizePartition", h, 1, out)
     assert exc is None
-    assert jvm.L.fj_inject_state() == 2, "set_weights ran inside finalizePartition(byte[])"
+    assert jvm.L.fj_inject_state() == 1, "set_weights waited for finalizePartition(byte[])'s heap copies"
     assert jvm.L.fj_inject_join() == 0
     w = O.fold(np.zeros(L), a) + O.fold(np.zeros(L), r)
     assert jvm.data(out, np.uint8).tobytes() == O.be_encode(w), "commit_update bytes not torn"
