@@ -1215,7 +1215,7 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
     if verify:
         from oracle import oracle as O   # checker only
         want = O.c_synth_sum_checksum(L, 0, K)
-    for mode in ("each", "coalesced"):
+    for mode in ("each", "coalesced", "coalesced_per_peer"):
         times = []
         for _ in range(reps):
             agg.reset()
@@ -1223,12 +1223,15 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
             e0.record(stream)
             t = 0
             for k in range(K):
+                if mode == "coalesced_per_peer":     # one call for peer k's P buckets (UpdateAsyncMany)
+                    t = agg.UpdateAsyncMany([(rows[q][k], q) for q in range(P)])
+                    continue
                 for q in range(P):
                     if mode == "each":
                         agg.Update(rows[q][k], q)
                     else:
                         t = agg.UpdateAsync(rows[q][k], q)
-            if mode == "coalesced":
+            if mode != "each":
                 agg.Wait(t)
             e1.record(stream)
             agg.sync()
@@ -1239,7 +1242,9 @@ def per_arrival_leg(ipls, torch, agg, rows, P: int, L: int, K: int, stream, veri
                      "ms_median": round(med, 4), "frac_median": round(nbytes / med / 1e6 / HBM_PEAK_GBS, 4),
                      "verified_checksum_p0": (agg.checksum(0) == want) if verify else None}
     out["note"] = ("one call per arriving bucket (peer-major); each = a fold launch per arrival, "
-                   "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), best (and median) of "
+                   "coalesced = queued device buckets folded together (ipls_agg_accumulate_async), "
+                   "coalesced_per_peer = the same queue fed one call per peer (Aggregator.UpdateAsyncMany: "
+                   "one Python -> C transition for a peer's P buckets), best (and median) of "
                    f"{reps}; algorithmic bytes P*(K+1)*L*8; Python caller through "
                    + ("ipls._fast (CPython extension, csrc/pyfast.c)" if agg._fast is not None else "ctypes"))
     # the same calls from a native caller (what a JNI shim sees): tools/host_e2e.cpp, a child process

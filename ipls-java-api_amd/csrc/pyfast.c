@@ -11,6 +11,11 @@
  *       ipls_agg_accumulate_async (include/ipls_agg.h)
  *   accumulate(h, p, target, src, n, kind)       -> rc
  *       ipls_agg_accumulate
+ *   accumulate_async_many(h, target, items) -> last ticket, or (rc < 0, index)
+ *       ipls_agg_accumulate_async for every (p, src, n, kind) of `items`, in
+ *       order, as ONE Python -> C transition: a caller that drains several
+ *       arrivals at once (one peer's buckets of every partition) pays the
+ *       interpreter once, not per bucket
  *   entry_points() -> the two addresses, which ipls compares with the
  *       library it bound before using this module
  *
@@ -93,6 +98,60 @@ static PyObject* fast_accumulate(PyObject* self, PyObject* const* a, Py_ssize_t 
   return PyLong_FromLong(rc);
 }
 
+typedef struct {
+  int p, kind;
+  const void* src;
+  int64_t n;
+} Item;
+
+static PyObject* fast_accumulate_async_many(PyObject* self, PyObject* const* a, Py_ssize_t na) {
+  (void)self;
+  if (na != 3) {
+    PyErr_Format(PyExc_TypeError, "expected 3 arguments (h, target, items), got %zd", na);
+    return NULL;
+  }
+  void* h = NULL;
+  int target;
+  if (as_ptr(a[0], &h) || as_int(a[1], &target)) return NULL;
+  PyObject* seq = PySequence_Fast(a[2], "items must be a sequence of (p, src, n, kind)");
+  if (!seq) return NULL;
+  const Py_ssize_t m = PySequence_Fast_GET_SIZE(seq);
+  Item* it = (Item*)PyMem_Malloc((size_t)(m > 0 ? m : 1) * sizeof(Item));
+  if (!it) {
+    Py_DECREF(seq);
+    return PyErr_NoMemory();
+  }
+  PyObject** el = PySequence_Fast_ITEMS(seq);
+  for (Py_ssize_t i = 0; i < m; ++i) {
+    PyObject* t = el[i];
+    void* src = NULL;
+    long long n;
+    if (!PyTuple_Check(t) || PyTuple_GET_SIZE(t) != 4 || as_int(PyTuple_GET_ITEM(t, 0), &it[i].p) ||
+        as_ptr(PyTuple_GET_ITEM(t, 1), &src) || as_int(PyTuple_GET_ITEM(t, 3), &it[i].kind) ||
+        ((n = PyLong_AsLongLong(PyTuple_GET_ITEM(t, 2))) == -1 && PyErr_Occurred())) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "items must be (p, src, n, kind) tuples");
+      PyMem_Free(it);
+      Py_DECREF(seq);
+      return NULL;
+    }
+    it[i].src = src;
+    it[i].n = (int64_t)n;
+  }
+  Py_DECREF(seq);
+  uint64_t ticket = 0;
+  int rc = 0;
+  Py_ssize_t i = 0;
+  Py_BEGIN_ALLOW_THREADS
+  for (; i < m; ++i) {
+    rc = ipls_agg_accumulate_async((ipls_agg*)h, it[i].p, target, it[i].src, it[i].n, it[i].kind, &ticket);
+    if (rc < 0) break;
+  }
+  Py_END_ALLOW_THREADS
+  PyMem_Free(it);
+  if (rc < 0) return Py_BuildValue("(in)", rc, i);
+  return PyLong_FromUnsignedLongLong(ticket);
+}
+
 /* the addresses this module calls, so ipls can check they are the entry
  * points of the library it bound itself (one mapping of one file) */
 static PyObject* fast_entry_points(PyObject* self, PyObject* unused) {
@@ -107,6 +166,8 @@ static PyMethodDef methods[] = {
      "entry_points() -> (address of ipls_agg_accumulate_async, address of ipls_agg_accumulate)"},
     {"accumulate_async", (PyCFunction)(void (*)(void))fast_accumulate_async, METH_FASTCALL,
      "accumulate_async(h, p, target, src, n, kind) -> ticket (>= 0) or the library's error code (< 0)"},
+    {"accumulate_async_many", (PyCFunction)(void (*)(void))fast_accumulate_async_many, METH_FASTCALL,
+     "accumulate_async_many(h, target, [(p, src, n, kind), ...]) -> last ticket, or (rc < 0, failing index)"},
     {"accumulate", (PyCFunction)(void (*)(void))fast_accumulate, METH_FASTCALL,
      "accumulate(h, p, target, src, n, kind) -> the library's return code"},
     {NULL, NULL, 0, NULL}};

@@ -302,6 +302,36 @@ class Aggregator:
                                                       N.HOST_BE if big_endian else N.HOST_F64, ctypes.byref(t)))
         return t.value
 
+    def UpdateAsyncMany(self, arrivals, from_clients: bool = True, *, big_endian: bool = True) -> int:
+        """UpdateAsync for several arrivals in order, e.g. every bucket the
+        Updater's queue holds at once (one peer's partitions): ``arrivals`` is
+        a sequence of (gradient, partition) with DeviceBuffer or PinnedBuffer
+        gradients.  Through ipls._fast it is one Python -> C transition for
+        the whole list; the folds, their order and their bits are those of
+        one UpdateAsync per arrival.  Returns the last ticket (0 for an empty
+        list).  An error stops at the failing arrival: the earlier ones are
+        queued, as after the same UpdateAsync calls."""
+        target = N.TGT_AGG if from_clients else N.TGT_REP
+        items = []
+        for g, p in arrivals:
+            if isinstance(g, DeviceBuffer):
+                items.append((p, g.ptr, g.n, N.DEV_BE if g.big_endian else N.DEV_F64))
+            elif isinstance(g, PinnedBuffer):
+                items.append((p, g.ptr, g.nbytes // 8, N.HOST_BE if big_endian else N.HOST_F64))
+            else:
+                raise TypeError("UpdateAsyncMany takes DeviceBuffer or PinnedBuffer gradients")
+        if not items:
+            return 0
+        if self._fast is not None:
+            t = self._fast.accumulate_async_many(self._hv, target, items)
+            if isinstance(t, tuple):
+                self._chk(t[0])
+            return t
+        t = ctypes.c_uint64()
+        for p, ptr, n, kind in items:
+            self._chk(self._lib.ipls_agg_accumulate_async(self._h, p, target, ptr, n, kind, ctypes.byref(t)))
+        return t.value
+
     def UpdateChunked(self, partition: int, n: int, source, *, big_endian: bool = True, from_clients: bool = True,
                       chunk: int = 1 << 19):
         """Updater._Update of one bucket that the caller produces chunk by

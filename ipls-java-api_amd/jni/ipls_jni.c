@@ -23,6 +23,16 @@
  * test build (-DIPLS_JNI_CALL_HOOK=fj_library_call) reports each one to the
  * fake JVM, which fails the test if a critical region is open at that point.
  *
+ * The one critical region the shim opens is critical_copy(): inside a chunk
+ * callback of the three heap-array natives (accumulate(double[]),
+ * finalizePartition(byte[]), getPartitions(double[])), around one memcpy of
+ * one ring chunk (4 MiB) between the array and the library's pinned ring,
+ * split over a few helper threads -- no JNI call and no library call inside,
+ * ~0.1 ms.  That is the time HotSpot's own Get/Set<T>ArrayRegion of the same
+ * chunk keeps the thread from a safepoint, and one CPU thread's memcpy is
+ * what held these natives to 33 / 21 GB/s against PCIe's 56 (VERDICT r5
+ * item 4).
+ *
  * Built against the JDK's <jni.h> on the Java side's build host (make -C
  * ipls-java-api_amd jni).  This image has no JDK: tests/test_jni.py compiles
  * it with -Wall -Wextra -Werror against tests/jni/jni.h and drives every
@@ -114,8 +124,130 @@ static void *stage(JNIEnv *env, int slot, size_t bytes) {
     return st->p[slot];
 }
 
-/* Values per chunk of the chunked natives: 4 MiB. */
-#define RING_CHUNK ((jsize)1 << 19)
+/* Values per chunk of the chunked natives, from the sweep of
+ * tools/jni_heap_probe.py over chunk size x copy threads on one 4M-double
+ * partition (profiles/r06/d): the heap -> ring direction (accumulate) runs
+ * best at 16 MiB chunks (51 GB/s vs 44.5 at 4 MiB: fewer, longer H2D
+ * transfers), the ring -> heap direction (finalizePartition, getPartitions)
+ * at 4 MiB (40-41 GB/s; 16 MiB: 38.5).  IPLS_JNI_RING_CHUNK (values, even,
+ * 2^16 .. 2^26) sets both, for sweeps. */
+static jsize g_in_chunk = (jsize)1 << 21, g_out_chunk = (jsize)1 << 19;
+static pthread_once_t g_ring_once = PTHREAD_ONCE_INIT;
+static void ring_init(void) {
+    const char *e = getenv("IPLS_JNI_RING_CHUNK");
+    const long v = e ? atol(e) : 0;
+    if (v >= (1L << 16) && v <= (1L << 26) && !(v & 1)) g_in_chunk = g_out_chunk = (jsize)v;
+}
+static jsize ring_chunk(int in) {
+    (void)pthread_once(&g_ring_once, ring_init);
+    return in ? g_in_chunk : g_out_chunk;
+}
+#define IN_CHUNK ring_chunk(1)    /* heap -> library: accumulate(double[]) */
+#define RING_CHUNK ring_chunk(0)  /* library -> heap: finalizePartition, getPartitions */
+
+/* ---- parallel copies between a Java array and the library's pinned ring ----
+ * One memcpy thread moves 21-30 GB/s between pageable and pinned host memory
+ * (tools/pinned_read_probe.hip, profiles/r05/h), half of what PCIe carries.
+ * A chunk of at least PAR_MIN bytes is split over IPLS_JNI_COPY_THREADS
+ * threads (default 4, the calling thread included): a pool of helpers created
+ * on first use, woken per chunk.  One caller at a time uses the pool; a
+ * caller that finds it busy (another Java thread in the same native) copies
+ * alone. */
+#define PAR_MIN ((size_t)1 << 20)
+#define PAR_MAX_THREADS 16
+static struct {
+    pthread_mutex_t use;          /* held by the caller whose chunk the helpers copy */
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    unsigned gen;                 /* chunk generation: helpers wake on a change */
+    int helpers, pending;
+    char *dst;
+    const char *src;
+    size_t bytes, part;
+} g_pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER,
+            PTHREAD_COND_INITIALIZER, 0, 0, 0, NULL, NULL, 0, 0};
+static pthread_once_t g_pool_once = PTHREAD_ONCE_INIT;
+
+static void *copy_helper(void *arg) {
+    const size_t i = (size_t)(intptr_t)arg;   /* part i; the caller copies part 0 */
+    unsigned seen = 0;
+    pthread_mutex_lock(&g_pool.mu);
+    for (;;) {
+        while (g_pool.gen == seen) pthread_cond_wait(&g_pool.go, &g_pool.mu);
+        seen = g_pool.gen;
+        char *d = g_pool.dst;
+        const char *s = g_pool.src;
+        const size_t b = g_pool.bytes, part = g_pool.part;
+        pthread_mutex_unlock(&g_pool.mu);
+        const size_t lo = part * i;
+        if (lo < b) memcpy(d + lo, s + lo, b - lo < part ? b - lo : part);
+        pthread_mutex_lock(&g_pool.mu);
+        if (--g_pool.pending == 0) pthread_cond_signal(&g_pool.done);
+    }
+    return NULL;
+}
+
+static void pool_init(void) {
+    const char *e = getenv("IPLS_JNI_COPY_THREADS");
+    int t = e ? atoi(e) : 4;
+    if (t < 1) t = 1;
+    if (t > PAR_MAX_THREADS) t = PAR_MAX_THREADS;
+    int made = 0;
+    for (int i = 1; i < t; ++i) {
+        pthread_t th;
+        pthread_attr_t at;
+        pthread_attr_init(&at);
+        pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+        if (pthread_create(&th, &at, copy_helper, (void *)(intptr_t)i) == 0) ++made;
+        pthread_attr_destroy(&at);
+        if (made != i) break;   /* parts are numbered 1..made */
+    }
+    g_pool.helpers = made;
+}
+
+/* memcpy(dst, src, bytes), split over the pool when it is large and free. */
+static void par_copy(void *dst, const void *src, size_t bytes) {
+    (void)pthread_once(&g_pool_once, pool_init);
+    if (bytes < PAR_MIN || g_pool.helpers == 0 || pthread_mutex_trylock(&g_pool.use) != 0) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t t = (size_t)g_pool.helpers + 1;
+    const size_t part = ((bytes + t - 1) / t + 4095) / 4096 * 4096;
+    pthread_mutex_lock(&g_pool.mu);
+    g_pool.dst = (char *)dst;
+    g_pool.src = (const char *)src;
+    g_pool.bytes = bytes;
+    g_pool.part = part;
+    g_pool.pending = g_pool.helpers;
+    ++g_pool.gen;
+    pthread_cond_broadcast(&g_pool.go);
+    pthread_mutex_unlock(&g_pool.mu);
+    memcpy(dst, src, bytes < part ? bytes : part);
+    pthread_mutex_lock(&g_pool.mu);
+    while (g_pool.pending > 0) pthread_cond_wait(&g_pool.done, &g_pool.mu);
+    pthread_mutex_unlock(&g_pool.mu);
+    pthread_mutex_unlock(&g_pool.use);
+}
+
+/* Copy `bytes` at byte offset `off` of a primitive array to (to_array == 0)
+ * or from (to_array == 1) `ring`, inside ONE short critical region (see the
+ * file comment); no JNI or library call happens while it is open.  Returns 0,
+ * or 1 when the JVM could not give the array (OutOfMemoryError pending) or
+ * gave a copy of it -- the caller then uses Get/Set<T>ArrayRegion instead. */
+static int critical_copy(JNIEnv *env, jarray a, size_t off, void *ring, size_t bytes, int to_array) {
+    jboolean is_copy = JNI_FALSE;
+    char *p = (char *)(*env)->GetPrimitiveArrayCritical(env, a, &is_copy);
+    if (!p) return 1;
+    if (is_copy) {   /* a whole-array copy per chunk would be quadratic */
+        (*env)->ReleasePrimitiveArrayCritical(env, a, p, JNI_ABORT);
+        return 1;
+    }
+    if (to_array) par_copy(p + off, ring, bytes);
+    else par_copy(ring, p + off, bytes);
+    (*env)->ReleasePrimitiveArrayCritical(env, a, p, to_array ? 0 : JNI_ABORT);
+    return 0;
+}
 
 /* A copy of the whole double[] / byte[] in staging slot `slot`. */
 static void *copy_doubles(JNIEnv *env, jdoubleArray a, jsize n, int slot) {
@@ -319,6 +451,10 @@ JNIEXPORT void JNICALL Java_NativeAggregator_updateGradientDirect(JNIEnv *env, j
 struct heap_source { JNIEnv *env; jdoubleArray a; };
 static int heap_source_fn(void *ctx, void *dst, int64_t off, int64_t n) {
     struct heap_source *s = (struct heap_source *)ctx;
+    /* [off, off + n) lies inside the array: the library asks only for values
+     * below L_p, and it refused an array shorter than L_p before any chunk */
+    if ((size_t)n * 8 >= PAR_MIN && critical_copy(s->env, s->a, (size_t)off * 8, dst, (size_t)n * 8, 0) == 0) return 0;
+    if ((*s->env)->ExceptionCheck(s->env)) return 1;
     (*s->env)->GetDoubleArrayRegion(s->env, s->a, (jsize)off, (jsize)n, (jdouble *)dst);
     return (*s->env)->ExceptionCheck(s->env) ? 1 : 0;
 }
@@ -329,14 +465,16 @@ JNIEXPORT void JNICALL Java_NativeAggregator_accumulate(JNIEnv *env, jclass c, j
     if (!g) return;   /* Gradient == null: the Updater loops do nothing (Updater.java:115) */
     /* One call for the whole arrival (Updater._Update under PeerData.mtx,
      * Updater.java:72-149): the library pulls the bucket's first L values
-     * chunk by chunk through heap_source_fn (GetDoubleArrayRegion into its
-     * pinned ring) while the previous chunk crosses PCIe, then folds the
-     * bucket in one launch.  No other caller's call on the partition's GPU
-     * lands inside it, a short array is ArrayIndexOutOfBoundsException before
-     * any copy, and a failed copy folds nothing. */
+     * chunk by chunk through heap_source_fn (critical_copy into its pinned
+     * ring) while the previous chunk crosses PCIe, then folds the bucket in
+     * one launch.  The arrival takes effect as one unit once its last chunk
+     * has landed (the GPU shard is not held while the chunks are copied: no
+     * other caller waits for this thread's heap copies), a short array is
+     * ArrayIndexOutOfBoundsException before any copy, and a failed copy
+     * folds nothing. */
     struct heap_source hs = {env, g};
     const jsize n = (*env)->GetArrayLength(env, g);
-    const int rc = LIB(ipls_agg_accumulate_chunked(H(h), p, tgt, n, IPLS_HOST_F64, RING_CHUNK, heap_source_fn, &hs));
+    const int rc = LIB(ipls_agg_accumulate_chunked(H(h), p, tgt, n, IPLS_HOST_F64, IN_CHUNK, heap_source_fn, &hs));
     if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_for(env, rc, H(h));
 }
 
@@ -445,6 +583,10 @@ out:
 struct bytes_sink { JNIEnv *env; jbyteArray out; };
 static int bytes_sink_fn(void *ctx, const double *values, int64_t off, int64_t n) {
     struct bytes_sink *b = (struct bytes_sink *)ctx;
+    /* the array holds 8 * L_p bytes (need_len before the call) */
+    if ((size_t)n * 8 >= PAR_MIN && critical_copy(b->env, b->out, (size_t)off * 8, (void *)values, (size_t)n * 8, 1) == 0)
+        return 0;
+    if ((*b->env)->ExceptionCheck(b->env)) return 1;
     (*b->env)->SetByteArrayRegion(b->env, b->out, (jsize)(8 * off), (jsize)(8 * n), (const jbyte *)values);
     return (*b->env)->ExceptionCheck(b->env) ? 1 : 0;
 }
@@ -460,8 +602,9 @@ JNIEXPORT void JNICALL Java_NativeAggregator_finalizePartition(JNIEnv *env, jcla
     if (L < 0 || !need_len(env, sum, 8 * L, "commit_update bytes")) return;
     /* One call: AggregatePartition on the device, then W's big-endian bytes
      * come back chunk by chunk through the library's pinned ring, each
-     * copied into the byte[] while the next is in flight.  No set_weights or
-     * finalize of another thread can land between the sum and its bytes. */
+     * copied into the byte[] while the next is in flight.  The bytes are a
+     * snapshot of this call's W: a set_weights or finalize of another thread
+     * meanwhile neither waits for the copies nor tears the bytes. */
     struct bytes_sink bs = {env, sum};
     const int rc = LIB(ipls_agg_finalize_chunked(H(h), p, IPLS_HOST_BE, RING_CHUNK, bytes_sink_fn, &bs));
     if (rc < 0 && !(*env)->ExceptionCheck(env)) throw_for(env, rc, H(h));
@@ -500,6 +643,10 @@ JNIEXPORT void JNICALL Java_NativeAggregator_setWeightsFrame(JNIEnv *env, jclass
 struct model_sink { JNIEnv *env; jdoubleArray out; };
 static int model_sink_fn(void *ctx, const double *values, int64_t off, int64_t n) {
     struct model_sink *m = (struct model_sink *)ctx;
+    /* off + n <= M <= the array's length (checked before the call) */
+    if ((size_t)n * 8 >= PAR_MIN && critical_copy(m->env, m->out, (size_t)off * 8, (void *)values, (size_t)n * 8, 1) == 0)
+        return 0;
+    if ((*m->env)->ExceptionCheck(m->env)) return 1;
     (*m->env)->SetDoubleArrayRegion(m->env, m->out, (jsize)off, (jsize)n, values);
     return (*m->env)->ExceptionCheck(m->env) ? 1 : 0;
 }

@@ -237,8 +237,9 @@ static void JNICALL GetDoubleArrayRegion(JNIEnv *env, jdoubleArray a, jsize s, j
 }
 
 /* ---- a second Java thread inside a native ----
- * fj_inject arms a one-shot.  At the `after`-th array-region copy
- * (Get/Set<T>ArrayRegion) from then on -- inside a chunked native, that is
+ * fj_inject arms a one-shot.  At the `after`-th array access (a
+ * Get/Set<T>ArrayRegion copy, or a GetPrimitiveArrayCritical: the shim's
+ * chunk copies use either) from then on -- inside a chunked native, that is
  * between two chunks of its library call -- a second thread calls the
  * library on the same handle by itself:
  *   op 0: ipls_agg_accumulate(h, p, tgt, src, n, IPLS_HOST_F64)
@@ -325,6 +326,8 @@ JNIEXPORT int fj_library_calls(void) { return g_library_calls; }
 
 static void *JNICALL GetPrimitiveArrayCritical(JNIEnv *env, jarray a, jboolean *c) {
     (void)env;
+    if (g_critical) violation("GetPrimitiveArrayCritical inside a critical region");
+    inject_tick();   /* an array access, like the region copies */
     if (g_exc) violation("GetPrimitiveArrayCritical with an exception pending");
     if (c) *c = JNI_FALSE;
     if (!a || a->kind == K_OBJECTS || a->kind == K_DIRECT || a->kind == K_CLASS) {

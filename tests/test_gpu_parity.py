@@ -2778,6 +2778,45 @@ def test_stateful_random_sequence_production_shapes(ipls, O, seed, P, L):
         assert shape in round_shapes, (shape, sorted(round_shapes))
 
 
+def test_update_async_many_is_the_per_arrival_calls(ipls, O):
+    """Aggregator.UpdateAsyncMany (ipls._fast.accumulate_async_many: one
+    Python -> C transition for a list of arrivals) folds
+    exactly what one UpdateAsync per arrival folds, in the same order: queued
+    device buckets (native and big-endian) and pinned host buckets over three
+    partitions and both targets, through _fast and through ctypes, equal to
+    the oracle.  A bad arrival in the middle raises; the ones before it are
+    queued, as after the same UpdateAsync calls."""
+    from ipls import _native as N
+    P, L = 3, 40003
+    vals = [O.synth_bucket(L, 11, k) for k in range(5)]
+    dv = [dev(v) for v in vals[:3]]
+    bt, bb = dev_be(vals[3])
+    pb = ipls.PinnedBuffer(8 * L)
+    pb.view()[:] = np.frombuffer(O.be_encode(vals[4]), dtype=np.uint8)
+    torch.cuda.synchronize()
+    arrivals = [(dv[k][1], p) for k in range(3) for p in range(P)] + [(bb, 1), (pb, 2)]
+    for library in (None, N.load(N.LIB_PATH)):
+        agg = ipls.Aggregator(n_partitions=P, bucket_len=L, library=library)
+        agg.set_coalesce(4)
+        assert (agg._fast is not None) == (library is None)
+        t = agg.UpdateAsyncMany(arrivals)
+        t2 = agg.UpdateAsyncMany([(dv[2][1], 0)], from_clients=False)
+        assert t2 > t > 0 and agg.UpdateAsyncMany([]) == 0
+        agg.Wait(t2)
+        ref = [O.reduce(vals[:3], L), O.reduce(vals[:4], L), O.reduce(vals[:3] + [vals[4]], L)]
+        for p in range(P):
+            assert_bits_equal(agg.read(p, ipls.TGT_AGG), ref[p], f"p{p} fast={agg._fast is not None}")
+        assert_bits_equal(agg.read(0, ipls.TGT_REP), O.reduce([vals[2]], L))
+        agg.reset()
+        with pytest.raises(ipls.IplsError):
+            agg.UpdateAsyncMany([(dv[0][1], 0), (dv[1][1], P), (dv[2][1], 1)])   # partition P out of range
+        agg.sync()
+        assert_bits_equal(agg.read(0, ipls.TGT_AGG), O.reduce([vals[0]], L), "the arrival before the bad one")
+        assert_bits_equal(agg.read(1, ipls.TGT_AGG), np.zeros(L), "nothing after it")
+        agg.close()
+    pb.close()
+
+
 def test_fast_extension_and_ctypes_give_the_same_bits(ipls, O):
     """A default Aggregator takes the per-arrival calls through ipls._fast
     (csrc/pyfast.c); one bound to another ctypes mapping of the same library

@@ -11,14 +11,23 @@ libipls_agg.so.  CPU tests cover the argument checks the shim does before
 the library is called; -m gpu tests run whole Java-API sequences through the
 natives against the oracle, including the exception mapping and the
 guarantee that a rejected call leaves the accumulators unchanged.
+
+The shim's ring chunk is pinned to 512 Ki values in both directions here
+(IPLS_JNI_RING_CHUNK, read once per process), so that the partitions of
+about 1M doubles below are multi-chunk calls whose chunk edges the tests
+name; its defaults (16 MiB in, 4 MiB out, profiles/r06/d) only change how
+many chunks a call takes.
 """
 import ctypes
+import os
 import subprocess
 
 import numpy as np
 import pytest
 
 from conftest import ROOT, assert_bits_equal
+
+os.environ["IPLS_JNI_RING_CHUNK"] = "524288"
 
 BUILD = ROOT / "tests" / "jni" / "build"
 LIB = BUILD / "libfakejni.so"
@@ -146,15 +155,25 @@ def test_no_critical_region_across_a_library_call(jvm):
     region while it calls into the library (a call that may wait on the GPU
     would block a real JVM's GC for that long).  The fake JVM fails any call
     made with a region open (JVM.call checks fj_violations after every
-    native); this checks the rule can fire, that the shim reports its library
-    calls, and that it has no critical region left at all."""
+    native, and that no region is left open); this checks the rule can fire
+    and that the shim reports its library calls.  The shim's one critical
+    region is critical_copy's: one memcpy of one ring
+    chunk inside a chunk callback, opened and released in that function with
+    no JNI or library call in between -- checked here on the source text."""
+    import re
     assert jvm.L.fj_selftest_critical_rule() >= 1
     before = jvm.L.fj_library_calls()
     r, exc = jvm.call("shardPlan", 4, 2, res=ctypes.c_void_p)
     assert exc is None and jvm.L.fj_library_calls() > before
     shim = (ROOT / "ipls-java-api_amd" / "jni" / "ipls_jni.c").read_text()
     code = "\n".join(ln for ln in shim.splitlines() if not ln.lstrip().startswith(("*", "/*")))
-    assert "GetPrimitiveArrayCritical" not in code
+    assert code.count("GetPrimitiveArrayCritical") == 1 and code.count("ReleasePrimitiveArrayCritical") == 2
+    body = code[code.index("static int critical_copy("):]
+    body = body[:body.index("\n}\n")]
+    assert "GetPrimitiveArrayCritical" in body and body.count("ReleasePrimitiveArrayCritical") == 2
+    end = body.rindex("ReleasePrimitiveArrayCritical") + len("ReleasePrimitiveArrayCritical")
+    inside = body[body.index("GetPrimitiveArrayCritical"):end]
+    assert not re.search(r"\(\*env\)->(?!ReleasePrimitiveArrayCritical)|LIB\(|ipls_agg_", inside), inside
 
 
 def test_shard_plan_native(jvm):
