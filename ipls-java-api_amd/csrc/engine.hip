@@ -324,6 +324,7 @@ int stage_acquire(ipls_dev* h, size_t dev_bytes, size_t slot_bytes, ipls_stage**
     if (!rc && !*e) rc = try_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
   if (!rc && st->d_cap < dev_bytes) {
     if (st->d) {
+      // the fold that last read `d` and every copy of the stage are done before it is freed
       if (st->free_pending) rc = try_hip(hipEventSynchronize(st->free_ev), "hipEventSynchronize");
       if (!rc) rc = try_hip(hipStreamSynchronize(st->copy), "hipStreamSynchronize");
       if (!rc) rc = try_hip(hipFree(st->d), "hipFree");
@@ -342,6 +343,12 @@ int stage_acquire(ipls_dev* h, size_t dev_bytes, size_t slot_bytes, ipls_stage**
     if (s.cap < slot_bytes) {
       if (s.pending) rc = try_hip(hipEventSynchronize(s.ev), "hipEventSynchronize");
       if (!rc) s.pending = false;
+      // never free a slot a copy may still read or write (the r05/h fault
+      // analysis): its last copy's event must have completed
+      if (!rc && s.host && s.ev && hipEventQuery(s.ev) != hipSuccess) {
+        (void)hipGetLastError();
+        rc = fail_nl(h, IPLS_E_DEVICE, "internal: pinned slot regrown with a copy in flight");
+      }
       if (!rc && s.host) rc = try_hip(hipHostFree(s.host), "hipHostFree");
       if (!rc) {
         s.host = nullptr;

@@ -1372,6 +1372,82 @@ def test_chunked_io_holds_no_shard_lock(ipls, O, devices):
 
 
 @pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_chunked_stage_pool_under_concurrency(ipls, O, devices):
+    """The per-call staging of the chunked calls (a pool of stages per shard,
+    each regrown only by the call that owns it): six threads, one partition
+    each (three per shard on a [0, 0] handle), run random sequences of
+    accumulate_chunked (chunk sizes from 2 Ki to 1 Mi values, so stages are
+    regrown both ways), sources that stop mid-bucket (nothing folded),
+    finalize_chunked (the commit_update bytes) and get_partitions_chunked
+    (every partition's snapshot; each thread checks its own slice).  Every
+    result is bit-exact against the oracle replaying that thread's sequence."""
+    import threading
+    from ipls import _native as N
+    P, L = 6, 200003
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    chunks = (2048, 65536, 100002, 1 << 20)
+    errs = []
+
+    def worker(p):
+        try:
+            rng = np.random.default_rng(100 + p)
+            acc, w = np.zeros(L), np.zeros(L)
+            for i in range(14):
+                op = rng.choice(["acc", "acc", "stop", "fin", "getp"])
+                chunk = int(rng.choice(chunks))
+                if op in ("acc", "stop"):
+                    g = O.synth_bucket(L, p, 1000 + i) * (1.0 + i)
+                    raw = g.tobytes()
+                    stop_at = int(rng.integers(0, (L + chunk - 1) // chunk)) if op == "stop" else -1
+
+                    @N.CHUNK_SOURCE
+                    def src(ctx, dst, off, n, raw=raw, stop_at=stop_at, chunk=chunk):
+                        ctypes.memmove(dst, ctypes.c_char_p(raw[8 * off:8 * (off + n)]), 8 * n)
+                        return 1 if off // chunk == stop_at else 0
+                    rc = lib.ipls_agg_accumulate_chunked(h, p, ipls.TGT_AGG, L, N.HOST_F64, chunk, src, None)
+                    if op == "acc":
+                        assert rc == 0, (p, i, rc)
+                        acc = O.fold(acc, g)
+                    else:
+                        assert rc == N.IPLS_E_INVAL, (p, i, rc)
+                elif op == "fin":
+                    out = bytearray(8 * L)
+
+                    @N.CHUNK_SINK
+                    def sink(ctx, vals, off, n, out=out):
+                        out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+                        return 0
+                    assert lib.ipls_agg_finalize_chunked(h, p, N.HOST_BE, chunk, sink, None) == 0
+                    w = acc + 0.0
+                    assert bytes(out) == O.be_encode(w), (p, i, "commit_update bytes")
+                    acc = np.zeros(L)
+                else:
+                    got = bytearray()
+                    lo, hi = 8 * p * (L - 1), 8 * (p + 1) * (L - 1)
+
+                    @N.CHUNK_SINK
+                    def gsink(ctx, vals, off, n, got=got):
+                        a, b = 8 * off, 8 * (off + n)
+                        if b > lo and a < hi:
+                            v = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+                            got.extend(v[max(lo - a, 0):min(hi, b) - a])
+                        return 0
+                    assert lib.ipls_agg_get_partitions_chunked(h, chunk, gsink, None) == 0
+                    assert bytes(got) == O.get_partitions([w]).tobytes(), (p, i, "GetPartitions slice")
+            assert_bits_equal(agg.read(p, ipls.TGT_AGG), acc, f"partition {p}")
+        except BaseException as e:   # noqa: BLE001 -- reported by the main thread
+            errs.append((p, repr(e)))
+    ths = [threading.Thread(target=worker, args=(p,)) for p in range(P)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs, errs
+    agg.close()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_finalize_chunked(ipls, O, devices):
     """ipls_agg_finalize_chunked: AggregatePartition (W = AGG + REP,
     IPLS.java:1248-1274) with W handed to a sink chunk by chunk, as one call:

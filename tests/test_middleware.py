@@ -119,3 +119,65 @@ def test_streamed_tasks_match_the_oracle_across_chunk_edges():
         la.update_model(g.astype(">f8").tobytes())
     assert bytes(la.get_partitions_wire()) == want
     la.close()
+
+
+@pytest.mark.gpu
+def test_a_stalled_client_holds_nothing():
+    """VERDICT r5 item 1, the Middleware side: a client that stops sending in
+    the middle of task 2 holds neither the GPU shard nor the server.  While
+    the server is blocked in recv inside partition 1's chunked fold, direct
+    folds into partitions 1 and 2 of the same handle (the Updater's, as the
+    reference's daemon threads make them under PeerData.mtx) return at once;
+    after io_timeout the server fails that task (on_error gets a timeout),
+    keeps partition 0 -- whose slice had fully arrived, each partition being
+    one all-or-nothing call -- and serves the next clients.  The round's
+    writeDouble reply then equals the oracle's fixed-order average of exactly
+    those contributions."""
+    import time
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu run without a visible GPU")
+    from oracle import oracle as O
+    from ipls.middleware import client_call, encode_get, encode_init, encode_update, parse_arguments, serve
+    M, P = 3 * 524287, 3
+    Ls = [O.partition_len(M, P, p) for p in range(P)]
+    opts = parse_arguments(f"-p 0 -pa {P} -mp 1 -n 2 -i 0 -training 60 -aggr 0".split())
+    ports, daemons, errors = [], [], []
+    ready = threading.Event()
+    th = threading.Thread(target=serve, kwargs=dict(opts=opts, max_connections=5, ready=ready, on_listen=ports.append,
+                                                    on_daemon=daemons.append, io_timeout=1.0,
+                                                    on_error=lambda t, e: errors.append((t, e))), daemon=True)
+    th.start()
+    assert ready.wait(30)
+    port = ports[0]
+    assert client_call(port, encode_init(False, [], "/ip4/127.0.0.1/tcp/5001", "m", M), 2) == b"\x00A"
+    agg = daemons[0].agg
+    stalled, g, h = (O.synth_bucket(M, 8, k) * (1.0 + k) for k in range(3))
+    extra = [O.synth_bucket(Ls[p], 9, p) for p in range(P)]
+    for e in extra:
+        e[-1] = 1.0                                   # a peer's count slot
+    payload = encode_update(stalled)
+    cut = 2 + 8 * ((Ls[0] - 1) + (Ls[1] - 1) // 2)    # all of partition 0's slice, half of partition 1's
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(payload[:cut])
+    time.sleep(0.2)                                   # the server is now in recv inside partition 1
+    t0 = time.perf_counter()
+    agg.Update(extra[1], 1)
+    agg.Update(extra[2], 2)
+    agg.sync()
+    inside = time.perf_counter() - t0
+    deadline = time.time() + 10
+    while not errors and time.time() < deadline:
+        time.sleep(0.05)
+    s.close()
+    assert inside < 0.5, f"direct folds waited {inside:.3f} s behind a stalled client"
+    assert len(errors) == 1 and errors[0][0] == 2 and isinstance(errors[0][1], OSError), errors
+    for peer in (g, h):
+        assert client_call(port, encode_update(peer), 2) == b"\x00A"
+    wire = client_call(port, encode_get(), 8 * M)
+    th.join(60)
+    parts = {k: O.organize_gradients(v, M, P) for k, v in (("s", stalled), ("g", g), ("h", h))}
+    firsts = [parts["s"][0], extra[1], extra[2]]
+    ws = [O.fold(O.fold(O.fold(np.zeros(Ls[p]), firsts[p]), parts["g"][p]), parts["h"][p]) + 0.0 for p in range(P)]
+    assert wire == O.be_encode_canonical(O.get_partitions(ws))
+    assert daemons[0].stats.get("failed") == 1 and daemons[0].rounds == 1

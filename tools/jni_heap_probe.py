@@ -27,7 +27,12 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT), str(ROOT / "ipls-java-api_amd"), str(ROOT / "tests")]
+_ring = os.environ.get("IPLS_JNI_RING_CHUNK")   # a sweep's value; test_jni pins its own on import
 import test_jni as TJ  # noqa: E402
+if _ring is None:
+    os.environ.pop("IPLS_JNI_RING_CHUNK", None)   # the shim's defaults (read at its first chunked native)
+else:
+    os.environ["IPLS_JNI_RING_CHUNK"] = _ring
 
 L = int(sys.argv[1]) if len(sys.argv) > 1 else 4194304
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
@@ -67,5 +72,5 @@ res["getPartitionsWire_pinned"] = timed(lambda: jvm.call("getPartitionsWire", h,
 jvm.call("close", h)
 print(json.dumps({"L": L, "bytes_per_call": 8 * L, "reps": reps,
                   "copy_threads": os.environ.get("IPLS_JNI_COPY_THREADS", "4 (default)"),
-                  "ring_chunk": os.environ.get("IPLS_JNI_RING_CHUNK", "524288 (default)"),
+                  "ring_chunk": os.environ.get("IPLS_JNI_RING_CHUNK", "default: 2097152 in, 524288 out"),
                   **{k: {"ms": round(v * 1e3, 3), "GBps": round(8 * L / v / 1e9, 2)} for k, v in res.items()}}))
