@@ -149,8 +149,10 @@ static jsize ring_chunk(int in) {
  * One memcpy thread moves 21-30 GB/s between pageable and pinned host memory
  * (tools/pinned_read_probe.hip, profiles/r05/h), half of what PCIe carries.
  * A chunk of at least PAR_MIN bytes is split over IPLS_JNI_COPY_THREADS
- * threads (default 4, the calling thread included): a pool of helpers created
- * on first use, woken per chunk.  One caller at a time uses the pool; a
+ * threads (default 6, the calling thread included: the ring -> heap copies
+ * of finalizePartition / getPartitions gain 1.5-2 GB/s from 4 to 6, the
+ * heap -> ring direction is flat, profiles/r06/d and h): a pool of helpers
+ * created on first use, woken per chunk.  One caller at a time uses the pool; a
  * caller that finds it busy (another Java thread in the same native) copies
  * alone. */
 #define PAR_MIN ((size_t)1 << 20)
@@ -189,7 +191,7 @@ static void *copy_helper(void *arg) {
 
 static void pool_init(void) {
     const char *e = getenv("IPLS_JNI_COPY_THREADS");
-    int t = e ? atoi(e) : 4;
+    int t = e ? atoi(e) : 6;
     if (t < 1) t = 1;
     if (t > PAR_MAX_THREADS) t = PAR_MAX_THREADS;
     int made = 0;

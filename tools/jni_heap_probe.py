@@ -71,6 +71,6 @@ res["getPartitions_heap_double[]"] = timed(lambda: jvm.call("getPartitions", h, 
 res["getPartitionsWire_pinned"] = timed(lambda: jvm.call("getPartitionsWire", h, pin_obj, 0, L64(8 * (L - 1))))
 jvm.call("close", h)
 print(json.dumps({"L": L, "bytes_per_call": 8 * L, "reps": reps,
-                  "copy_threads": os.environ.get("IPLS_JNI_COPY_THREADS", "4 (default)"),
+                  "copy_threads": os.environ.get("IPLS_JNI_COPY_THREADS", "6 (default)"),
                   "ring_chunk": os.environ.get("IPLS_JNI_RING_CHUNK", "default: 2097152 in, 524288 out"),
                   **{k: {"ms": round(v * 1e3, 3), "GBps": round(8 * L / v / 1e9, 2)} for k, v in res.items()}}))
