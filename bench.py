@@ -394,6 +394,30 @@ def f_stream_leg(ipls, torch, device: int, P: int = 16, L: int = 8388608, K: int
                     f"memory; Python caller"}
 
 
+def jni_heap_leg(L: int = 4194304, reps: int = 20) -> dict:
+    """The JNI shim's heap-array natives against its direct-buffer ones
+    (DESIGN.md §5.2): tools/jni_heap_probe.py in a child
+    process -- the shim and the fake JVM (tests/jni/fake_jvm.c) built with
+    gcc, driving the real library on this GPU, one partition of L doubles per
+    call.  GB/s = bytes of the Java-side array / wall time per call.  No JDK
+    exists here: the fake JVM's Get/Set<T>ArrayRegion and critical regions
+    are plain memcpy / pointer hand-outs, as HotSpot's are for primitive
+    arrays.  Never the value."""
+    import subprocess
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "jni_heap_probe.py"), str(L), str(reps)],
+                       capture_output=True, text=True, timeout=240,
+                       env={k: v for k, v in os.environ.items() if not k.startswith("IPLS_JNI_")})
+    if r.returncode != 0:
+        return {"error": r.stderr[-400:]}
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    keep = ("accumulate_heap_double[]", "accumulateDirect_pinned_BE", "finalize_heap_byte[]", "finalizeDirect_pinned",
+            "getPartitions_heap_double[]", "getPartitionsWire_pinned")
+    out = {k: d[k]["GBps"] for k in keep if k in d}
+    out.update(unit="GB/s", bucket_doubles=L, copy_threads=d.get("copy_threads"), ring_chunk=d.get("ring_chunk"),
+               source="tools/jni_heap_probe.py (shim + fake JVM, gcc-built in a child process)")
+    return out
+
+
 def middleware_socket_leg(ipls, torch, device: int, P: int = 16, Lv: int = 4194303, K: int = 32, D: int = 4,
                           verify: bool = True, warm_rounds: int = 3) -> dict:
     """The north_star's host boundary at model scale: the Middleware loopback
@@ -1931,6 +1955,8 @@ def main():
             out["host_inclusive"] = side(host_inclusive, ipls, ipls.Aggregator, L, K, args.e2e_reps, local)
         if world == 1 and not args.no_e2e and not args.no_middleware:
             out["middleware_socket"] = side(middleware_socket_leg, ipls, torch, local, verify=not args.no_verify)
+        if world == 1 and not args.no_e2e:
+            out["jni_heap"] = side(jni_heap_leg)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = side(cpu_baseline, L, K, args.cpu_passes)
         if world == 1 and not args.no_other_configs and args.config == "C" and not args.be:

@@ -1466,9 +1466,10 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
   if (!h || !source) return fail_nl(h, IPLS_E_INVAL, "null argument");
   if (chunk < 2 || (chunk & 1))
     return fail_nl(h, IPLS_E_INVAL, "chunk of %lld values: even and >= 2", (long long)chunk);
-  // geometry is fixed at open: validated without the lock
+  // geometry is fixed at open: validated without the lock (the target's
+  // offset is not read here: promote_future swaps AGG/FUT storage under it)
   if (p < 0 || p >= h->P) return fail_nl(h, IPLS_E_RANGE, "partition %d out of range [0,%d)", p, h->P);
-  if (target_off(h, p, target) < 0) return fail_nl(h, IPLS_E_INVAL, "bad target %d", target);
+  if (target < IPLS_TGT_AGG || target > IPLS_TGT_FUTURE) return fail_nl(h, IPLS_E_INVAL, "bad target %d", target);
   if (src_kind != IPLS_HOST_F64 && src_kind != IPLS_HOST_BE)
     return fail_nl(h, IPLS_E_INVAL, "a chunked fold takes HOST_F64 or HOST_BE values, not kind %d", src_kind);
   const int64_t L = h->len[p];
