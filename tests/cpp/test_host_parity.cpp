@@ -8,6 +8,7 @@
 // ETHModel (config A) is read from tests/golden/ethmodel.f64be.gz via zlib.
 #include <zlib.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -249,6 +250,58 @@ int main(int argc, char** argv) {
       CHECK(srv_err.empty(), ("server: " + srv_err).c_str());
       CHECK(server.stats().rounds == 2 && server.stats().updates == 6 && server.init().file_name == "ETHModel",
             "two rounds of three updates");
+    });
+
+    run("Middleware.main: a client that stalls in task 2 holds no GPU shard and times out", [&] {
+      // the server's chunk source is a blocking recv with
+      // no shard lock held and SO_RCVTIMEO on the connection.  A client
+      // sends task 2 and 100,000 of partition 0's 147,871 values, then stops:
+      // folds into partitions 0 and 1 of the same handle from this thread
+      // return at once, and after the timeout the task fails (the server
+      // throws, as Middleware.main ends on an exception) with partition 0
+      // holding only those folds -- its cut-short slice folded nothing.
+      const int64_t M = 443610;
+      PeerData opts = Middleware::parse_arguments({"-p", "0", "-pa", "3", "-mp", "1", "-n", "3", "-i", "0",
+                                                   "-training", "60", "-aggr", "0"});
+      MiddlewareServer server(opts, 73934, 500);
+      const int port = server.listen(0);
+      std::string srv_err;
+      std::atomic<bool> srv_done{false};
+      std::thread srv([&] {
+        try {
+          server.serve(2);
+        } catch (const std::exception& e) {
+          srv_err = e.what();
+        }
+        srv_done = true;
+      });
+      MiddlewareClient::init(port, (int32_t)M, "/ip4/127.0.0.1/tcp/5001", "m");
+      const int fd = MiddlewareClient::connect_to(port);
+      std::vector<uint8_t> part((size_t)2 + 100000 * 8, 0x3f);
+      part[0] = 0;
+      part[1] = 2;   // task 2
+      CHECK(send_all(fd, part.data(), part.size()), "partial task 2 sent");
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));   // the server now waits in recv
+      ipls_agg* h = server.ipls()->handle();
+      const int64_t L0 = ipls_oracle_partition_len(M, 3, 0), L1 = ipls_oracle_partition_len(M, 3, 1);
+      const auto g0 = synth(L0, 0, 91), g1 = synth(L1, 1, 92);
+      const auto t0 = std::chrono::steady_clock::now();
+      CHECK(ipls_agg_accumulate(h, 0, IPLS_TGT_AGG, g0.data(), L0, IPLS_HOST_F64) == 0 &&
+                ipls_agg_accumulate(h, 1, IPLS_TGT_AGG, g1.data(), L1, IPLS_HOST_F64) == 0 && ipls_agg_sync(h) == 0,
+            "folds beside the stalled task");
+      const double inside = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      CHECK(inside < 0.3, "the folds did not wait for the stalled client");
+      for (int i = 0; i < 100 && !srv_done; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      ::close(fd);
+      CHECK(srv_done.load(), "the server gave up on the stalled client");
+      srv.join();
+      CHECK(!srv_err.empty(), "task 2 failed with an exception");
+      std::vector<double> got((size_t)L0);
+      CHECK(ipls_agg_read(h, 0, IPLS_TGT_AGG, got.data(), L0, IPLS_HOST_F64) == 0, "read AGG[0]");
+      std::vector<double> want((size_t)L0);
+      const double* bp[1] = {g0.data()};
+      ipls_oracle_reduce(want.data(), bp, 1, L0, 1);
+      CHECK(bits_equal(got.data(), want.data(), (size_t)L0), "AGG[0] holds only the direct fold");
     });
 
     run("Updater file + frame arrivals, replicas, commit bytes", [&] {
