@@ -74,10 +74,11 @@ public final class NativeAggregator implements AutoCloseable {
 
     /** Updater._Update: client buckets -> TGT_AGG, replica partials -> TGT_REP.
      *  One library call for the whole bucket (ipls_agg_accumulate_chunked: the
-     *  array is copied out chunk by chunk inside it), so no other thread's call
-     *  on the partition lands between two of its chunks -- the whole-bucket fold
-     *  the Updater does under PeerData.mtx (Updater.java:72-149).  A failed copy
-     *  folds nothing. */
+     *  array is copied out chunk by chunk inside it, with no GPU lock held), and
+     *  the bucket takes effect as one unit once its last chunk has landed: no
+     *  other thread's fold lands between two of its chunks -- the whole-bucket
+     *  fold the Updater does under PeerData.mtx (Updater.java:72-149) -- and no
+     *  other thread waits for its heap copies.  A failed copy folds nothing. */
     public void update(double[] gradient, int p, boolean fromClients) {
         if (gradient != null) accumulate(handle, p, fromClients ? TGT_AGG : TGT_REP, gradient);
     }
@@ -190,8 +191,9 @@ public final class NativeAggregator implements AutoCloseable {
     }
 
     /** AggregatePartition (IPLS.java:1248-1274); returns the commit_update file bytes.
-     *  One library call (ipls_agg_finalize_chunked): no cache_partition or fold of
-     *  another thread lands between the sum and its bytes. */
+     *  One library call (ipls_agg_finalize_chunked): the bytes are a snapshot of
+     *  this call's sum, so a cache_partition or fold of another thread neither
+     *  tears them nor waits for their copy into the array. */
     public byte[] aggregatePartition(int p) {
         byte[] sum = new byte[8 * partitionLength(p)];
         finalizePartition(handle, p, sum);
