@@ -5,12 +5,15 @@
 // GPU, one HIP stream, one mutex.
 //
 // Device layout: one arena of doubles per handle holding, for
-// every partition p, three arrays of L_p doubles -- AGG (Aggregated_Gradients,
-// PeerData.java:144), REP (Replicas_Gradients, :137) and W (Weights, :149,
-// which IPLS.java:1141 aliases with Weight_Address, :189) -- each starting on
-// a 256-byte boundary.  Device-side tables (partition descriptors + bucket
-// pointers) are uploaded through a small pinned ring and cached, so a
-// repeated reduce over resident buckets is one kernel launch and nothing else.
+// every partition p, four arrays of L_p doubles -- AGG (Aggregated_Gradients,
+// PeerData.java:144), REP (Replicas_Gradients, :137), FUT (Aggregated_
+// Gradients_from_future) and W (Weights, :149, which IPLS.java:1141 aliases
+// with Weight_Address, :189) -- each starting on a 256-byte boundary.
+// Device-side tables (partition descriptors + bucket pointers) are uploaded
+// through a small pinned ring and cached, so a repeated reduce over resident
+// buckets is one kernel launch and nothing else.  The chunked calls stage
+// through a stage each (struct ipls_stage, pooled per engine) and take the
+// engine lock only for their fold or snapshot.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -65,12 +68,16 @@ struct PinnedSlot {
 // is `pending` (its event recorded after that copy); `free_pending` says a
 // kernel on the shard stream may still read `d` (recorded after it).
 struct ipls_stage {
-  hipStream_t copy = nullptr;
+  // chunk k crosses PCIe on copy[k % n_copy]: with two streams the DMA setup
+  // of chunk k + 1 overlaps the transfer of chunk k (IPLS_STAGE_STREAMS=1
+  // gives one stream, the A/B of profiles/r06)
+  hipStream_t copy[2] = {};
+  int n_copy = 0;
   PinnedSlot slot[2];
   void* d = nullptr;
   size_t d_cap = 0;
-  hipEvent_t landed = nullptr;    // copy stream -> shard stream: every chunk is in `d`
-  hipEvent_t ready = nullptr;     // shard stream -> copy stream: the snapshot is in `d`
+  hipEvent_t landed[2] = {};      // copy streams -> shard stream: every chunk is in `d`
+  hipEvent_t ready = nullptr;     // shard stream -> copy streams: the snapshot is in `d`
   hipEvent_t free_ev = nullptr;   // shard stream: the fold that read `d` has run
   bool free_pending = false;
 };
@@ -319,14 +326,19 @@ int stage_acquire(ipls_dev* h, size_t dev_bytes, size_t slot_bytes, ipls_stage**
                    hipGetErrorString(e));
   };
   int rc = IPLS_OK;
-  if (!st->copy) rc = try_hip(hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking), "hipStreamCreate");
-  for (hipEvent_t* e : {&st->landed, &st->ready, &st->free_ev})
+  if (!st->n_copy) {
+    const char* e = std::getenv("IPLS_STAGE_STREAMS");
+    st->n_copy = (e && std::atoi(e) == 1) ? 1 : 2;
+  }
+  for (int i = 0; i < st->n_copy && !rc; ++i)
+    if (!st->copy[i]) rc = try_hip(hipStreamCreateWithFlags(&st->copy[i], hipStreamNonBlocking), "hipStreamCreate");
+  for (hipEvent_t* e : {&st->landed[0], &st->landed[1], &st->ready, &st->free_ev})
     if (!rc && !*e) rc = try_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
   if (!rc && st->d_cap < dev_bytes) {
     if (st->d) {
       // the fold that last read `d` and every copy of the stage are done before it is freed
       if (st->free_pending) rc = try_hip(hipEventSynchronize(st->free_ev), "hipEventSynchronize");
-      if (!rc) rc = try_hip(hipStreamSynchronize(st->copy), "hipStreamSynchronize");
+      for (int i = 0; i < st->n_copy && !rc; ++i) rc = try_hip(hipStreamSynchronize(st->copy[i]), "hipStreamSynchronize");
       if (!rc) rc = try_hip(hipFree(st->d), "hipFree");
       if (!rc) {
         st->d = nullptr;
@@ -1101,16 +1113,17 @@ int dev_close(ipls_dev* h) {
     if (s.ev) hipEventDestroy(s.ev);
   }
   for (ipls_stage* st : h->stage_all) {
-    if (st->copy) {
-      hipStreamSynchronize(st->copy);
-      hipStreamDestroy(st->copy);
-    }
+    for (hipStream_t cs : st->copy)
+      if (cs) {
+        hipStreamSynchronize(cs);
+        hipStreamDestroy(cs);
+      }
     for (auto& s : st->slot) {
       if (s.host) hipHostFree(s.host);
       if (s.ev) hipEventDestroy(s.ev);
     }
     if (st->d) hipFree(st->d);
-    for (hipEvent_t e : {st->landed, st->ready, st->free_ev})
+    for (hipEvent_t e : {st->landed[0], st->landed[1], st->ready, st->free_ev})
       if (e) hipEventDestroy(e);
     delete st;
   }
@@ -1489,7 +1502,8 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
     }
   };
   // the fold that last read the device buffer runs before these copies overwrite it
-  if (st->free_pending) try_hip(hipStreamWaitEvent(st->copy, st->free_ev, 0), "hipStreamWaitEvent");
+  for (int i = 0; i < st->n_copy && st->free_pending; ++i)
+    try_hip(hipStreamWaitEvent(st->copy[i], st->free_ev, 0), "hipStreamWaitEvent");
   for (int64_t k = 0, off = 0; off < L && !rc; ++k, off += c) {
     PinnedSlot& sl = st->slot[k & 1];
     if ((rc = stage_slot_free(h, sl))) break;   // the copy of chunk k - 2 still reads this slot
@@ -1498,14 +1512,15 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
       rc = fail_nl(h, IPLS_E_INVAL, "the chunk source stopped at offset %lld: nothing folded", (long long)off);
       break;
     }
-    try_hip(hipMemcpyAsync(d_in + off, sl.host, (size_t)len * 8, hipMemcpyHostToDevice, st->copy), "hipMemcpyAsync");
-    try_hip(hipEventRecord(sl.ev, st->copy), "hipEventRecord");
+    hipStream_t cs = st->copy[k % st->n_copy];
+    try_hip(hipMemcpyAsync(d_in + off, sl.host, (size_t)len * 8, hipMemcpyHostToDevice, cs), "hipMemcpyAsync");
+    try_hip(hipEventRecord(sl.ev, cs), "hipEventRecord");
     if (!rc) sl.pending = true;
   }
-  if (!rc) try_hip(hipEventRecord(st->landed, st->copy), "hipEventRecord");
+  for (int i = 0; i < st->n_copy && !rc; ++i) try_hip(hipEventRecord(st->landed[i], st->copy[i]), "hipEventRecord");
   if (rc) {
     // nothing folded; the copies already queued finish before the stage is reused
-    (void)hipStreamSynchronize(st->copy);
+    for (int i = 0; i < st->n_copy; ++i) (void)hipStreamSynchronize(st->copy[i]);
     (void)hipGetLastError();
     for (auto& sl : st->slot) sl.pending = false;
     stage_release(h, st);
@@ -1514,8 +1529,8 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
   {
     std::lock_guard<std::mutex> lk(h->mu);
     rc = flush_pending(h);   // earlier queued device buckets fold first
-    if (!rc) {
-      const hipError_t e = hipStreamWaitEvent(h->stream, st->landed, 0);
+    for (int i = 0; i < st->n_copy && !rc; ++i) {
+      const hipError_t e = hipStreamWaitEvent(h->stream, st->landed[i], 0);
       if (e != hipSuccess) {
         (void)hipGetLastError();
         rc = fail(h, IPLS_E_DEVICE, "hipStreamWaitEvent failed: %s", hipGetErrorString(e));
@@ -1533,7 +1548,7 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
     }
   }
   if (rc) {   // the shard stream may not have waited for the copies: drain them
-    (void)hipStreamSynchronize(st->copy);
+    for (int i = 0; i < st->n_copy; ++i) (void)hipStreamSynchronize(st->copy[i]);
     (void)hipGetLastError();
   }
   stage_release(h, st);
@@ -1555,13 +1570,14 @@ static int stage_deliver(ipls_dev* h, ipls_stage* st, int64_t n, int64_t c, int6
       rc = fail_nl(h, IPLS_E_DEVICE, "%s failed: %s", what, hipGetErrorString(e));
     }
   };
-  try_hip(hipStreamWaitEvent(st->copy, st->ready, 0), "hipStreamWaitEvent");
+  for (int i = 0; i < st->n_copy; ++i) try_hip(hipStreamWaitEvent(st->copy[i], st->ready, 0), "hipStreamWaitEvent");
   const int64_t K = n > 0 ? (n + c - 1) / c : 0;
   auto issue = [&](int64_t k) {
     PinnedSlot& sl = st->slot[k & 1];
     const int64_t off = k * c, len = std::min(c, n - off);
-    try_hip(hipMemcpyAsync(sl.host, d + off, (size_t)len * 8, hipMemcpyDeviceToHost, st->copy), "hipMemcpyAsync");
-    try_hip(hipEventRecord(sl.ev, st->copy), "hipEventRecord");
+    hipStream_t cs = st->copy[k % st->n_copy];
+    try_hip(hipMemcpyAsync(sl.host, d + off, (size_t)len * 8, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
+    try_hip(hipEventRecord(sl.ev, cs), "hipEventRecord");
   };
   if (K > 0) issue(0);
   for (int64_t k = 0; k < K && !rc; ++k) {
@@ -1578,7 +1594,7 @@ static int stage_deliver(ipls_dev* h, ipls_stage* st, int64_t n, int64_t c, int6
   // every copy of this call is done before the stage can be reused (on the
   // success path they already are: each chunk's event was waited for)
   if (rc) {
-    (void)hipStreamSynchronize(st->copy);
+    for (int i = 0; i < st->n_copy; ++i) (void)hipStreamSynchronize(st->copy[i]);
     (void)hipGetLastError();
   }
   for (auto& sl : st->slot) sl.pending = false;
