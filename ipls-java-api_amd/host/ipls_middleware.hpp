@@ -116,7 +116,7 @@ class MiddlewareServer {
     int32_t model_size = 0;
   };
   struct Stats {
-    int64_t updates = 0, replies = 0, rounds = 0;
+    int64_t updates = 0, replies = 0, rounds = 0, failed = 0;
     double update_s = 0, reply_s = 0;   // inside the task handlers, socket reads/writes included
   };
 
@@ -157,7 +157,13 @@ class MiddlewareServer {
   // The library holds no shard lock while a task's socket is read or
   // written (the chunked calls lock for the fold / the snapshot only), so
   // other threads' calls on the same IPLS instance never wait for a client.
-  void serve(int max_connections = -1) {
+  // on_error: when given, a task that fails calls on_error(task, exception)
+  // and the server goes on with the next connection instead of throwing (what
+  // ipls.middleware.serve does; a server of many peers should not be ended
+  // by one bad client).  task is 0 when the connection failed before its
+  // task number arrived.
+  using OnError = std::function<void(int16_t task, const JavaException& e)>;
+  void serve(int max_connections = -1, const OnError& on_error = nullptr) {
     for (int served = 0; max_connections < 0 || served < max_connections; ++served) {
       const int fd = ::accept(lfd_, nullptr, nullptr);
       if (fd < 0) {
@@ -168,11 +174,17 @@ class MiddlewareServer {
       big_socket_buffers(fd);
       io_timeout(fd, io_timeout_ms_);
       int16_t task = 0;
-      if (!read_i16(fd, &task)) throw BufferUnderflowException(IPLS_E_FORMAT, "EOFException: no task");
-      if (task == 1) task1(fd);
-      else if (task == 2) task2(fd);
-      else if (task == 3) task3(fd);
-      // else: Ipls.terminate (the reference does nothing)
+      try {
+        if (!read_i16(fd, &task)) throw BufferUnderflowException(IPLS_E_FORMAT, "EOFException: no task");
+        if (task == 1) task1(fd);
+        else if (task == 2) task2(fd);
+        else if (task == 3) task3(fd);
+        // else: Ipls.terminate (the reference does nothing)
+      } catch (const JavaException& e) {
+        if (!on_error) throw;
+        ++stats_.failed;
+        on_error(task, e);
+      }
     }
   }
 

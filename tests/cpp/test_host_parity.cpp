@@ -304,6 +304,39 @@ int main(int argc, char** argv) {
       CHECK(bits_equal(got.data(), want.data(), (size_t)L0), "AGG[0] holds only the direct fold");
     });
 
+    run("Middleware.main with on_error: a failed task ends its connection only", [&] {
+      // the same stalled client against serve(n, on_error): the server reports
+      // the task and answers the next client's task 3 from the same instance
+      const int64_t M = 443610;
+      PeerData opts = Middleware::parse_arguments({"-p", "0", "-pa", "3", "-mp", "1", "-n", "3", "-i", "0",
+                                                   "-training", "60", "-aggr", "0"});
+      MiddlewareServer server(opts, 73934, 300);
+      const int port = server.listen(0);
+      std::vector<int> failed_tasks;
+      std::string srv_err;
+      std::thread srv([&] {
+        try {
+          server.serve(3, [&](int16_t task, const JavaException&) { failed_tasks.push_back(task); });
+        } catch (const std::exception& e) {
+          srv_err = e.what();
+        }
+      });
+      MiddlewareClient::init(port, (int32_t)M, "/ip4/127.0.0.1/tcp/5001", "m");
+      const int fd = MiddlewareClient::connect_to(port);
+      const uint8_t head[2] = {0, 2};
+      CHECK(send_all(fd, head, 2), "task 2 header sent");   // then nothing: the recv times out
+      std::vector<uint8_t> got((size_t)M * 8, 1);
+      MiddlewareClient::get(port, got.data(), got.size());   // task 3 on the next connection
+      ::close(fd);
+      srv.join();
+      CHECK(srv_err.empty(), ("server: " + srv_err).c_str());
+      CHECK(failed_tasks == std::vector<int>{2} && server.stats().failed == 1 && server.stats().replies == 1,
+            "one failed task 2, then the reply");
+      bool zeros = true;   // nothing folded, no round closed: the initial (zero) model comes back
+      for (uint8_t b : got) zeros = zeros && b == 0;
+      CHECK(zeros, "the reply is the untouched model");
+    });
+
     run("Updater file + frame arrivals, replicas, commit bytes", [&] {
       const int64_t L = 70001;
       PeerData pd;
