@@ -333,3 +333,53 @@ def test_half_shape_ragged_model_geometry(ipls, O, start):
     agg.close()
     del t
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_chunked_calls_at_production_partitions(ipls, O, devices):
+    """The chunked calls (round 6: per-call stages, two copy streams, chunk k
+    on stream k mod 2) at config C's partition length, L = 4,194,304, with the
+    chunk sizes the JNI shim and the Middleware servers use (2^19 and 2^21
+    values) and one that leaves a short last chunk: three arrivals into AGG
+    and one into REP of partition 1 through accumulate_chunked (big-endian and
+    native), then finalize_chunked's commit_update bytes and
+    get_partitions_wire_chunked's stream over both partitions -- bit for bit
+    against the oracle (Updater.java:115-117, IPLS.java:1248-1274, 1159-1174,
+    Middleware.java:164-170)."""
+    import ctypes
+    from ipls import _native as N
+    L, P = 4_194_304, 2
+    agg = ipls.Aggregator(n_partitions=P, bucket_len=L, devices=devices)
+    lib, h = agg._lib, agg._h
+    gs = [O.synth_bucket(L, 1, 700 + k) * (1.0 + k) for k in range(4)]
+    for g in gs:
+        g[-1] = 1.0                                    # each arrival's count slot
+    for k, (g, chunk, be, tgt) in enumerate(((gs[0], 1 << 19, True, N.TGT_AGG), (gs[1], 1 << 21, False, N.TGT_AGG),
+                                             (gs[2], 1_000_002, True, N.TGT_AGG), (gs[3], 1 << 19, True, N.TGT_REP))):
+        raw = O.be_encode(g) if be else g.tobytes()
+
+        @N.CHUNK_SOURCE
+        def src(ctx, dst, off, n, raw=raw):
+            ctypes.memmove(dst, ctypes.c_char_p(raw[8 * off:8 * (off + n)]), 8 * n)
+            return 0
+        assert lib.ipls_agg_accumulate_chunked(h, 1, tgt, L, N.HOST_BE if be else N.HOST_F64, chunk, src, None) == 0
+    agg_want = O.fold(O.fold(O.fold(np.zeros(L), gs[0]), gs[1]), gs[2])
+    assert_bits_equal(agg.read(1, N.TGT_AGG), agg_want, "AGG[1]")
+    w = agg_want + O.fold(np.zeros(L), gs[3])
+    out = bytearray(8 * L)
+
+    @N.CHUNK_SINK
+    def sink(ctx, vals, off, n):
+        out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+        return 0
+    assert lib.ipls_agg_finalize_chunked(h, 1, N.HOST_BE, 1 << 19, sink, None) == 0
+    assert bytes(out) == O.be_encode(w), "commit_update bytes of W[1]"
+    got = bytearray()
+
+    @N.CHUNK_SINK
+    def wsink(ctx, vals, off, n):
+        got.extend(ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n))
+        return 0
+    assert lib.ipls_agg_get_partitions_wire_chunked(h, 1 << 19, wsink, None) == 0
+    assert bytes(got) == O.be_encode_canonical(O.get_partitions([np.zeros(L), w])), "task-3 stream"
+    agg.close()
