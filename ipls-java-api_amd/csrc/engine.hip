@@ -1570,6 +1570,10 @@ static int stage_deliver(ipls_dev* h, ipls_stage* st, int64_t n, int64_t c, int6
       rc = fail_nl(h, IPLS_E_DEVICE, "%s failed: %s", what, hipGetErrorString(e));
     }
   };
+  // a previous call's H2D may still read a slot (accumulate_chunked does not
+  // wait for its copies on the host): the D2H into it waits for that copy
+  for (auto& sl : st->slot)
+    if (!rc) rc = stage_slot_free(h, sl);
   for (int i = 0; i < st->n_copy; ++i) try_hip(hipStreamWaitEvent(st->copy[i], st->ready, 0), "hipStreamWaitEvent");
   const int64_t K = n > 0 ? (n + c - 1) / c : 0;
   auto issue = [&](int64_t k) {
