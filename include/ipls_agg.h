@@ -419,7 +419,7 @@ int ipls_agg_finalize(ipls_agg *h, int p, void *sum_out, int sum_kind, double *a
 
 /* ipls_agg_finalize of one partition with its sum handed to a sink chunk by
  * chunk, as ONE call: AggregatePartition (IPLS.java:1248-1274), then W[p]
- * comes back through a pinned two-slot ring in chunks of `chunk` values
+ * comes back through a pinned ring (three slots) in chunks of `chunk` values
  * (even, >= 2), sink(ctx, values, offset, n) on the calling thread for
  * consecutive ranges of [0, L_p), so the sink's copy of one chunk overlaps
  * the transfer of the next.  values: n 8-byte values, doubles (HOST_F64) or
@@ -468,7 +468,7 @@ int ipls_agg_get_partitions(ipls_agg *h, void *out, int64_t n, int out_kind);
  * model order: the divide runs once on the GPU into staging of this call's
  * own -- every shard's, each under its shard lock for that launch only,
  * before any chunk is delivered, so the whole model is one snapshot -- then
- * each chunk comes back through a pinned two-slot ring with no lock held, so
+ * each chunk comes back through a pinned ring (three slots) with no lock held, so
  * the sink's copy of chunk k overlaps the transfer of chunk k + 1 (the JNI
  * getPartitions(double[]) copies each chunk into the Java array with
  * SetDoubleArrayRegion).  `values` is valid only during the sink call.  A

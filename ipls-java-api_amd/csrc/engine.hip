@@ -46,6 +46,7 @@ thread_local std::string g_tls_err;
 
 constexpr int64_t kAlignElems = 32;  // 256 B
 constexpr int kRingSlots = 4;
+constexpr int kStageSlots = 3;   // pinned slots of a chunked call's ring (IPLS_STAGE_SLOTS overrides)
 
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
@@ -61,8 +62,8 @@ struct PinnedSlot {
 // The staging of one chunked call (accumulate / finalize / get_partitions
 // _chunked), owned by that call alone from acquire to release, so the
 // caller's source or sink -- a socket recv/send, a JNI array copy -- runs
-// with no engine lock held.  A pinned two-slot host ring,
-// a device buffer for the whole bucket (or snapshot) and a copy stream of its
+// with no engine lock held.  A pinned host ring,
+// a device buffer for the whole bucket (or snapshot) and two copy streams of its
 // own.  Stages are pooled per shard and freed only at close.
 // Invariants at release: every pinned slot whose copy may still be in flight
 // is `pending` (its event recorded after that copy); `free_pending` says a
@@ -73,7 +74,12 @@ struct ipls_stage {
   // gives one stream, the A/B of profiles/r06)
   hipStream_t copy[2] = {};
   int n_copy = 0;
-  PinnedSlot slot[2];
+  // the pinned host ring: chunk k in slot k % n_slot, so the copy engine can
+  // run up to n_slot - 1 chunks ahead of a caller's slow source or sink
+  // (IPLS_STAGE_SLOTS, 2..4)
+  static constexpr int kMaxSlots = 4;
+  PinnedSlot slot[kMaxSlots];
+  int n_slot = 0;
   void* d = nullptr;
   size_t d_cap = 0;
   hipEvent_t landed[2] = {};      // copy streams -> shard stream: every chunk is in `d`
@@ -329,6 +335,8 @@ int stage_acquire(ipls_dev* h, size_t dev_bytes, size_t slot_bytes, ipls_stage**
   if (!st->n_copy) {
     const char* e = std::getenv("IPLS_STAGE_STREAMS");
     st->n_copy = (e && std::atoi(e) == 1) ? 1 : 2;
+    const char* sl = std::getenv("IPLS_STAGE_SLOTS");
+    st->n_slot = sl ? std::max(2, std::min(ipls_stage::kMaxSlots, std::atoi(sl))) : kStageSlots;
   }
   for (int i = 0; i < st->n_copy && !rc; ++i)
     if (!st->copy[i]) rc = try_hip(hipStreamCreateWithFlags(&st->copy[i], hipStreamNonBlocking), "hipStreamCreate");
@@ -350,7 +358,8 @@ int stage_acquire(ipls_dev* h, size_t dev_bytes, size_t slot_bytes, ipls_stage**
     if (!rc) rc = try_hip(hipMalloc(&st->d, cap), "hipMalloc");
     if (!rc) st->d_cap = cap;
   }
-  for (auto& s : st->slot) {
+  for (int i = 0; i < st->n_slot; ++i) {
+    PinnedSlot& s = st->slot[i];
     if (rc) break;
     if (s.cap < slot_bytes) {
       if (s.pending) rc = try_hip(hipEventSynchronize(s.ev), "hipEventSynchronize");
@@ -383,7 +392,7 @@ void stage_release(ipls_dev* h, ipls_stage* st) {
   h->stage_idle.push_back(st);
 }
 
-// The host may write pinned slot k & 1 again: the copy that last read it is done.
+// The host may write this pinned slot again: the copy that last read it is done.
 int stage_slot_free(ipls_dev* h, PinnedSlot& sl) {
   if (sl.pending) {
     HIP_TRY_NL(h, hipEventSynchronize(sl.ev));
@@ -1505,8 +1514,8 @@ int dev_accumulate_chunked(ipls_dev* h, int p, int target, int64_t n, int src_ki
   for (int i = 0; i < st->n_copy && st->free_pending; ++i)
     try_hip(hipStreamWaitEvent(st->copy[i], st->free_ev, 0), "hipStreamWaitEvent");
   for (int64_t k = 0, off = 0; off < L && !rc; ++k, off += c) {
-    PinnedSlot& sl = st->slot[k & 1];
-    if ((rc = stage_slot_free(h, sl))) break;   // the copy of chunk k - 2 still reads this slot
+    PinnedSlot& sl = st->slot[k % st->n_slot];
+    if ((rc = stage_slot_free(h, sl))) break;   // the copy of chunk k - n_slot still reads this slot
     const int64_t len = std::min(c, L - off);
     if (source(ctx, sl.host, off, len) != 0) {
       rc = fail_nl(h, IPLS_E_INVAL, "the chunk source stopped at offset %lld: nothing folded", (long long)off);
@@ -1576,24 +1585,27 @@ static int stage_deliver(ipls_dev* h, ipls_stage* st, int64_t n, int64_t c, int6
     if (!rc) rc = stage_slot_free(h, sl);
   for (int i = 0; i < st->n_copy; ++i) try_hip(hipStreamWaitEvent(st->copy[i], st->ready, 0), "hipStreamWaitEvent");
   const int64_t K = n > 0 ? (n + c - 1) / c : 0;
-  auto issue = [&](int64_t k) {
-    PinnedSlot& sl = st->slot[k & 1];
+  const int S = st->n_slot;
+  int64_t issued = 0;
+  auto issue = [&]() {   // the next chunk, into slot issued % S (its previous chunk's sink has returned)
+    const int64_t k = issued++;
+    PinnedSlot& sl = st->slot[k % S];
     const int64_t off = k * c, len = std::min(c, n - off);
     hipStream_t cs = st->copy[k % st->n_copy];
     try_hip(hipMemcpyAsync(sl.host, d + off, (size_t)len * 8, hipMemcpyDeviceToHost, cs), "hipMemcpyAsync");
     try_hip(hipEventRecord(sl.ev, cs), "hipEventRecord");
   };
-  if (K > 0) issue(0);
+  while (issued < K && issued < S && !rc) issue();   // the ring's first fill
   for (int64_t k = 0; k < K && !rc; ++k) {
-    if (k + 1 < K) issue(k + 1);   // into the slot chunk k - 1 used, whose sink has returned
-    if (rc) break;
-    PinnedSlot& sl = st->slot[k & 1];
+    PinnedSlot& sl = st->slot[k % S];
     try_hip(hipEventSynchronize(sl.ev), "hipEventSynchronize");
     if (rc) break;
     const int64_t off = k * c, len = std::min(c, n - off);
     if (sink(ctx, (const double*)sl.host, base + off, len) != 0)
       rc = fail_nl(h, IPLS_E_INVAL, "the chunk sink stopped the transfer at offset %lld%s", (long long)(base + off),
                    stopped_note);
+    else if (issued < K)
+      issue();   // into the slot just consumed
   }
   // every copy of this call is done before the stage can be reused (on the
   // success path they already are: each chunk's event was waited for)
@@ -1913,7 +1925,7 @@ int dev_finalize(ipls_dev* h, int p, void* sum_out, int sum_kind, double* avg_ou
 // engine lock: W = AGG + REP and a snapshot of W (or of its big-endian bytes)
 // into this call's own staging -- one kernel or copy on the shard stream.
 // The lock is then released and the snapshot goes to the sink through the
-// pinned two-slot ring, chunk k + 1 in flight while sink() copies chunk k.
+// pinned ring, chunks k + 1 .. k + 2 in flight while sink() copies chunk k.
 // The bytes are the W of this call's AggregatePartition whatever another
 // caller's set_weights / fold / finalize does meanwhile (the per-range reads
 // of dev_read_range cannot promise that), and a slow sink (a socket send)
@@ -2338,7 +2350,7 @@ int dev_get_partitions(ipls_dev* h, void* out, int64_t n, int out_kind) {
 //    own staging (wire: the same values as Middleware's task-3 writeDouble
 //    stream -- big-endian, NaN canonical: k_divide's OUT_BE form);
 //  * deliver, with no lock held: chunk k + 1 is copied into one slot of the
-//    stage's pinned two-slot ring while sink() consumes chunk k from the other,
+//    stage's pinned ring while sink() consumes chunk k from another slot,
 //    on the calling thread (the JNI shim's sink is SetDoubleArrayRegion, the
 //    Middleware's a socket send).  sink gets flat model offsets (this engine's
 //    segment starts at flat_base); a non-zero return stops the transfer

@@ -15,7 +15,8 @@ One partition of L doubles (one bucket per call, as the Updater folds):
   getPartitionsWire(ByteBuffer)-- the same as Middleware's big-endian stream into
                                   a pinned direct buffer
 GB/s = bytes of the Java-side array / wall time per call (median of reps).
-Usage: jni_heap_probe.py [L] [reps]"""
+Usage: jni_heap_probe.py [L] [reps] [--ab-slots=2,3,4]
+(--ab-slots: the stage ring depth, one handle per value, interleaved in one process)"""
 import ctypes
 import json
 import os
@@ -34,8 +35,10 @@ if _ring is None:
 else:
     os.environ["IPLS_JNI_RING_CHUNK"] = _ring
 
-L = int(sys.argv[1]) if len(sys.argv) > 1 else 4194304
-reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+_pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+L = int(_pos[0]) if len(_pos) > 0 else 4194304
+reps = int(_pos[1]) if len(_pos) > 1 else 20
+_ab = next((a.split("=", 1)[1].split(",") for a in sys.argv[1:] if a.startswith("--ab-slots=")), None)
 jvm = TJ.JVM()
 L64 = ctypes.c_int64
 # one partition of L doubles: model_size = L - 1 (the chunk rule gives L_0 = M + 1)
@@ -60,6 +63,39 @@ def timed(fn):
         ts.append(time.perf_counter() - t0)
     return float(np.median(ts))
 
+
+if _ab:
+    # the stage ring depth, A/B in ONE process: a handle per IPLS_STAGE_SLOTS
+    # value (a stage reads it when it is made, at the handle's first chunked
+    # call), the heap natives timed rep by rep in turn on each
+    model = jvm.doubles(np.zeros(L - 1))
+    hs = {}
+    for v in _ab:
+        os.environ["IPLS_STAGE_SLOTS"] = v
+        hv, exc = jvm.call("open", L64(L - 1), 1, 3, 0, 0, 0, res=ctypes.c_int64)
+        assert exc is None and hv
+        hs[v] = L64(hv)
+        for name, args in (("accumulate", (hs[v], 0, 0, arr)), ("finalizePartition", (hs[v], 0, out_heap)),
+                           ("getPartitions", (hs[v], model))):
+            assert jvm.call(name, *args)[1] is None
+    # accumulate(double[]) is not timed here: it returns once its fold is
+    # queued, so one handle's copies would run under the other's timed call
+    ops = {"finalize_heap_byte[]": lambda hv: jvm.call("finalizePartition", hv, 0, out_heap),
+           "getPartitions_heap_double[]": lambda hv: jvm.call("getPartitions", hv, model)}
+    out = {"L": L, "reps": reps, "mode": "ab-slots, interleaved in one process"}
+    for name, fn in ops.items():
+        ts = {v: [] for v in _ab}
+        for _ in range(reps):
+            for v in _ab:
+                t0 = time.perf_counter()
+                fn(hs[v])
+                ts[v].append(time.perf_counter() - t0)
+        out[name] = {f"slots_{v}": round(8 * L / float(np.median(t)) / 1e9, 2) for v, t in ts.items()}
+    for hv in hs.values():
+        jvm.call("close", hv)
+    jvm.call("close", h)
+    print(json.dumps(out))
+    sys.exit(0)
 
 res = {}
 res["accumulate_heap_double[]"] = timed(lambda: jvm.call("accumulate", h, 0, 0, arr))
