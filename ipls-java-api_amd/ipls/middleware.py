@@ -42,6 +42,12 @@ class MissingOptionError(SystemExit):
     pass
 
 
+class MiddlewareTaskError(RuntimeError):
+    """A task the server cannot run: task 2 or 3 before any task 1 (Java's
+    Middleware dereferences a null ipls_daemon there, Middleware.java:243-246,
+    254, and exits)."""
+
+
 @dataclass
 class Options:
     """Middleware.parse_arguments (Middleware.java:26-110)."""
@@ -320,12 +326,14 @@ def serve(opts: Options, max_connections: int | None = None, device: int = 0, in
                         if on_daemon is not None:
                             on_daemon(daemon)
                         conn.sendall(ACK)
+                    elif task in (2, 3) and daemon is None:
+                        raise MiddlewareTaskError(f"task {task} before task 1")
                     elif task == 2:
                         daemon.update_from_socket(conn)
                         conn.sendall(ACK)
                     elif task == 3:
                         daemon.reply_to_socket(conn)
-                except (OSError, EOFError, IplsError) as e:   # socket.timeout is an OSError
+                except (OSError, EOFError, IplsError, MiddlewareTaskError) as e:   # socket.timeout is an OSError
                     if daemon is not None:
                         daemon.stats["failed"] = daemon.stats.get("failed", 0) + 1
                     if on_error is not None:
