@@ -1177,6 +1177,53 @@ def test_chunked_calls_tiny_partitions_and_wire(ipls, O, devices):
         agg.close()
 
 
+@pytest.mark.parametrize("case", ["szero", "cancel", "special"])
+def test_chunked_calls_golden_edge_values(ipls, O, golden, case):
+    """The golden edge buckets (signed zeros, cancellation order, NaN / inf /
+    -0.0 / subnormals, the count slot among them) through the chunked calls
+    with two-value chunks, so neighbouring special values cross PCIe in
+    different chunks, ring slots and copy streams, alternately big-endian
+    and native: AGG equals the golden fold from +0.0 bit for bit, the
+    commit_update bytes are W's (AggregatePartition, IPLS.java:1248-1274),
+    and the task-3 stream is the oracle's writeDouble bytes of the divide
+    (NaN canonical, Middleware.java:164-170)."""
+    from ipls import _native as N
+    bufs = golden[f"{case}_bufs"]
+    L = bufs.shape[1]
+    agg = ipls.Aggregator(n_partitions=1, bucket_len=L)
+    lib, h = agg._lib, agg._h
+    for k, g in enumerate(bufs):
+        be = k % 2 == 0
+        raw = O.be_encode(g) if be else np.ascontiguousarray(g).tobytes()
+
+        @N.CHUNK_SOURCE
+        def src(ctx, dst, off, n, raw=raw):
+            ctypes.memmove(dst, ctypes.c_char_p(raw[8 * off:8 * (off + n)]), 8 * n)
+            return 0
+        assert lib.ipls_agg_accumulate_chunked(h, 0, N.TGT_AGG, L, N.HOST_BE if be else N.HOST_F64, 2, src,
+                                               None) == 0
+    assert_bits_equal(agg.read(0, N.TGT_AGG), golden[f"{case}_zero"], f"{case}: AGG")
+    W = golden[f"{case}_zero"] + 0.0
+    out = bytearray(8 * L)
+
+    @N.CHUNK_SINK
+    def sink(ctx, vals, off, n):
+        out[8 * off:8 * (off + n)] = ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n)
+        return 0
+    assert lib.ipls_agg_finalize_chunked(h, 0, N.HOST_BE, 2, sink, None) == 0
+    # putDouble keeps a NaN's payload, which Java does not specify: compared as values, NaN meeting NaN
+    assert_bits_equal(np.frombuffer(bytes(out), dtype=">f8").astype(np.float64), W, f"{case}: commit_update bytes")
+    got = bytearray()
+
+    @N.CHUNK_SINK
+    def wsink(ctx, vals, off, n):
+        got.extend(ctypes.string_at(ctypes.cast(vals, ctypes.c_void_p), 8 * n))
+        return 0
+    assert lib.ipls_agg_get_partitions_wire_chunked(h, 2, wsink, None) == 0
+    assert bytes(got) == O.be_encode_canonical(O.get_partitions([W])), f"{case}: task-3 stream"
+    agg.close()
+
+
 @pytest.mark.parametrize("devices", [None, [0, 0]])
 def test_accumulate_chunked_threads_serialise(ipls, O, devices):
     """Four threads fold four buckets into the same partition, each as one
